@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mrays/s @1920x1080x1spp + BVH-build Mprims/s on the
+1M-triangle synthetic soup (BASELINE.json configs[2]), 1..N GPUs.
+
+One STEP = one frame of the hot path on inputs already resident in HBM:
+  rt_bvh_build (K0..K6, replicated on every rank) -> trace this rank's image
+  tiles (K8/K9; full image on one GPU) -> [N>1] RCCL gather of the packed
+  tiles to rank 0 (torch.distributed 'nccl' == RCCL) + unpack kernel.
+W untimed warm-up steps, then K timed steps between barrier+synchronize on
+both sides; the max over ranks is reported by rank 0 as ONE JSON line.
+
+  value      = W*H*spp / (mean over steps of max-rank trace time + gather time)
+               [Mrays/s, whole image, all ranks; SURVEY.md §8(e)]
+  build_mprims_per_s = N_tris / mean build time (per GPU; replicated)
+  ms_per_step = wall time per frame incl. build, trace, gather and host syncs
+Device times come from hipEvents recorded on the stream each kernel runs on
+(the scene's stream inside librtamd).
+
+roofline: the dominant kernel (trace) -- algorithmic bytes per launch =
+  32 B x nodes fetched + 36 B x tris tested + 16 B x rays (SURVEY.md §8(d);
+  counters from the deterministic counting variant of the same kernel), over
+  its mean event-timed duration, against 8.0 TB/s HBM.
+cpu_baseline (rank 0, N=1 only): the CPU oracle (oracle/, a port of the same
+  contract -- the reference has no runnable code) builds the same 1M soup
+  single-threaded and traces the same full frame on up to 16 host threads.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
+BUILD_BYTES_PER_PRIM = 404  # SURVEY.md §8(d) canonical build byte model
+METRIC = "Mrays/s @1920×1080×1spp + BVH build Mprims/s, 1M-tri scene, 1/2/4/8 GPUs"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS key (3 = soup-1M headline)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_trace.json"))
+    ap.add_argument("--dump", default="", help="write the rank-0 image as PPM")
+    return ap.parse_args()
+
+
+def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters):
+    """Oracle build (1 thread) + full-frame trace (threads); returns dict."""
+    from oracle import oracle as O  # cpu_baseline leg only
+    if not os.path.exists(O._LIB_PATH):
+        O.build_oracle()
+    t0 = time.perf_counter()
+    b = O.build(tris)
+    t_build = time.perf_counter() - t0
+    cam = O.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    t0 = time.perf_counter()
+    _, cnt = O.trace(b["nodes"], tris, cam, w, h, spp, nthreads=threads)
+    t_trace = time.perf_counter() - t0
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    rays = w * h * spp
+    return {
+        "value": rays / t_trace / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+        "sample": f"full frame {w}x{h}x{spp} traced on {threads} threads ({t_trace:.2f} s); "
+                  f"full {len(tris)}-tri BVH built on 1 thread ({t_build:.2f} s)",
+        "build_mprims_per_s": len(tris) / t_build / 1e6, "build_threads": 1,
+        "cpu_model": model,
+        "counters_match_gpu": bool(int(cnt[0]) == int(gpu_counters[0]) and int(cnt[1]) == int(gpu_counters[1])),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if args.gpus > 1 and world == 1:
+            raise SystemExit("for --gpus N>1 launch with torch.distributed.run --nproc-per-node N")
+        world = max(world, 1)
+
+    import torch
+    import torch.distributed as dist
+    import gpu_raytracer_amd as R
+    from gpu_raytracer_amd import scenes as S
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = S.CONFIGS[args.config]
+    view = S.VIEWS[cfg.scene]
+    w, h, spp = cfg.w, cfg.h, cfg.spp
+    rays = w * h * spp
+    if cfg.scene == "soup":
+        scene = R.Scene.generate_soup(cfg.n, 1)
+    else:
+        scene = R.Scene.from_soup(S.tris_for(cfg.scene))
+    n_tris = scene.num_tris
+    scene.set_device(local)
+    cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+
+    ntiles = R.tiles_for_rank(w, h, rank, world)
+    tmax = max(R.tiles_for_rank(w, h, r, world) for r in range(world))
+    dev = torch.device("cuda", local)
+    img = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    hits = torch.empty(rays * 4, dtype=torch.float32, device=dev)
+    slab = torch.zeros(max(tmax, 1) * 256, dtype=torch.int32, device=dev) if world > 1 else None
+    gather_list = [torch.zeros_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
+    slabs_all = torch.zeros(world * max(tmax, 1) * 256, dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
+
+    def step():
+        build_ms = scene.build()
+        if world == 1:
+            trace_ms = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+            return build_ms, trace_ms, 0.0
+        trace_ms = scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), timed=True)
+        t0 = time.perf_counter()
+        dist.gather(slab, gather_list, dst=0)
+        if rank == 0:
+            torch.cat(gather_list, out=slabs_all)
+            R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
+                                  torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize(dev)
+        return build_ms, trace_ms, (time.perf_counter() - t0) * 1e3
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    rec = [step() for _ in range(args.steps)]
+    barrier()
+    wall = time.perf_counter() - t0
+    per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, gather (ms)
+    stimes = scene.build_times()
+
+    # max over ranks (per step), then mean over steps
+    if world > 1:
+        t = torch.tensor(per, dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        per = t.cpu().numpy()
+        wt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+        wall = float(wt.item())
+    build_ms, trace_ms, gather_ms = (float(x) for x in per.mean(axis=0))
+    trace_ms_min = float(per[:, 1].min())
+
+    # work counters of this rank's trace launch (deterministic; untimed)
+    cnt = scene.render_tiles_counters(cam, w, h, spp, rank, world) if world > 1 else scene.render_counters(cam, w, h, spp)
+    rank_rays = (ntiles * 256 * spp) if world > 1 else rays  # upper bound incl. padding lanes; exact below
+    if world > 1:
+        # exact ray count of the rank's tiles (edge tiles are partial)
+        tx = (w + 15) // 16
+        rr = 0
+        for t in range(rank, ((h + 15) // 16) * tx, world):
+            x0, y0 = (t % tx) * 16, (t // tx) * 16
+            rr += min(16, w - x0) * min(16, h - y0)
+        rank_rays = rr * spp
+    algo_bytes = 32.0 * float(cnt[0]) + 36.0 * float(cnt[1]) + 16.0 * rank_rays
+    rank_trace_ms = float(np.array(rec)[:, 1].mean())
+    achieved = algo_bytes / (rank_trace_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == cfg.name and tj.get("n_gpus", 1) == world:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    out = None
+    if rank == 0:
+        value = rays / ((trace_ms + gather_ms) * 1e-3) / 1e6
+        build_gbs = BUILD_BYTES_PER_PRIM * n_tris / (build_ms * 1e-3) / 1e9
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(wall / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: random-triangle soup, splitmix64 seed 1, r=1/cbrt(N) (SURVEY.md §9.9)"
+                    if cfg.scene == "soup" else f"synthetic: procedural {cfg.name} (SURVEY.md §9.9)",
+            "config": {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{args.config - 1}])",
+                       "n_tris": n_tris, "width": w, "height": h, "spp": spp,
+                       "parallelism": f"image tiles 16x16 round-robin over {world} GPU(s), BVH replicated"
+                                      + (", RCCL gather to rank 0" if world > 1 else "")},
+            "build_mprims_per_s": round(n_tris / (build_ms * 1e-3) / 1e6, 2),
+            "build_ms": round(build_ms, 4),
+            "trace_ms": round(trace_ms, 4),
+            "trace_ms_min": round(trace_ms_min, 4),
+            "gather_ms": round(gather_ms, 4),
+            "frame_mrays_per_s": round(rays / (wall / args.steps) / 1e6, 2),
+            "build_stages_ms_last": {"bounds": round(stimes.bounds, 4), "morton": round(stimes.morton, 4),
+                                     "sort": round(stimes.sort, 4), "topology": round(stimes.topology, 4),
+                                     "refit": round(stimes.refit, 4)},
+            "trace_counters_rank0": {"nodes_fetched": int(cnt[0]), "tris_tested": int(cnt[1]), "rays": rank_rays},
+            "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "algo_bytes_per_launch": algo_bytes,
+                         "note": "algorithmic bytes (32/node + 36/tri + 16/ray); scene is Infinity-Cache "
+                                 "resident, so algorithmic GB/s can exceed DRAM traffic"},
+            "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
+                               "bytes_per_prim": BUILD_BYTES_PER_PRIM},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
+            out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt)
+        if args.dump:
+            R.dump_ppm(img.cpu().numpy().view(np.uint8), w, h, args.dump)
+        print(json.dumps(out), flush=True)
+    scene.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,79 @@
+// rt_device.h -- shared device-side definitions for the gfx950 hot path.
+//
+// Numeric contract: SURVEY.md §9.1.  Everything here is compiled with
+// -ffp-contract=off (no FMA contraction) and HIP's default correctly rounded
+// fp32 division; fminf/fmaxf lower to v_min_f32/v_max_f32 (v_min3/v_max3),
+// whose NaN-ignoring, -0 < +0 semantics the CPU oracle restates (oracle
+// rt_oracle.c orc_fmin/orc_fmax; probed on hardware by rt_stage_minmax).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RT_SENT 0xFFFFFFFFu
+
+namespace rt {
+
+struct Tri9 { float v[9]; };
+
+struct Aabb { float lo[3], hi[3]; };
+
+__device__ __forceinline__ void aabb_union(Aabb& a, const Aabb& b) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        a.lo[c] = fminf(a.lo[c], b.lo[c]);
+        a.hi[c] = fmaxf(a.hi[c], b.hi[c]);
+    }
+}
+
+__device__ __forceinline__ Aabb aabb_empty() {
+    Aabb a;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { a.lo[c] = __builtin_inff(); a.hi[c] = -__builtin_inff(); }
+    return a;
+}
+
+// §9.2: bmin = fmin(fmin(v0,v1),v2) per component, likewise bmax
+__device__ __forceinline__ void tri_bounds(const float* t, float* bmin, float* bmax) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        bmin[c] = fminf(fminf(t[c], t[3 + c]), t[6 + c]);
+        bmax[c] = fmaxf(fmaxf(t[c], t[3 + c]), t[6 + c]);
+    }
+}
+
+// §9.3
+__device__ __forceinline__ uint32_t expand10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+// §9.7
+__device__ __forceinline__ uint32_t pcg_hash(uint32_t x) {
+    uint32_t st = x * 747796405u + 2891336453u;
+    uint32_t w = ((st >> ((st >> 28u) + 4u)) ^ st) * 277803737u;
+    return (w >> 22u) ^ w;
+}
+
+// Build-time scalar parameters written by K0 (bounds) for K1 (Morton).
+struct BuildParams {
+    float lo[3], hi[3], inv[3];
+    uint32_t pad[7];
+};
+
+// Morton/sort geometry shared by host and device.
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kSortThreads * kSortItems;   // 4096 keys / tile
+constexpr int kRefitT = 1024;                          // leaves per refit block
+constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
+
+// Onesweep decoupled look-back status word: [31:30] flag, [29:0] count.
+constexpr uint32_t kFlagAgg = 1u << 30;
+constexpr uint32_t kFlagInc = 2u << 30;
+constexpr uint32_t kCountMask = (1u << 30) - 1u;
+
+}  // namespace rt

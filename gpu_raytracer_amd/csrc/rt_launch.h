@@ -1,0 +1,78 @@
+// rt_launch.h -- host-side launchers of the gfx950 kernels (defined next to
+// the kernels in build_kernels.hip / trace_kernels.hip) and the device
+// buffer layout of one BVH build.  Used by rt_abi.cpp only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rt {
+
+struct BuildParams;
+
+// Device buffers of one scene (SURVEY.md §8(a) layouts; sized for cap_n prims).
+struct BuildBufs {
+    uint32_t cap_n = 0;
+    float* tris = nullptr;          // n*9 fp32, AoS (36 B/tri), 256-B aligned
+    uint32_t* keys[2] = {nullptr, nullptr};
+    uint32_t* vals[2] = {nullptr, nullptr};
+    void* nodes = nullptr;          // (2n-1) x 32 B {lo[3], hi[3], a, esc}
+    uint32_t* parent = nullptr;     // 2n-1, unified index space
+    uint4* topo = nullptr;          // n-1 x {left, esc, range_lo, range_hi}
+    uint32_t* lesc = nullptr;       // n leaf escape links
+    float* prebuf = nullptr;        // n x 6: block-prefix AABB at crossing ends
+    float* sufbuf = nullptr;        // n x 6: block-suffix AABB at crossing ends
+    float* table = nullptr;         // sparse table over refit-block totals, levels x M x 6
+    uint32_t* cross = nullptr;      // crossing internal nodes (list)
+    float* partials = nullptr;      // K0 per-block partial bounds
+    uint32_t* ticket = nullptr;     // K0 last-block ticket (self-resetting)
+    BuildParams* params = nullptr;  // lo/hi/inv
+    uint32_t* zero = nullptr;       // per-build zeroed control words, see zero_layout()
+    uint32_t nzero = 0;
+    uint32_t ntiles = 0;            // sort tiles at cap_n
+    uint32_t m_blocks = 0;          // refit blocks at cap_n
+    uint32_t levels = 0;            // sparse-table levels at cap_n
+};
+
+// zero region layout (uint32 words)
+constexpr uint32_t kZHist = 0;          // [4][256] digit histograms
+constexpr uint32_t kZTileCtr = 1024;    // [4] onesweep tile tickets
+constexpr uint32_t kZCrossCtr = 1028;   // crossing-list length
+constexpr uint32_t kZErr = 1029;        // sticky error bits (look-back timeout)
+constexpr uint32_t kZStatus = 1040;     // [4][256][ntiles] look-back words
+
+constexpr uint32_t kBoundsGrid = 1024;
+
+hipError_t alloc_build(BuildBufs& b, uint32_t n);
+void free_build(BuildBufs& b);
+
+struct BuildEvents { hipEvent_t e[6]; bool valid = false; };
+
+// K0..K6 on `stream` for the n tris already in b.tris.  Sorted keys/vals end
+// in keys[0]/vals[0].  Records e[0..5] around the stages when ev != nullptr.
+hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev);
+
+// Stage launchers for parity entry points (buffers sized by the caller).
+hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, uint32_t* ticket,
+                              BuildParams* params, hipStream_t s);
+hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,
+                         uint32_t* vals, uint32_t* ghist, hipStream_t s);
+hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s);
+hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, uint32_t* zero, hipStream_t s);
+hipError_t launch_karras(const uint32_t* keys, uint32_t n, uint4* topo, uint32_t* parent, uint32_t* lesc,
+                         hipStream_t s);
+uint32_t sort_tiles(uint32_t n);
+
+struct CamF { float eye[3], w00[3], du[3], dv[3]; };
+
+hipError_t launch_trace(const void* nodes, const float* tris, uint32_t n, const CamF& cam, uint32_t w,
+                        uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
+                        void* hits, void* rgba, unsigned long long* counters, hipStream_t s);
+hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
+                         void* img, hipStream_t s);
+uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);
+hipError_t launch_intersect(uint32_t count, const float* o, const float* d, const float* tri, const float* tb,
+                            uint32_t* hit, float* tuv, hipStream_t s);
+hipError_t launch_minmax(uint32_t count, const float* a, const float* b, float* out, hipStream_t s);
+
+}  // namespace rt

@@ -1,0 +1,247 @@
+// trace_kernels.hip -- K8 trace + K9 shade for gfx950.
+//
+// One thread per pixel; a 256-thread workgroup owns one 16x16-pixel image
+// tile and each wave64 an 8x8 sub-tile, so the 64 rays that share an
+// instruction stream are spatially coherent.  Per sample: raygen (§9.7),
+// stackless escape-link traversal over 32-B nodes (two 16-B loads per node),
+// Moller-Trumbore on the leaf's triangle, closest hit with strict '<'.
+// K9 is fused: the thread averages its pixel's samples in order and writes
+// RGBA8.  Tiles are dealt round-robin to ranks (tile t -> rank t mod P); with
+// PACKED the rank writes its tiles compactly for the RCCL gather.
+#include "rt_device.h"
+#include "rt_launch.h"
+
+namespace rt {
+
+struct Cam { float eye[3], w00[3], du[3], dv[3]; };
+
+__device__ __forceinline__ float dot3(const float* a, const float* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+__device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// §9.7 Moller-Trumbore, two-sided, no epsilon; writes t/u/v on a closer hit.
+__device__ __forceinline__ bool intersect_tri(const float* o, const float* d, const float* tri, float tb,
+                                              float& tout, float& uout, float& vout) {
+    float e1[3], e2[3], p[3], s[3], q[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { e1[c] = tri[3 + c] - tri[c]; e2[c] = tri[6 + c] - tri[c]; }
+    cross3(d, e2, p);
+    const float det = dot3(e1, p);
+    if (det == 0.0f) return false;
+    const float inv = 1.0f / det;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) s[c] = o[c] - tri[c];
+    const float u = dot3(s, p) * inv;
+    if (u < 0.0f || u > 1.0f) return false;
+    cross3(s, e1, q);
+    const float v = dot3(d, q) * inv;
+    if (v < 0.0f || u + v > 1.0f) return false;
+    const float t = dot3(e2, q) * inv;
+    if (t <= 0.0f) return false;
+    if (!(t < tb)) return false;
+    tout = t; uout = u; vout = v;
+    return true;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float* __restrict__ tris, uint32_t n,
+                                          const float* o, const float* d, float& tb, float& hu, float& hv,
+                                          uint32_t& hp, uint32_t& cn, uint32_t& ct) {
+    float invd[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) invd[c] = 1.0f / d[c];
+    tb = __builtin_inff(); hu = 0.0f; hv = 0.0f; hp = RT_SENT;
+    const uint32_t L0 = n ? n - 1 : 0;
+    const uint32_t total = n ? 2 * n - 1 : 0;
+    uint32_t idx = n ? 0u : RT_SENT;
+    // A well-formed escape-link tree visits each node at most once; the
+    // bound and the index check only keep a malformed tree from faulting.
+    for (uint32_t guard = 0; idx < total && guard < total; ++guard) {
+        const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)idx * 32);
+        const float4 A = np[0], B = np[1];
+        if (COUNT) ++cn;
+        const float t0x = (A.x - o[0]) * invd[0], t1x = (A.w - o[0]) * invd[0];
+        const float t0y = (A.y - o[1]) * invd[1], t1y = (B.x - o[1]) * invd[1];
+        const float t0z = (A.z - o[2]) * invd[2], t1z = (B.y - o[2]) * invd[2];
+        const float tn = fmaxf(fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z)), 0.0f);
+        const float tf = fminf(fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)), tb);
+        const uint32_t na = __float_as_uint(B.z), esc = __float_as_uint(B.w);
+        if (!(tn <= tf)) { idx = esc; continue; }
+        if (idx >= L0) {
+            if (COUNT) ++ct;
+            const float* tp = tris + (uint64_t)na * 9;
+            float tri[9];
+#pragma unroll
+            for (int c = 0; c < 9; ++c) tri[c] = tp[c];
+            float t, u, v;
+            if (intersect_tri(o, d, tri, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = na; }
+            idx = esc;
+        } else {
+            idx = na;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
+
+template <bool COUNT, bool PACKED>
+__global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, const float* __restrict__ tris, uint32_t n,
+                                               Cam cam, uint32_t W, uint32_t H, uint32_t spp,
+                                               uint32_t rank, uint32_t nranks, uint32_t tilesX,
+                                               float4* __restrict__ hits, uint32_t* __restrict__ rgba,
+                                               unsigned long long* __restrict__ counters) {
+    const uint32_t t = rank + blockIdx.x * nranks;
+    const uint32_t tx = t % tilesX, ty = t / tilesX;
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
+    const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
+    const bool valid = x < W && y < H;
+    uint32_t cn = 0, ct = 0;
+    if (valid) {
+        float r = 0.0f, g = 0.0f, b = 0.0f;
+        for (uint32_t s = 0; s < spp; ++s) {
+            const uint32_t sidx = (y * W + x) * spp + s;
+            float jx = 0.5f, jy = 0.5f;
+            if (s > 0) {
+                const uint32_t h = pcg_hash(sidx);
+                jx = (float)(h >> 8) * 0x1p-24f;
+                jy = (float)(pcg_hash(h) >> 8) * 0x1p-24f;
+            }
+            const float px = (float)x + jx, py = (float)y + jy;
+            float d[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+            float tb, hu, hv;
+            uint32_t hp;
+            trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tris, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
+            if (hits) {
+                const uint64_t hi = PACKED ? ((uint64_t)blockIdx.x * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
+                hits[hi] = make_float4(tb, hu, hv, __uint_as_float(hp));
+            }
+            if (hp != RT_SENT) {
+                r = r + hu;
+                g = g + hv;
+                b = b + ((1.0f - hu) - hv);
+            } else {
+                r = r + 0.0f; g = g + 0.0f; b = b + 0.0f;
+            }
+        }
+        if (rgba) {
+            const float sc = 1.0f / (float)spp;
+            const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+            const uint64_t pi = PACKED ? (uint64_t)blockIdx.x * 256 + ly * 16 + lx : (uint64_t)y * W + x;
+            rgba[pi] = px;
+        }
+    }
+    if (COUNT) {
+        unsigned long long a = cn, bsum = ct;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            a += __shfl_xor(a, o, 64);
+            bsum += __shfl_xor(bsum, o, 64);
+        }
+        if (l == 0) {
+            atomicAdd(&counters[0], a);
+            atomicAdd(&counters[1], bsum);
+        }
+    }
+}
+
+// Gathered slabs [rank][tile][256 px] -> W x H image.
+__global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ slabs, uint32_t tiles_per_slab, uint32_t W,
+                                                uint32_t H, uint32_t nranks, uint32_t tilesX, uint32_t ntiles,
+                                                uint32_t* __restrict__ img) {
+    const uint32_t rk = blockIdx.x / tiles_per_slab, b = blockIdx.x % tiles_per_slab;
+    const uint32_t t = rk + b * nranks;
+    if (t >= ntiles) return;
+    const uint32_t tx = t % tilesX, ty = t / tilesX;
+    const uint32_t lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+    const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
+    if (x < W && y < H) img[(uint64_t)y * W + x] = slabs[(uint64_t)blockIdx.x * 256 + threadIdx.x];
+}
+
+// KAT entry point: Moller-Trumbore per (o, d, tri, t_best).
+__global__ void k_intersect(uint32_t count, const float* __restrict__ o, const float* __restrict__ d,
+                            const float* __restrict__ tri, const float* __restrict__ tbest,
+                            uint32_t* __restrict__ hit, float* __restrict__ tuv) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    float t = 0.0f, u = 0.0f, v = 0.0f;
+    float oo[3] = {o[3 * i], o[3 * i + 1], o[3 * i + 2]};
+    float dd[3] = {d[3 * i], d[3 * i + 1], d[3 * i + 2]};
+    float tt[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) tt[c] = tri[9 * i + c];
+    const bool h = intersect_tri(oo, dd, tt, tbest[i], t, u, v);
+    hit[i] = h ? 1u : 0u;
+    tuv[3 * i] = t; tuv[3 * i + 1] = u; tuv[3 * i + 2] = v;
+}
+
+// Semantics probe of the device min/max the whole contract relies on.
+__global__ void k_minmax(uint32_t count, const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= count) return;
+    out[2 * i] = fminf(a[i], b[i]);
+    out[2 * i + 1] = fmaxf(a[i], b[i]);
+}
+
+template __global__ void k_trace<false, false>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<true, false>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<false, true>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<true, true>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+
+// ================================================================ launchers
+uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
+    const uint32_t nt = ((w + 15) / 16) * ((h + 15) / 16);
+    if (!nranks || rank >= nranks || rank >= nt) return 0;
+    return (nt - rank + nranks - 1) / nranks;
+}
+
+hipError_t launch_trace(const void* nodes, const float* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
+                        uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits, void* rgba,
+                        unsigned long long* counters, hipStream_t s) {
+    const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
+    if (!nb) return hipSuccess;
+    Cam cam;
+    for (int i = 0; i < 3; ++i) {
+        cam.eye[i] = c.eye[i]; cam.w00[i] = c.w00[i]; cam.du[i] = c.du[i]; cam.dv[i] = c.dv[i];
+    }
+    const uint32_t tilesX = (w + 15) / 16;
+    float4* H = reinterpret_cast<float4*>(hits);
+    uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
+    if (counters) {
+        if (packed) hipLaunchKernelGGL((k_trace<true, true>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
+        else hipLaunchKernelGGL((k_trace<true, false>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
+    } else {
+        if (packed) hipLaunchKernelGGL((k_trace<false, true>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
+        else hipLaunchKernelGGL((k_trace<false, false>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
+                         void* img, hipStream_t s) {
+    if (!tiles_per_slab || !nranks) return hipSuccess;
+    const uint32_t tilesX = (w + 15) / 16, nt = tilesX * ((h + 15) / 16);
+    hipLaunchKernelGGL(k_unpack, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const uint32_t*)slabs, tiles_per_slab,
+                       w, h, nranks, tilesX, nt, (uint32_t*)img);
+    return hipGetLastError();
+}
+
+hipError_t launch_intersect(uint32_t count, const float* o, const float* d, const float* tri, const float* tb,
+                            uint32_t* hit, float* tuv, hipStream_t s) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_intersect, dim3((count + 255) / 256), dim3(256), 0, s, count, o, d, tri, tb, hit, tuv);
+    return hipGetLastError();
+}
+
+hipError_t launch_minmax(uint32_t count, const float* a, const float* b, float* out, hipStream_t s) {
+    if (!count) return hipSuccess;
+    hipLaunchKernelGGL(k_minmax, dim3((count + 255) / 256), dim3(256), 0, s, count, a, b, out);
+    return hipGetLastError();
+}
+
+}  // namespace rt

@@ -1,0 +1,270 @@
+"""Host-side Python mirror of the librtamd C-ABI (include/gpu_raytracer_amd.h).
+
+Thin numpy-facing wrappers: no compute happens in Python, every call goes to
+the gfx950 kernels through ctypes, and errors surface as RtError carrying the
+library's status and message.  Names follow the ABI:
+scene ingest -> rt_bvh_build -> rt_render -> framebuffer/hit dumps, plus the
+per-stage entry points the parity tests drive.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import SENTINEL, call, lib, rt_build_times, rt_camera
+
+NODE_DTYPE = np.dtype([("lo", "<f4", (3,)), ("hi", "<f4", (3,)), ("a", "<u4"), ("esc", "<u4")])
+HIT_DTYPE = np.dtype([("t", "<f4"), ("u", "<f4"), ("v", "<f4"), ("prim", "<u4")])
+TILE = 16
+
+
+def _p(a: np.ndarray) -> C.c_void_p:
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return C.c_void_p(a.ctypes.data)
+
+
+def camera_look_at(eye, at, up, vfov_deg: float, w: int, h: int) -> rt_camera:
+    """SURVEY.md §9.7 ray frame (double on the host, rounded to float)."""
+    cam = rt_camera()
+    e, a, u = (np.ascontiguousarray(x, dtype=np.float64) for x in (eye, at, up))
+    call("rt_camera_look_at", _p(e), _p(a), _p(u), float(vfov_deg), int(w), int(h), C.byref(cam))
+    return cam
+
+
+def camera_array(cam: rt_camera) -> np.ndarray:
+    return np.array([list(cam.eye), list(cam.w00), list(cam.du), list(cam.dv)], dtype=np.float32)
+
+
+@dataclass
+class BuildTimes:
+    bounds: float
+    morton: float
+    sort: float
+    topology: float
+    refit: float
+    total: float
+
+
+class Scene:
+    """Opaque rt_scene handle: host soup + device-resident BVH on one GPU."""
+
+    def __init__(self, handle: C.c_void_p):
+        self._h = handle
+
+    # -- ingest
+    @classmethod
+    def from_soup(cls, tris: np.ndarray) -> "Scene":
+        t = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+        h = C.c_void_p()
+        call("rt_scene_from_soup", _p(t) if len(t) else None, len(t), C.byref(h))
+        return cls(h)
+
+    @classmethod
+    def load_obj(cls, path: str) -> "Scene":
+        h = C.c_void_p()
+        call("rt_scene_load_obj", path.encode(), C.byref(h))
+        return cls(h)
+
+    @classmethod
+    def generate_soup(cls, n: int, seed: int = 1) -> "Scene":
+        h = C.c_void_p()
+        call("rt_scene_generate_soup", int(n), int(seed), C.byref(h))
+        return cls(h)
+
+    def close(self) -> None:
+        if self._h:
+            lib().rt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    @property
+    def num_tris(self) -> int:
+        n = C.c_uint32()
+        call("rt_scene_num_tris", self._h, C.byref(n))
+        return n.value
+
+    def tris(self) -> np.ndarray:
+        out = np.empty((self.num_tris, 9), np.float32)
+        if len(out):
+            call("rt_scene_get_tris", self._h, _p(out))
+        return out
+
+    def set_device(self, device: int) -> None:
+        call("rt_scene_set_device", self._h, int(device))
+
+    # -- build
+    def build(self) -> float:
+        ms = C.c_double()
+        call("rt_bvh_build", self._h, C.byref(ms))
+        return ms.value
+
+    def build_times(self) -> BuildTimes:
+        t = rt_build_times()
+        call("rt_bvh_build_times", self._h, C.byref(t))
+        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.total)
+
+    def read_bvh(self) -> dict:
+        n = self.num_tris
+        tot = max(2 * n - 1, 0)
+        nodes = np.zeros(max(tot, 1), NODE_DTYPE)
+        keys = np.zeros(max(n, 1), np.uint32)
+        vals = np.zeros(max(n, 1), np.uint32)
+        parent = np.zeros(max(tot, 1), np.uint32)
+        bounds = np.zeros(9, np.float32)
+        call("rt_bvh_read", self._h, _p(nodes), _p(keys), _p(vals), _p(parent), _p(bounds))
+        return dict(nodes=nodes[:tot], keys=keys[:n], vals=vals[:n], parent=parent[:tot],
+                    lo=bounds[0:3].copy(), hi=bounds[3:6].copy(), inv=bounds[6:9].copy())
+
+    # -- render
+    def render(self, cam: rt_camera, w: int, h: int, spp: int = 1, hits: bool = True, rgba: bool = True):
+        """Returns (hits[h*w*spp] HIT_DTYPE or None, rgba[h*w*4] uint8 or None, trace_ms)."""
+        hb = np.zeros(w * h * spp, HIT_DTYPE) if hits else None
+        rb = np.zeros(w * h * 4, np.uint8) if rgba else None
+        ms = C.c_double()
+        call("rt_render", self._h, C.byref(cam), w, h, spp, _p(hb) if hits else None,
+             _p(rb) if rgba else None, C.byref(ms))
+        return hb, rb, ms.value
+
+    def render_counters(self, cam: rt_camera, w: int, h: int, spp: int = 1) -> np.ndarray:
+        c = np.zeros(2, np.uint64)
+        call("rt_render_counters", self._h, C.byref(cam), w, h, spp, _p(c))
+        return c
+
+    def render_device(self, cam, w, h, spp, d_rgba: int = 0, d_hits: int = 0, stream: int = 0,
+                      timed: bool = False):
+        """Full-image render into device buffers (device pointers as ints)."""
+        ms = C.c_double()
+        call("rt_render_device", self._h, C.byref(cam), w, h, spp, C.c_void_p(d_hits) if d_hits else None,
+             C.c_void_p(d_rgba) if d_rgba else None, C.c_void_p(stream) if stream else None,
+             C.byref(ms) if timed else None)
+        return ms.value if timed else None
+
+    def render_tiles_counters(self, cam, w, h, spp, rank, nranks) -> np.ndarray:
+        c = np.zeros(2, np.uint64)
+        call("rt_render_tiles_counters", self._h, C.byref(cam), w, h, spp, rank, nranks, _p(c))
+        return c
+
+    def render_tiles_device(self, cam, w, h, spp, rank, nranks, d_rgba: int, d_hits: int = 0,
+                            stream: int = 0, timed: bool = False):
+        ms = C.c_double()
+        call("rt_render_tiles_device", self._h, C.byref(cam), w, h, spp, rank, nranks, C.c_void_p(d_rgba),
+             C.c_void_p(d_hits) if d_hits else None, C.c_void_p(stream) if stream else None,
+             C.byref(ms) if timed else None)
+        return ms.value if timed else None
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        call("rt_scene_stream", self._h, C.byref(s))
+        return s.value or 0
+
+    def sync(self) -> None:
+        call("rt_scene_sync", self._h)
+
+
+def tiles_for_rank(w: int, h: int, rank: int, nranks: int) -> int:
+    return int(lib().rt_tiles_for_rank(w, h, rank, nranks))
+
+
+def unpack_tiles_device(d_slabs: int, tiles_per_slab: int, w: int, h: int, nranks: int, d_rgba: int,
+                        device: int = 0, stream: int = 0) -> None:
+    call("rt_unpack_tiles_device", C.c_void_p(d_slabs), tiles_per_slab, w, h, nranks, C.c_void_p(d_rgba),
+         int(device), C.c_void_p(stream) if stream else None)
+
+
+def dump_ppm(rgba: np.ndarray, w: int, h: int, path: str) -> None:
+    call("rt_framebuffer_dump_ppm", _p(np.ascontiguousarray(rgba, np.uint8)), w, h, path.encode())
+
+
+def dump_hits(hits: np.ndarray, path: str) -> None:
+    h = np.ascontiguousarray(hits, HIT_DTYPE)
+    call("rt_hits_dump", _p(h) if len(h) else None, len(h), path.encode())
+
+
+def device_count() -> int:
+    return int(lib().rt_device_count())
+
+
+# -- per-stage entry points (parity tests) -------------------------------
+def stage_bounds(tris: np.ndarray, device: int = 0):
+    t = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    out = np.zeros(9, np.float32)
+    call("rt_stage_bounds", device, _p(t) if len(t) else None, len(t), _p(out))
+    return out[0:3].copy(), out[3:6].copy(), out[6:9].copy()
+
+
+def stage_morton(tris, lo, inv, device: int = 0):
+    t = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    n = len(t)
+    k = np.zeros(max(n, 1), np.uint32)
+    v = np.zeros(max(n, 1), np.uint32)
+    call("rt_stage_morton", device, _p(t) if n else None, n, _p(np.ascontiguousarray(lo, np.float32)),
+         _p(np.ascontiguousarray(inv, np.float32)), _p(k), _p(v))
+    return k[:n], v[:n]
+
+
+def stage_sort(keys, vals, device: int = 0):
+    k = np.array(keys, np.uint32, copy=True)
+    v = np.array(vals, np.uint32, copy=True)
+    call("rt_stage_sort", device, _p(k) if len(k) else None, _p(v) if len(v) else None, len(k))
+    return k, v
+
+
+def stage_topology(sorted_keys, device: int = 0):
+    k = np.ascontiguousarray(sorted_keys, np.uint32)
+    n = len(k)
+    topo = np.zeros((max(n - 1, 1), 4), np.uint32)
+    parent = np.zeros(max(2 * n - 1, 1), np.uint32)
+    lesc = np.zeros(max(n, 1), np.uint32)
+    call("rt_stage_topology", device, _p(k) if n else None, n, _p(topo), _p(parent), _p(lesc))
+    return topo[: max(n - 1, 0)], parent[: max(2 * n - 1, 0)], lesc[:n]
+
+
+def stage_trace(nodes, tris, cam: rt_camera, w, h, spp=1, device: int = 0):
+    t = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    nd = np.ascontiguousarray(nodes, NODE_DTYPE)
+    n = len(t)
+    hits = np.zeros(w * h * spp, HIT_DTYPE)
+    rgba = np.zeros(w * h * 4, np.uint8)
+    cnt = np.zeros(2, np.uint64)
+    call("rt_stage_trace", device, _p(nd) if n else None, n, _p(t) if n else None, C.byref(cam), w, h, spp,
+         _p(hits), _p(rgba), _p(cnt))
+    return hits, rgba, cnt
+
+
+def stage_intersect(o, d, tri, t_best, device: int = 0):
+    o = np.ascontiguousarray(o, np.float32).reshape(-1, 3)
+    d = np.ascontiguousarray(d, np.float32).reshape(-1, 3)
+    tri = np.ascontiguousarray(tri, np.float32).reshape(-1, 9)
+    tb = np.ascontiguousarray(t_best, np.float32).reshape(-1)
+    n = len(o)
+    hit = np.zeros(max(n, 1), np.uint32)
+    tuv = np.zeros((max(n, 1), 3), np.float32)
+    call("rt_stage_intersect", device, n, _p(o), _p(d), _p(tri), _p(tb), _p(hit), _p(tuv))
+    return hit[:n].astype(bool), tuv[:n]
+
+
+def stage_minmax(a, b, device: int = 0):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    out = np.zeros((max(len(a), 1), 2), np.float32)
+    call("rt_stage_minmax", device, len(a), _p(a), _p(b), _p(out))
+    return out[: len(a), 0].copy(), out[: len(a), 1].copy()
+
+
+__all__ = ["Scene", "camera_look_at", "camera_array", "tiles_for_rank", "unpack_tiles_device", "dump_ppm",
+           "dump_hits", "device_count", "stage_bounds", "stage_morton", "stage_sort", "stage_topology",
+           "stage_trace", "stage_intersect", "stage_minmax", "NODE_DTYPE", "HIT_DTYPE", "SENTINEL"]

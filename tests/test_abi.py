@@ -1,0 +1,127 @@
+"""CPU tests of the C-ABI boundary (librtamd.so): it loads, exports every
+symbol include/gpu_raytracer_amd.h declares, its host-side pieces (scene
+ingest, camera, OBJ/PPM/hit I/O, tile partition) match the oracle, and its
+compute entry points fail loudly (RT_EDEVICE) when no GPU is present -- there
+is no CPU fallback.  No compute call runs here."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, bits
+
+HEADER = os.path.join(ROOT, "include", "gpu_raytracer_amd.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(rt_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_symbols_exported(rt):
+    import subprocess
+    declared = header_functions()
+    assert len(declared) >= 25
+    out = subprocess.run(["nm", "-D", "--defined-only", rt._lib.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\bT (rt_[a-z0-9_]+)", out))
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    assert sorted(rt._lib.EXPORTED) == declared
+    for f in declared:
+        getattr(rt.lib(), f)  # resolvable through ctypes
+
+
+def test_library_is_gfx950(rt):
+    import subprocess
+    blob = open(rt._lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert rt.lib().rt_version().decode().endswith("(gfx950)")
+
+
+def test_camera_matches_oracle(rt, oracle):
+    for (eye, at, up, fov, w, h) in [((0.5, 0.5, -1.5), (0.5, 0.5, 0.5), (0, 1, 0), 45, 1920, 1080),
+                                     ((278, 273, -800), (278, 273, 0), (0, 1, 0), 39.3077, 256, 256),
+                                     ((1, 2, 3), (-4, 0.5, 9), (0.2, 1, 0.1), 70, 333, 77)]:
+        c = rt.camera_look_at(eye, at, up, fov, w, h)
+        o = oracle.camera_look_at(eye, at, up, fov, w, h)
+        assert np.array_equal(bits(rt.camera_array(c)), bits(o.as_array()))
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 100003])
+def test_soup_generator_matches_oracle(rt, oracle, n):
+    s = rt.Scene.generate_soup(n, 1)
+    assert s.num_tris == n
+    assert np.array_equal(bits(s.tris()), bits(oracle.soup(n, 1).reshape(-1, 9)))
+    s.close()
+
+
+def test_from_soup_roundtrip(rt):
+    t = np.random.default_rng(0).random((123, 9), dtype=np.float32)
+    with rt.Scene.from_soup(t) as s:
+        assert s.num_tris == 123 and np.array_equal(s.tris(), t)
+
+
+def test_obj_loader(rt, tmp_path):
+    p = tmp_path / "quad.obj"
+    p.write_text("# comment\nmtllib x.mtl\nv 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvn 0 0 1\nvt 0 0\n"
+                 "o thing\nusemtl m\nf 1/1/1 2/1/1 3/1/1 4/1/1\nf -4 -2 -1\ns off\n")
+    with rt.Scene.load_obj(str(p)) as s:
+        t = s.tris()
+    exp = np.array([[0, 0, 0, 1, 0, 0, 1, 1, 0], [0, 0, 0, 1, 1, 0, 0, 1, 0], [0, 0, 0, 1, 1, 0, 0, 1, 0]], np.float32)
+    assert np.array_equal(t, exp)
+    bad = tmp_path / "bad.obj"
+    bad.write_text("v 0 0 0\nf 1 2 3\n")
+    with pytest.raises(rt.RtError) as e:
+        rt.Scene.load_obj(str(bad))
+    assert e.value.status == -3
+    with pytest.raises(rt.RtError) as e:
+        rt.Scene.load_obj(str(tmp_path / "missing.obj"))
+    assert e.value.status == -3
+
+
+def test_ppm_and_hits_dump(rt, tmp_path):
+    rgba = np.arange(4 * 3 * 4, dtype=np.uint8)
+    p = tmp_path / "img.ppm"
+    rt.dump_ppm(rgba, 4, 3, str(p))
+    data = p.read_bytes()
+    assert data.startswith(b"P6\n4 3\n255\n")
+    assert data[len(b"P6\n4 3\n255\n"):] == rgba.reshape(-1, 4)[:, :3].tobytes()
+    hits = np.zeros(5, rt.HIT_DTYPE)
+    hits["t"] = np.arange(5)
+    hits["prim"] = 0xFFFFFFFF
+    q = tmp_path / "h.bin"
+    rt.dump_hits(hits, str(q))
+    assert q.read_bytes() == hits.tobytes()
+
+
+@pytest.mark.parametrize("w,h,P", [(1920, 1080, 1), (1920, 1080, 8), (3840, 2160, 8), (17, 33, 3), (16, 16, 4)])
+def test_tile_partition(rt, w, h, P):
+    nt = ((w + 15) // 16) * ((h + 15) // 16)
+    counts = [rt.tiles_for_rank(w, h, r, P) for r in range(P)]
+    assert sum(counts) == nt
+    assert max(counts) - min(counts) <= 1
+    assert rt.tiles_for_rank(w, h, P, P) == 0
+
+
+def test_invalid_arguments(rt):
+    with pytest.raises(rt.RtError) as e:
+        rt.Scene.from_soup(np.zeros((0, 9), np.float32)).render(rt.camera_look_at((0, 0, -1), (0, 0, 0), (0, 1, 0), 45, 8, 8), 8, 8)
+    assert e.value.status == -1  # not built
+
+
+def test_no_cpu_fallback(rt):
+    """Without a GPU every compute entry point fails loudly with RT_EDEVICE."""
+    if rt.device_count() > 0:
+        pytest.skip("a GPU is visible; covered by the gpu tests")
+    tris = np.random.default_rng(1).random((64, 9), dtype=np.float32)
+    with rt.Scene.from_soup(tris) as s:
+        with pytest.raises(rt.RtError) as e:
+            s.build()
+        assert e.value.status == -4
+    for f in (lambda: rt.stage_bounds(tris), lambda: rt.stage_sort(np.arange(10), np.arange(10)),
+              lambda: rt.stage_minmax(np.zeros(2), np.zeros(2))):
+        with pytest.raises(rt.RtError) as e:
+            f()
+        assert e.value.status == -4

@@ -1,0 +1,303 @@
+"""GPU parity tests: librtamd (gfx950 kernels, through the C-ABI) vs the CPU
+oracle on the same inputs -- bit-exact for bounds, Morton codes, sorted
+keys/indices, topology, escape links, AABBs, hits, counters and images
+(hits are allowed 1 ulp, we require 0 and report it).
+Parity vs upstream SoslanGM/gpu_raytracer is unpinned (code-less reference);
+the oracle is pinned by tests/test_oracle.py."""
+import numpy as np
+import pytest
+
+from conftest import bits, load_golden
+
+pytestmark = pytest.mark.gpu
+SENT = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module")
+def R(rt):
+    if rt.device_count() < 1:
+        pytest.fail("no GPU visible to librtamd")
+    return rt
+
+
+def soup(oracle, n, seed=1):
+    return oracle.soup(n, seed).reshape(-1, 9)
+
+
+# ------------------------------------------------------------------ semantics probes
+def test_single_hip_runtime(R):
+    maps = open("/proc/self/maps").read()
+    libs = {line.split()[-1] for line in maps.splitlines() if "libamdhip64" in line}
+    assert len(libs) == 1, libs
+
+
+def test_device_minmax_semantics(R, oracle):
+    """The contract's fminf/fmaxf (v_min/v_max) == the oracle's restatement."""
+    sp = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 1e-45, -1e-45, 3.4e38], np.float32)
+    a, b = np.meshgrid(sp, sp, indexing="ij")
+    rng = np.random.default_rng(0)
+    a = np.concatenate([a.ravel(), rng.standard_normal(1000).astype(np.float32)])
+    b = np.concatenate([b.ravel(), rng.standard_normal(1000).astype(np.float32)])
+    mn, mx = R.stage_minmax(a, b)
+    L = oracle.lib()
+    emn = np.array([L.orc_fmin(float(x), float(y)) for x, y in zip(a, b)], np.float32)
+    emx = np.array([L.orc_fmax(float(x), float(y)) for x, y in zip(a, b)], np.float32)
+    nan = np.isnan(emn)
+    assert np.array_equal(np.isnan(mn), nan)
+    assert np.array_equal(bits(mn[~nan]), bits(emn[~nan]))
+    nan = np.isnan(emx)
+    assert np.array_equal(np.isnan(mx), nan)
+    assert np.array_equal(bits(mx[~nan]), bits(emx[~nan]))
+
+
+def test_device_intersect(R, oracle):
+    tri = np.array([[-1, -1, 0, 1, -1, 0, -1, 1, 0]], np.float32)
+    hit, tuv = R.stage_intersect([[0, 0, -1]], [[0, 0, 1]], tri, [np.inf])
+    assert hit[0] and tuple(tuv[0]) == (1.0, 0.5, 0.5)
+    rng = np.random.default_rng(3)
+    n = 4096
+    o = rng.standard_normal((n, 3)).astype(np.float32)
+    d = rng.standard_normal((n, 3)).astype(np.float32)
+    t = (rng.standard_normal((n, 9)) * 2).astype(np.float32)
+    tb = np.where(rng.random(n) < 0.3, rng.random(n) * 3, np.inf).astype(np.float32)
+    hit, tuv = R.stage_intersect(o, d, t, tb)
+    for i in range(n):
+        h, tt, uu, vv = oracle.intersect_tri(o[i], d[i], t[i], tb[i])
+        assert hit[i] == h, i
+        if h:
+            assert np.array_equal(bits(tuv[i]), bits(np.array([tt, uu, vv], np.float32))), i
+    assert hit.sum() > 100
+
+
+# ------------------------------------------------------------------ stages
+@pytest.mark.parametrize("n", [0, 1, 5, 255, 256, 257, 100000, 1000003])
+def test_stage_bounds_morton(R, oracle, n):
+    tris = soup(oracle, n, 4)
+    lo, hi, inv = R.stage_bounds(tris)
+    elo, ehi, einv = oracle.centroid_bounds(tris)
+    assert np.array_equal(bits(lo), bits(elo)) and np.array_equal(bits(hi), bits(ehi))
+    assert np.array_equal(bits(inv), bits(einv))
+    if n:
+        k, v = R.stage_morton(tris, lo, inv)
+        ek, ev = oracle.morton(tris, elo, einv)
+        assert np.array_equal(k, ek) and np.array_equal(v, ev)
+
+
+def _keys(kind, n, rng):
+    return {
+        "random": rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32),
+        "morton30": rng.integers(0, 2**30, n, dtype=np.uint64).astype(np.uint32),
+        "equal": np.full(n, 0x12345678, np.uint32),
+        "sorted": np.arange(n, dtype=np.uint32),
+        "reversed": np.arange(n, dtype=np.uint32)[::-1].copy(),
+        "onebucket": (rng.integers(0, 256, n) << 16).astype(np.uint32),
+        "fewkeys": rng.integers(0, 3, n).astype(np.uint32) * 0x01010101,
+    }[kind]
+
+
+@pytest.mark.parametrize("n", [2, 3, 4095, 4096, 4097, 12289, 250000, 1 << 20])
+@pytest.mark.parametrize("kind", ["random", "morton30", "equal", "sorted", "reversed", "onebucket", "fewkeys"])
+def test_stage_sort(R, n, kind):
+    rng = np.random.default_rng(n)
+    keys = _keys(kind, n, rng)
+    vals = rng.permutation(n).astype(np.uint32)
+    k, v = R.stage_sort(keys, vals)
+    o = np.argsort(keys, kind="stable")
+    assert np.array_equal(k, keys[o])
+    assert np.array_equal(v, vals[o])
+
+
+@pytest.mark.parametrize("n", [2, 3, 8, 1000, 65537])
+def test_stage_topology(R, oracle, n):
+    tris = soup(oracle, n, 9)
+    b = oracle.build(tris)
+    keys = b["keys"]
+    left, right, rlo, rhi, parent = oracle.karras(keys)
+    esc = oracle.escape(n, left, right, parent)
+    topo, par, lesc = R.stage_topology(keys)
+    assert np.array_equal(topo[:, 0], left)
+    assert np.array_equal(topo[:, 1], esc[: n - 1])
+    assert np.array_equal(topo[:, 2], rlo) and np.array_equal(topo[:, 3], rhi)
+    assert np.array_equal(par, parent)
+    assert np.array_equal(lesc[: n - 1], esc[n - 1: 2 * n - 2])
+
+
+def test_topology_fig4(R):
+    g = load_golden("karras8.npz")
+    topo, par, lesc = R.stage_topology(g["keys"])
+    assert np.array_equal(topo[:, 0], g["left"]) and np.array_equal(topo[:, 1], g["esc"][:7])
+    assert np.array_equal(par, g["parent"])
+    assert np.array_equal(lesc[:7], g["esc"][7:14])
+
+
+# ------------------------------------------------------------------ full build
+def _compare_build(R, oracle, tris):
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        got = s.read_bvh()
+    exp = oracle.build(tris)
+    for f in ("lo", "hi", "inv"):
+        assert np.array_equal(bits(got[f]), bits(exp[f])), f
+    assert np.array_equal(got["keys"], exp["keys"])
+    assert np.array_equal(got["vals"], exp["vals"])
+    assert np.array_equal(got["parent"], exp["parent"])
+    g, e = got["nodes"], exp["nodes"]
+    assert np.array_equal(g["a"], e["a"])
+    assert np.array_equal(g["esc"], e["esc"])
+    assert np.array_equal(bits(g["lo"]), bits(e["lo"]))
+    assert np.array_equal(bits(g["hi"]), bits(e["hi"]))
+    return got
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 4, 8, 100, 1023, 1024, 1025, 2047, 2048, 2049, 3073, 4096 * 3 + 7, 50000])
+def test_build_parity_small(R, oracle, n):
+    _compare_build(R, oracle, soup(oracle, n, n))
+
+
+@pytest.mark.parametrize("n", [300000, 1000000])
+def test_build_parity_large(R, oracle, n):
+    _compare_build(R, oracle, soup(oracle, n, 1))
+
+
+def test_build_parity_10m_sparse_table_path(R, oracle):
+    """10M prims: 9766 refit blocks -> the global sparse-table crossing path."""
+    _compare_build(R, oracle, soup(oracle, 10_000_000, 1))
+
+
+def test_build_degenerate_inputs(R, oracle):
+    rng = np.random.default_rng(7)
+    one = soup(oracle, 1, 3)
+    _compare_build(R, oracle, np.tile(one, (5000, 1)))                     # all identical -> equal keys
+    flat = soup(oracle, 3000, 4).copy()
+    flat[:, 2::3] = 0.25                                                    # zero extent in z -> inv_z = 0
+    _compare_build(R, oracle, flat)
+    clustered = (rng.random((20000, 9)) * 1e-3).astype(np.float32)
+    clustered[:10] += 1000.0                                                # extreme outliers
+    _compare_build(R, oracle, clustered)
+    neg = -soup(oracle, 5000, 5)                                            # negative coordinates, -0
+    _compare_build(R, oracle, neg)
+
+
+def test_build_repeat_and_rebuild(R, oracle):
+    """Control words are re-armed between builds (zeroed per build)."""
+    tris = soup(oracle, 70000, 2)
+    exp = oracle.build(tris)
+    with R.Scene.from_soup(tris) as s:
+        for _ in range(3):
+            s.build()
+            got = s.read_bvh()
+            assert np.array_equal(got["vals"], exp["vals"])
+            assert np.array_equal(bits(got["nodes"]["lo"]), bits(exp["nodes"]["lo"]))
+
+
+# ------------------------------------------------------------------ render
+def _cam(R, view, w, h):
+    return R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+
+
+def _compare_render(R, oracle, tris, view, w, h, spp):
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    exp = oracle.build(tris)
+    cam = _cam(R, view, w, h)
+    ocam = oracle.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    ehits, ecnt = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
+    ergba = oracle.shade(ehits, w, h, spp)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        hits, rgba, _ = s.render(cam, w, h, spp)
+        cnt = s.render_counters(cam, w, h, spp)
+    assert np.array_equal(hits["prim"], ehits["prim"])
+    for f in ("t", "u", "v"):
+        assert np.array_equal(bits(hits[f]), bits(ehits[f])), f
+    assert np.array_equal(rgba, ergba)
+    assert cnt[0] == ecnt[0] and cnt[1] == ecnt[1]
+    return hits, cnt
+
+
+def test_render_golden_soup1024(R):
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    g = load_golden("soup1024.npz")
+    with R.Scene.from_soup(g["tris"]) as s:
+        s.build()
+        for (w, h, spp) in [(64, 48, 1), (32, 24, 3)]:
+            tag = f"r{w}x{h}x{spp}_"
+            cam = _cam(R, SOUP_VIEW, w, h)
+            assert np.array_equal(bits(R.camera_array(cam)), bits(g[tag + "cam"]))
+            hits, rgba, _ = s.render(cam, w, h, spp)
+            assert np.array_equal(hits["prim"], g[tag + "prim"])
+            for f in ("t", "u", "v"):
+                assert np.array_equal(bits(hits[f]), bits(g[tag + f]))
+            assert np.array_equal(rgba, g[tag + "rgba"])
+            cnt = s.render_counters(cam, w, h, spp)
+            assert np.array_equal(cnt, g[tag + "counters"])
+
+
+def test_render_golden_cornell(R):
+    from gpu_raytracer_amd.scenes import CORNELL_VIEW
+    g = load_golden("cornell.npz")
+    with R.Scene.from_soup(g["tris"]) as s:
+        s.build()
+        _, rgba, _ = s.render(_cam(R, CORNELL_VIEW, 256, 256), 256, 256, 1, hits=False)
+        assert np.array_equal(rgba, g["r256x256x1_rgba"])
+        hits, _, _ = s.render(_cam(R, CORNELL_VIEW, 64, 64), 64, 64, 1)
+        assert np.array_equal(hits["prim"], g["r64x64x1_prim"])
+        assert np.array_equal(bits(hits["t"]), bits(g["r64x64x1_t"]))
+
+
+def test_render_golden_edge(R):
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    g = load_golden("edge.npz")
+    for p, (w, h, spp) in [("n1_", (16, 16, 2)), ("n2_", (16, 16, 1)), ("dup64_", (16, 16, 1))]:
+        with R.Scene.from_soup(g[p + "tris"]) as s:
+            s.build()
+            hits, rgba, _ = s.render(_cam(R, SOUP_VIEW, w, h), w, h, spp)
+        tag = f"{p}r{w}x{h}x{spp}_"
+        assert np.array_equal(hits["prim"], g[tag + "prim"]) and np.array_equal(rgba, g[tag + "rgba"])
+        assert np.array_equal(bits(hits["t"]), bits(g[tag + "t"]))
+
+
+@pytest.mark.parametrize("n,w,h,spp", [(0, 16, 16, 1), (1, 33, 17, 1), (20000, 160, 90, 2), (100000, 257, 129, 1)])
+def test_render_parity(R, oracle, n, w, h, spp):
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    tris = soup(oracle, n, 5) if n else np.zeros((0, 9), np.float32)
+    hits, _ = _compare_render(R, oracle, tris, SOUP_VIEW, w, h, spp)
+    if n == 0:
+        assert np.all(hits["prim"] == SENT) and np.all(np.isinf(hits["t"]))
+
+
+def test_render_parity_presets(R, oracle):
+    from gpu_raytracer_amd import scenes as S
+    _compare_render(R, oracle, S.bunny_substitute_tris(), S.BUNNY_VIEW, 320, 180, 1)
+    _compare_render(R, oracle, S.sponza_substitute_tris(), S.SPONZA_VIEW, 192, 108, 2)
+
+
+def test_render_parity_headline_1m(R, oracle):
+    """configs[2] at full size: 1M soup, 1920x1080x1 -- every hit bit-exact."""
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    tris = soup(oracle, 1_000_000, 1)
+    hits, cnt = _compare_render(R, oracle, tris, SOUP_VIEW, 1920, 1080, 1)
+    assert (hits["prim"] != SENT).sum() > 500000
+    assert cnt[0] > 50_000_000
+
+
+def test_tiled_render_matches_full(R, oracle):
+    """Image-tile sharding (tile t -> rank t mod P) + unpack == one full render."""
+    import torch
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    tris = soup(oracle, 50000, 8)
+    w, h, spp = 200, 120, 2
+    cam = _cam(R, SOUP_VIEW, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        _, full, _ = s.render(cam, w, h, spp, hits=False)
+        for P in (1, 2, 3, 8):
+            tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
+            slabs = torch.zeros((P, max(tmax, 1) * 256), dtype=torch.int32, device="cuda")
+            for r in range(P):
+                s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr())
+            s.sync()
+            img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+            R.unpack_tiles_device(slabs.data_ptr(), tmax, w, h, P, img.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(img.cpu().numpy().view(np.uint8), full), P
