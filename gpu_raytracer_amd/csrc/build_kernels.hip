@@ -48,8 +48,8 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Stage `cnt` (<=256) AoS triangles starting at tri `base` into LDS.
-__device__ __forceinline__ void stage_tris(const float* __restrict__ tris, uint64_t base, uint32_t cnt, float4* stage) {
-    const float* src = tris + base * 9;
+__device__ __forceinline__ void stage_tris(const float* __restrict__ tris, uint32_t base, uint32_t cnt, float4* stage) {
+    const float* src = tris + (uint64_t)base * 9;
     if (cnt == 256) {  // 9216 B, 16-B aligned (base % 256 == 0)
         const float4* s4 = reinterpret_cast<const float4*>(src);
         for (int j = threadIdx.x; j < 576; j += 256) stage[j] = s4[j];
@@ -73,8 +73,9 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
     float lo[3], hi[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += (uint64_t)gridDim.x * 256) {
-        const uint32_t cnt = (uint32_t)min<uint64_t>(256, n - base);
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+        const uint32_t rem = n - base;
+        const uint32_t cnt = rem < 256u ? rem : 256u;
         stage_tris(tris, base, cnt, stage);
         __syncthreads();
         if (threadIdx.x < cnt) {
@@ -167,8 +168,9 @@ __global__ __launch_bounds__(256) void k_morton(const float* __restrict__ tris, 
     __shared__ uint32_t hist[4 * 256];
     for (int j = threadIdx.x; j < 1024; j += 256) hist[j] = 0u;
     const BuildParams p = *params;
-    for (uint64_t base = (uint64_t)blockIdx.x * 256; base < n; base += (uint64_t)gridDim.x * 256) {
-        const uint32_t cnt = (uint32_t)min<uint64_t>(256, n - base);
+    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+        const uint32_t rem = n - base;
+        const uint32_t cnt = rem < 256u ? rem : 256u;
         stage_tris(tris, base, cnt, stage);
         __syncthreads();
         if (threadIdx.x < cnt) {
@@ -179,9 +181,9 @@ __global__ __launch_bounds__(256) void k_morton(const float* __restrict__ tris, 
 #pragma unroll
             for (int c = 0; c < 3; ++c) q[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
             const uint32_t key = expand10(q[0]) * 4u + expand10(q[1]) * 2u + expand10(q[2]);
-            const uint64_t i = base + threadIdx.x;
+            const uint32_t i = base + threadIdx.x;
             keys[i] = key;
-            vals[i] = (uint32_t)i;
+            vals[i] = i;
 #pragma unroll
             for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((key >> (8 * d)) & 0xFFu)], 1u);
         }
@@ -232,12 +234,12 @@ __global__ __launch_bounds__(kSortThreads) void k_onesweep(const uint32_t* __res
     for (uint32_t j = tid; j < W * 256; j += kSortThreads) (&s_wc[0][0])[j] = 0u;
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint64_t base = (uint64_t)tile * kSortTile;
+    const uint32_t base = tile * (uint32_t)kSortTile;
 
     uint32_t k[kSortItems], v[kSortItems], r[kSortItems];
 #pragma unroll
     for (int i = 0; i < kSortItems; ++i) {
-        const uint64_t idx = base + (uint64_t)w * (64 * kSortItems) + i * 64 + l;
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
         const bool ok = idx < n;
         k[i] = ok ? kin[idx] : 0u;
         v[i] = ok ? vin[idx] : 0u;
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(kSortThreads) void k_onesweep(const uint32_t* __res
     // ---- stable per-wave ranking: order (i, lane) == original index order
 #pragma unroll
     for (int i = 0; i < kSortItems; ++i) {
-        const uint64_t idx = base + (uint64_t)w * (64 * kSortItems) + i * 64 + l;
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
         const bool ok = idx < n;
         const uint32_t d = (k[i] >> SHIFT) & 0xFFu;
         uint64_t peers = __ballot(ok);
@@ -301,7 +303,7 @@ __global__ __launch_bounds__(kSortThreads) void k_onesweep(const uint32_t* __res
     // ---- local scatter into LDS buckets
 #pragma unroll
     for (int i = 0; i < kSortItems; ++i) {
-        const uint64_t idx = base + (uint64_t)w * (64 * kSortItems) + i * 64 + l;
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
         if (idx < n) {
             const uint32_t dd = (k[i] >> SHIFT) & 0xFFu;
             const uint32_t pos = s_lstart[dd] + s_wc[w][dd] + r[i];
@@ -310,7 +312,8 @@ __global__ __launch_bounds__(kSortThreads) void k_onesweep(const uint32_t* __res
         }
     }
     __syncthreads();
-    const uint32_t tcount = (uint32_t)min<uint64_t>(kSortTile, n - base);
+    const uint32_t trem = n - base;
+    const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
 #pragma unroll
     for (int m = 0; m < kSortItems; ++m) {
         const uint32_t pidx = tid + m * kSortThreads;
@@ -430,9 +433,11 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(const float* __restrict
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t L0 = n - 1;
-    const uint64_t B0 = (uint64_t)blockIdx.x * T;
-    const uint64_t B1 = min<uint64_t>(B0 + T, n);
-    const uint64_t k = B0 + tid;
+    // 32-bit index math throughout (n <= 2^30): a 64-bit min() here was
+    // miscompiled by hipcc 7.2 (v_cmp_*_u64 + s_cselect on a stale SCC).
+    const uint32_t B0 = blockIdx.x * (uint32_t)T;
+    const uint32_t B1 = (n - B0) < (uint32_t)T ? n : B0 + (uint32_t)T;
+    const uint32_t k = B0 + tid;
     const bool valid = k < B1;
 
     Aabb box = aabb_empty();
@@ -581,7 +586,7 @@ __global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__
     __shared__ uint32_t hist[4 * 256];
     for (int j = threadIdx.x; j < 1024; j += 256) hist[j] = 0u;
     __syncthreads();
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
         const uint32_t key = keys[i];
 #pragma unroll
         for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((key >> (8 * d)) & 0xFFu)], 1u);
@@ -740,6 +745,8 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     if ((e = launch_sort(K, V, n, b.zero, s)) != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;
     if ((e = launch_karras(b.keys[0], n, b.topo, b.parent, b.lesc, s)) != hipSuccess) return e;
+    // n == 1: no internal node, K4 is not launched; the root is leaf 0.
+    if (n == 1 && (e = hipMemsetAsync(b.parent, 0xFF, 4, s)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
     if (n && (e = launch_refit(b, n, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
