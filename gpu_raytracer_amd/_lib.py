@@ -23,7 +23,8 @@ except Exception:  # pragma: no cover - torch is optional for the ABI itself
     _torch = None
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "librtamd.so")
+# RT_LIB overrides the library path (diagnostic stamp build, tools/diag_stamps.py)
+LIB_PATH = os.environ.get("RT_LIB") or os.path.join(PKG_DIR, "lib", "librtamd.so")
 
 RT_OK, RT_EINVAL, RT_ENOMEM, RT_EIO, RT_EDEVICE, RT_ECOMM = 0, -1, -2, -3, -4, -5
 SENTINEL = 0xFFFFFFFF

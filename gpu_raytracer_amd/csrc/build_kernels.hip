@@ -1,27 +1,27 @@
 // build_kernels.hip -- BVH build hot path for gfx950.
 //
-//   K0 k_bounds      centroid bounds (grid-stride, LDS-staged float4 loads of
-//                    the AoS soup) + last-block reduction -> BuildParams;
-//                    also zeroes the per-build control words (sort status,
-//                    tile tickets, digit histograms, crossing-list counter).
-//   K1 k_morton      Morton codes (§9.3) + the 4 global 8-bit digit histograms
-//                    (LDS histograms, one global atomic per non-empty bin).
-//   K2/K3 k_onesweep stable LSB radix sort, one launch per 8-bit digit:
-//                    wave64 ballot match-any ranking into LDS buckets, decoupled
-//                    look-back over per-tile digit counts (single 32-bit
-//                    {flag,count} words, relaxed agent-scope atomics: the data is
-//                    the flag), LDS-staged coalesced scatter.
-//   K4 k_karras      Karras 2012 topology (§9.5) + closed-form escape links
-//                    (§9.6) + parent pointers.
-//   K5/K6 k_refit_local  block-local bottom-up refit in LDS (leaf AABBs gathered
-//                    from the soup; LDS arrival counters; no inter-workgroup
-//                    traffic) + per-block prefix/suffix/total AABBs.
-//   K6 k_refit_cross nodes whose leaf range crosses a refit-block boundary:
-//                    union(suffix, middle blocks, prefix) -- exact, order-free.
-//
-// No kernel waits on another workgroup except the onesweep look-back (dynamic
-// tile ids make it deadlock-free) and K0's last-block hand-off (Guideline 16
-// recipe: release fence + ticket, acquire in the last block).
+//   K0 k_bounds         centroid bounds: 8 AoS triangles per thread as 18
+//                       independent 16-B loads, wave/LDS min-max, last-block
+//                       reduction (Guideline 16 release/ticket/acquire) ->
+//                       BuildParams {lo, hi, inv}.  Also zeroes the per-build
+//                       control words (digit histograms, crossing counters).
+//   K1 k_morton         Morton codes (§9.3); one block = one 4096-key sort tile,
+//                       so it also writes the tile's pass-0 digit counts and
+//                       adds the 4 global digit histograms (sort_kernels.hip).
+//   K2/K3               radix sort, sort_kernels.hip.
+//   K4 k_karras_leaves  Karras 2012 topology (§9.5) + closed-form escape links
+//                       (§9.6) + parent pointers for internal node i, and, in the
+//                       same thread, leaf i: gather of its triangle (independent
+//                       loads that overlap the binary-search latency), leaf node
+//                       {AABB, prim, esc} and the leaf-ordered {v0,e1,e2} record
+//                       the trace kernel reads.
+//   K6 k_refit_local    per 1024-leaf block: bottom-up refit of every internal
+//                       node whose leaf range lies in the block, in LDS only
+//                       (LDS arrival counters), plus block prefix/suffix/total
+//                       AABBs for the crossing nodes.
+//   K6 k_refit_cross    nodes whose range crosses a block boundary:
+//                       union(suffix, middle blocks, prefix) -- exact min/max,
+//                       so the result is independent of evaluation order.
 #include "rt_device.h"
 #include "rt_launch.h"
 
@@ -29,13 +29,11 @@
 
 namespace rt {
 
+#ifdef RT_STAMPS
+hipError_t read_stamps_build(void* out, size_t bytes) { return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stamps), bytes); }
+#endif
+
 // ---------------------------------------------------------------- helpers
-__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
-
-__device__ __forceinline__ uint32_t count_below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
 __device__ __forceinline__ float wave_min(float v) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
@@ -47,16 +45,31 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-// Stage `cnt` (<=256) AoS triangles starting at tri `base` into LDS.
-__device__ __forceinline__ void stage_tris(const float* __restrict__ tris, uint32_t base, uint32_t cnt, float4* stage) {
-    const float* src = tris + (uint64_t)base * 9;
-    if (cnt == 256) {  // 9216 B, 16-B aligned (base % 256 == 0)
-        const float4* s4 = reinterpret_cast<const float4*>(src);
-        for (int j = threadIdx.x; j < 576; j += 256) stage[j] = s4[j];
-    } else {
-        float* sf = reinterpret_cast<float*>(stage);
-        for (uint32_t j = threadIdx.x; j < cnt * 9; j += 256) sf[j] = src[j];
+// 8 consecutive AoS triangles (tris [8g, 8g+8)): 18 independent 16-B loads,
+// no LDS, no barrier.  A full group is 288 B, 16-B aligned.  Tail groups use
+// predicated scalar loads with compile-time register indices (no scratch).
+// All index math is 32-bit (n <= 2^30): a 64-bit min() of the tail size was
+// miscompiled by hipcc 7.2 (v_cmp_*_u64 feeding an s_cselect on a stale SCC).
+constexpr uint32_t kTrisPerThread = 8;
+
+__device__ __forceinline__ uint32_t load_tri8(const float* __restrict__ tris, uint32_t n, uint32_t g, float (&t)[72]) {
+    const uint32_t first = g * kTrisPerThread;
+    if (first + kTrisPerThread <= n) {
+        const float4* p = reinterpret_cast<const float4*>(tris + (uint64_t)first * 9);
+        float4 v[18];
+#pragma unroll
+        for (int j = 0; j < 18; ++j) v[j] = p[j];
+#pragma unroll
+        for (int j = 0; j < 18; ++j) {
+            t[4 * j] = v[j].x; t[4 * j + 1] = v[j].y; t[4 * j + 2] = v[j].z; t[4 * j + 3] = v[j].w;
+        }
+        return kTrisPerThread;
     }
+    const uint32_t cnt = first < n ? n - first : 0u;
+    const float* src = tris + (uint64_t)first * 9;
+#pragma unroll
+    for (int j = 0; j < 72; ++j) t[j] = ((uint32_t)j < cnt * 9u) ? src[j] : 0.0f;
+    return cnt;
 }
 
 // ---------------------------------------------------------------- K0
@@ -64,32 +77,29 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
                                                 float* __restrict__ partials, uint32_t* ticket,
                                                 BuildParams* __restrict__ params,
                                                 uint32_t* __restrict__ zero_words, uint32_t nzero) {
-    __shared__ float4 stage[576];
     __shared__ float red[4][6];
     __shared__ uint32_t s_last;
-    // zero the per-build control words (visible to K1.. after this launch)
-    for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < nzero; j += gridDim.x * 256) zero_words[j] = 0u;
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nzero; j += gridDim.x * 256u) zero_words[j] = 0u;
 
     float lo[3], hi[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
-    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
-        const uint32_t rem = n - base;
-        const uint32_t cnt = rem < 256u ? rem : 256u;
-        stage_tris(tris, base, cnt, stage);
-        __syncthreads();
-        if (threadIdx.x < cnt) {
-            const float* t = reinterpret_cast<const float*>(stage) + threadIdx.x * 9;
-            float bmin[3], bmax[3];
-            tri_bounds(t, bmin, bmax);
+    {
+        float t[72];
+        const uint32_t cnt = load_tri8(tris, n, blockIdx.x * 256u + threadIdx.x, t);
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float cc = (bmin[c] + bmax[c]) * 0.5f;
-                lo[c] = fminf(lo[c], cc);
-                hi[c] = fmaxf(hi[c], cc);
+        for (uint32_t q = 0; q < kTrisPerThread; ++q) {
+            if (q < cnt) {
+                float bmin[3], bmax[3];
+                tri_bounds(t + 9 * q, bmin, bmax);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float cc = (bmin[c] + bmax[c]) * 0.5f;
+                    lo[c] = fminf(lo[c], cc);
+                    hi[c] = fmaxf(hi[c], cc);
+                }
             }
         }
-        __syncthreads();
     }
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
@@ -111,8 +121,8 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
         // Guideline 16 producer: release (write back L2), explicit wait, ticket.
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (t == gridDim.x - 1) ? 1u : 0u;
+        const uint32_t tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (tk == gridDim.x - 1) ? 1u : 0u;
     }
     __syncthreads();
     if (!s_last) return;
@@ -160,174 +170,59 @@ __device__ __forceinline__ uint32_t quant(float c, float lo, float inv) {
     return (uint32_t)fminf(fmaxf(x, 0.0f), 1023.0f);
 }
 
-__global__ __launch_bounds__(256) void k_morton(const float* __restrict__ tris, uint32_t n,
-                                                const BuildParams* __restrict__ params,
-                                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
-                                                uint32_t* __restrict__ ghist /* [4][256] */) {
-    __shared__ float4 stage[576];
+// one block = one radix-sort tile: kSortThreads x kTrisPerThread = 4096 prims
+static_assert(kSortThreads * kTrisPerThread == kSortTile, "K1 block must be one sort tile");
+
+__global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict__ tris, uint32_t n,
+                                                         const BuildParams* __restrict__ params,
+                                                         uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
+                                                         uint32_t* __restrict__ ghist /* [4][256] */,
+                                                         uint32_t* __restrict__ counts0 /* [tile][256] */) {
     __shared__ uint32_t hist[4 * 256];
-    for (int j = threadIdx.x; j < 1024; j += 256) hist[j] = 0u;
+    for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) hist[j] = 0u;
     const BuildParams p = *params;
-    for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
-        const uint32_t rem = n - base;
-        const uint32_t cnt = rem < 256u ? rem : 256u;
-        stage_tris(tris, base, cnt, stage);
-        __syncthreads();
-        if (threadIdx.x < cnt) {
-            const float* t = reinterpret_cast<const float*>(stage) + threadIdx.x * 9;
-            float bmin[3], bmax[3];
-            tri_bounds(t, bmin, bmax);
-            uint32_t q[3];
+    const uint32_t g = blockIdx.x * (uint32_t)kSortThreads + threadIdx.x;
+    float t[72];
+    const uint32_t cnt = load_tri8(tris, n, g, t);
+    uint32_t k8[kTrisPerThread];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) q[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
-            const uint32_t key = expand10(q[0]) * 4u + expand10(q[1]) * 2u + expand10(q[2]);
-            const uint32_t i = base + threadIdx.x;
-            keys[i] = key;
-            vals[i] = i;
+    for (uint32_t q = 0; q < kTrisPerThread; ++q) {
+        float bmin[3], bmax[3];
+        tri_bounds(t + 9 * q, bmin, bmax);
+        uint32_t qq[3];
 #pragma unroll
-            for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((key >> (8 * d)) & 0xFFu)], 1u);
-        }
-        __syncthreads();
+        for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
+        k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
     }
-    for (int j = threadIdx.x; j < 1024; j += 256) {
+    const uint32_t first = g * kTrisPerThread;
+    if (cnt == kTrisPerThread) {
+        uint4* kp = reinterpret_cast<uint4*>(keys + first);
+        uint4* vp = reinterpret_cast<uint4*>(vals + first);
+        kp[0] = make_uint4(k8[0], k8[1], k8[2], k8[3]);
+        kp[1] = make_uint4(k8[4], k8[5], k8[6], k8[7]);
+        vp[0] = make_uint4(first, first + 1, first + 2, first + 3);
+        vp[1] = make_uint4(first + 4, first + 5, first + 6, first + 7);
+    } else {
+#pragma unroll
+        for (uint32_t q = 0; q < kTrisPerThread; ++q)
+            if (q < cnt) { keys[first + q] = k8[q]; vals[first + q] = first + q; }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < kTrisPerThread; ++q)
+        if (q < cnt) {
+#pragma unroll
+            for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((k8[q] >> (8 * d)) & 0xFFu)], 1u);
+        }
+    __syncthreads();
+    if (threadIdx.x < 256) counts0[(uint64_t)blockIdx.x * 256 + threadIdx.x] = hist[threadIdx.x];
+    for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) {
         const uint32_t v = hist[j];
         if (v) atomicAdd(&ghist[j], v);
     }
 }
 
-// ---------------------------------------------------------------- K2/K3 onesweep
-// 256-thread exclusive scan (4 waves); returns exclusive prefix, *total = sum.
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t* sw /* [4] */, uint32_t* total) {
-    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (l >= (uint32_t)o) x += y;
-    }
-    if (l == 63) sw[w] = x;
-    __syncthreads();
-    uint32_t pre = 0;
-    for (uint32_t k = 0; k < w; ++k) pre += sw[k];
-    *total = sw[0] + sw[1] + sw[2] + sw[3];
-    __syncthreads();
-    return pre + x - v;
-}
-
-template <int SHIFT>
-__global__ __launch_bounds__(kSortThreads) void k_onesweep(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
-                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                           uint32_t n, const uint32_t* __restrict__ ghist /* this digit's 256 bins */,
-                                                           uint32_t* status /* [256][ntiles] */, uint32_t ntiles,
-                                                           uint32_t* tile_ctr, uint32_t* err) {
-    constexpr int W = kSortThreads / 64;
-    __shared__ uint32_t s_wc[W][256];
-    __shared__ uint32_t s_key[kSortTile];
-    __shared__ uint32_t s_val[kSortTile];
-    __shared__ uint32_t s_lstart[256];
-    __shared__ uint32_t s_gofs[256];
-    __shared__ uint32_t s_sw[4];
-    __shared__ uint32_t s_tile;
-
-    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
-    for (uint32_t j = tid; j < W * 256; j += kSortThreads) (&s_wc[0][0])[j] = 0u;
-    __syncthreads();
-    const uint32_t tile = s_tile;
-    const uint32_t base = tile * (uint32_t)kSortTile;
-
-    uint32_t k[kSortItems], v[kSortItems], r[kSortItems];
-#pragma unroll
-    for (int i = 0; i < kSortItems; ++i) {
-        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
-        const bool ok = idx < n;
-        k[i] = ok ? kin[idx] : 0u;
-        v[i] = ok ? vin[idx] : 0u;
-    }
-    // ---- stable per-wave ranking: order (i, lane) == original index order
-#pragma unroll
-    for (int i = 0; i < kSortItems; ++i) {
-        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
-        const bool ok = idx < n;
-        const uint32_t d = (k[i] >> SHIFT) & 0xFFu;
-        uint64_t peers = __ballot(ok);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(ok && bit);
-            peers &= bit ? bal : ~bal;
-        }
-        const uint32_t below = count_below(peers);
-        const uint32_t cur = s_wc[w][d];
-        r[i] = cur + below;
-        if (ok && below == 0) s_wc[w][d] = cur + (uint32_t)__popcll(peers);
-    }
-    __syncthreads();
-    // ---- per-digit tile count, per-wave exclusive prefix (in place)
-    const uint32_t d = tid;  // kSortThreads == 256: one digit per thread
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int ww = 0; ww < W; ++ww) {
-        const uint32_t c = s_wc[ww][d];
-        s_wc[ww][d] = cnt;
-        cnt += c;
-    }
-    // publish this tile's aggregate as early as possible
-    uint32_t* st = status + (uint64_t)d * ntiles;
-    __hip_atomic_store(st + tile, (tile == 0 ? kFlagInc : kFlagAgg) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint32_t tot;
-    const uint32_t lstart = block_excl_scan256(cnt, s_sw, &tot);
-    s_lstart[d] = lstart;
-    const uint32_t dbase = block_excl_scan256(ghist[d], s_sw, &tot);
-    // ---- decoupled look-back for digit d
-    uint32_t excl = 0;
-    if (tile > 0) {
-        int64_t kk = (int64_t)tile - 1;
-        uint32_t spins = 0;
-        while (kk >= 0) {
-            const uint32_t s = __hip_atomic_load(st + kk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t flag = s & ~kCountMask;
-            if (flag == 0u) {
-                if (++spins > (1u << 22)) { atomicOr(err, 1u); break; }
-                __builtin_amdgcn_s_sleep(1);
-                continue;
-            }
-            excl += s & kCountMask;
-            if (flag == kFlagInc) break;
-            --kk;
-        }
-        __hip_atomic_store(st + tile, kFlagInc | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_gofs[d] = dbase + excl;
-    __syncthreads();
-    // ---- local scatter into LDS buckets
-#pragma unroll
-    for (int i = 0; i < kSortItems; ++i) {
-        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
-        if (idx < n) {
-            const uint32_t dd = (k[i] >> SHIFT) & 0xFFu;
-            const uint32_t pos = s_lstart[dd] + s_wc[w][dd] + r[i];
-            s_key[pos] = k[i];
-            s_val[pos] = v[i];
-        }
-    }
-    __syncthreads();
-    const uint32_t trem = n - base;
-    const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
-#pragma unroll
-    for (int m = 0; m < kSortItems; ++m) {
-        const uint32_t pidx = tid + m * kSortThreads;
-        if (pidx < tcount) {
-            const uint32_t key = s_key[pidx];
-            const uint32_t dd = (key >> SHIFT) & 0xFFu;
-            const uint32_t o = s_gofs[dd] + (pidx - s_lstart[dd]);
-            kout[o] = key;
-            vout[o] = s_val[pidx];
-        }
-    }
-}
-
-// ---------------------------------------------------------------- K4 Karras
+// ---------------------------------------------------------------- K4 (+K5)
 __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ keys, int64_t n, int64_t i, uint32_t ki, int64_t j) {
     if (j < 0 || j >= n) return -1;
     const uint32_t kj = keys[j];
@@ -340,48 +235,92 @@ __device__ __forceinline__ int kdir(const uint32_t* __restrict__ keys, int64_t n
     return (kdelta(keys, n, i, ki, i + 1) - kdelta(keys, n, i, ki, i - 1)) > 0 ? 1 : -1;
 }
 
-__global__ __launch_bounds__(256) void k_karras(const uint32_t* __restrict__ keys, uint32_t n,
-                                                uint4* __restrict__ topo, uint32_t* __restrict__ parent,
-                                                uint32_t* __restrict__ lesc) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int64_t N = n;
-    if (i >= N - 1) return;
-    const uint32_t L0 = n - 1;
-    const uint32_t ki = keys[i];
-    const int d = (kdelta(keys, N, i, ki, i + 1) - kdelta(keys, N, i, ki, i - 1)) > 0 ? 1 : -1;
-    const int dmin = kdelta(keys, N, i, ki, i - d);
-    int64_t lmax = 2;
-    while (kdelta(keys, N, i, ki, i + lmax * d) > dmin) lmax <<= 1;
-    int64_t l = 0;
-    for (int64_t t = lmax >> 1; t >= 1; t >>= 1)
-        if (kdelta(keys, N, i, ki, i + (l + t) * d) > dmin) l += t;
-    const int64_t j = i + l * d;
-    const int dnode = kdelta(keys, N, i, ki, j);
-    int64_t s = 0, t = l;
-    do {
-        t = (t + 1) >> 1;
-        if (kdelta(keys, N, i, ki, i + (s + t) * d) > dnode) s += t;
-    } while (t > 1);
-    const int64_t g = i + s * d + (d < 0 ? d : 0);
-    const int64_t mn = d > 0 ? i : j, mx = d > 0 ? j : i;
-    const uint32_t left = (mn == g) ? (uint32_t)(L0 + g) : (uint32_t)g;
-    const uint32_t right = (mx == g + 1) ? (uint32_t)(L0 + g + 1) : (uint32_t)(g + 1);
-    // §9.6 closed form: esc(node with range end r) = r == n-1 ? SENT
-    //   : (r+1 <= n-2 && dir(r+1) == +1) ? internal r+1 : leaf r+1
-    uint32_t esc;
-    if (mx == N - 1) esc = RT_SENT;
-    else if (mx + 1 <= N - 2 && kdir(keys, N, mx + 1) > 0) esc = (uint32_t)(mx + 1);
-    else esc = (uint32_t)(L0 + mx + 1);
-    topo[i] = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
-    parent[left] = (uint32_t)i;
-    parent[right] = (uint32_t)i;
-    if (i == 0) parent[0] = RT_SENT;
-    // leaf i-1 escapes to the right child of split i-1 == internal i iff dir(i) == +1
-    if (i >= 1) lesc[i - 1] = d > 0 ? (uint32_t)i : (uint32_t)(L0 + i);
-    if (i == N - 2) { lesc[N - 2] = L0 + (uint32_t)(N - 1); lesc[N - 1] = RT_SENT; }
+__device__ __forceinline__ void store_node(void* nodes, uint32_t idx, const Aabb& b, uint32_t a, uint32_t esc) {
+    float4* p = reinterpret_cast<float4*>(reinterpret_cast<char*>(nodes) + (uint64_t)idx * 32);
+    p[0] = make_float4(b.lo[0], b.lo[1], b.lo[2], b.hi[0]);
+    p[1] = make_float4(b.hi[1], b.hi[2], __uint_as_float(a), __uint_as_float(esc));
 }
 
-// ---------------------------------------------------------------- K5/K6 refit
+// Leaf-ordered triangle record for the trace kernel: {v0, e1 = v1-v0,
+// e2 = v2-v0} in three 16-B words.  The subtractions are the ones the
+// Moller-Trumbore test performs (§9.7), so precomputing them is bit-exact.
+__device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint32_t k, const float* t) {
+    float4* o = tri_s + (uint64_t)k * 3;
+    o[0] = make_float4(t[0], t[1], t[2], t[3] - t[0]);
+    o[1] = make_float4(t[4] - t[1], t[5] - t[2], t[6] - t[0], t[7] - t[1]);
+    o[2] = make_float4(t[8] - t[2], 0.0f, 0.0f, 0.0f);
+}
+
+// Thread i: internal node i (i < n-1) and leaf i (i < n).
+__global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ svals,
+                                                       const float* __restrict__ tris, uint32_t n,
+                                                       uint4* __restrict__ topo, uint32_t* __restrict__ parent,
+                                                       void* __restrict__ nodes, float4* __restrict__ tri_s) {
+    const uint32_t i32 = blockIdx.x * 256u + threadIdx.x;
+    if (i32 >= n) return;
+    const int64_t i = i32, N = n;
+    const uint32_t L0 = n - 1;
+    // leaf i's triangle: issue the gather first, consume it last
+    const uint32_t prim = svals[i32];
+    float tv[9];
+    const float* src = tris + (uint64_t)prim * 9;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) tv[c] = src[c];
+    if (i32 == 0) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
+    uint32_t lesc;
+    if (i < N - 1) {
+        const uint32_t ki = keys[i];
+        const int d = (kdelta(keys, N, i, ki, i + 1) - kdelta(keys, N, i, ki, i - 1)) > 0 ? 1 : -1;
+        const int dmin = kdelta(keys, N, i, ki, i - d);
+        int64_t lmax = 2;
+        while (kdelta(keys, N, i, ki, i + lmax * d) > dmin) lmax <<= 1;
+        int64_t l = 0;
+        for (int64_t t = lmax >> 1; t >= 1; t >>= 1)
+            if (kdelta(keys, N, i, ki, i + (l + t) * d) > dmin) l += t;
+        const int64_t j = i + l * d;
+        const int dnode = kdelta(keys, N, i, ki, j);
+        int64_t s = 0, t = l;
+        do {
+            t = (t + 1) >> 1;
+            if (kdelta(keys, N, i, ki, i + (s + t) * d) > dnode) s += t;
+        } while (t > 1);
+        const int64_t g = i + s * d + (d < 0 ? d : 0);
+        const int64_t mn = d > 0 ? i : j, mx = d > 0 ? j : i;
+        const uint32_t left = (mn == g) ? (uint32_t)(L0 + g) : (uint32_t)g;
+        const uint32_t right = (mx == g + 1) ? (uint32_t)(L0 + g + 1) : (uint32_t)(g + 1);
+        // §9.6 closed form: esc(node with range end r) = r == n-1 ? SENT
+        //   : (r+1 <= n-2 && dir(r+1) == +1) ? internal r+1 : leaf r+1
+        uint32_t esc;
+        if (mx == N - 1) esc = RT_SENT;
+        else if (mx + 1 <= N - 2 && kdir(keys, N, mx + 1) > 0) esc = (uint32_t)(mx + 1);
+        else esc = (uint32_t)(L0 + mx + 1);
+        topo[i] = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
+        parent[left] = i32;
+        parent[right] = i32;
+        // leaf i's range ends at i: same closed form with r = i
+        lesc = (i + 1 <= N - 2 && kdir(keys, N, i + 1) > 0) ? (uint32_t)(i + 1) : (uint32_t)(L0 + i + 1);
+    } else {
+        lesc = RT_SENT;  // leaf n-1
+    }
+    Aabb box;
+    tri_bounds(tv, box.lo, box.hi);
+    store_node(nodes, L0 + i32, box, prim, lesc);
+    store_leaf_tri(tri_s, i32, tv);
+}
+
+// Stand-alone leaf-triangle pass (rt_stage_trace on caller nodes).
+__global__ __launch_bounds__(256) void k_leaf_tris(const void* __restrict__ nodes, const float* __restrict__ tris,
+                                                   uint32_t n, float4* __restrict__ tri_s) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t prim = reinterpret_cast<const uint32_t*>(nodes)[((uint64_t)(n - 1) + k) * 8 + 6];
+    float t[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) t[c] = tris[(uint64_t)prim * 9 + c];
+    store_leaf_tri(tri_s, k, t);
+}
+
+// ---------------------------------------------------------------- K6 refit
 __device__ __forceinline__ void shfl_up_aabb(Aabb& a, int o) {
     Aabb b;
 #pragma unroll
@@ -393,12 +332,6 @@ __device__ __forceinline__ void shfl_down_aabb(Aabb& a, int o) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) { b.lo[c] = __shfl_down(a.lo[c], o, 64); b.hi[c] = __shfl_down(a.hi[c], o, 64); }
     if ((int)(threadIdx.x & 63) + o < 64) aabb_union(a, b);
-}
-
-__device__ __forceinline__ void store_node(void* nodes, uint32_t idx, const Aabb& b, uint32_t a, uint32_t esc) {
-    float4* p = reinterpret_cast<float4*>(reinterpret_cast<char*>(nodes) + (uint64_t)idx * 32);
-    p[0] = make_float4(b.lo[0], b.lo[1], b.lo[2], b.hi[0]);
-    p[1] = make_float4(b.hi[1], b.hi[2], __uint_as_float(a), __uint_as_float(esc));
 }
 
 __device__ __forceinline__ void store_aabb(float* buf, uint64_t idx, const Aabb& b) {
@@ -415,44 +348,40 @@ __device__ __forceinline__ Aabb load_aabb(const float* buf, uint64_t idx) {
 }
 
 // One block = kRefitT consecutive sorted leaves [B0, B1), one thread per leaf.
-__global__ __launch_bounds__(kRefitT) void k_refit_local(const float* __restrict__ tris, uint32_t n,
-                                                         const uint32_t* __restrict__ svals,
-                                                         const uint4* __restrict__ topo,
+__global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4* __restrict__ topo,
                                                          const uint32_t* __restrict__ parent,
-                                                         const uint32_t* __restrict__ lesc,
                                                          void* __restrict__ nodes,
                                                          float* __restrict__ prebuf, float* __restrict__ sufbuf,
                                                          float* __restrict__ totals,
-                                                         uint32_t* __restrict__ cross, uint32_t* cross_ctr) {
+                                                         uint32_t* __restrict__ cross, uint32_t* cross_ctr,
+                                                         uint32_t cross_cap) {
     constexpr int T = kRefitT, NW = T / 64;
     __shared__ Aabb s_box[2 * T];      // [0,T) leaves, [T,2T) internal nodes of the block
     __shared__ uint4 s_topo[T];
     __shared__ uint32_t s_par[2 * T];
     __shared__ uint32_t s_cnt[T];
     __shared__ Aabb s_wpre[NW], s_wsuf[NW];
+    __shared__ uint32_t s_ncross, s_cbase;
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t L0 = n - 1;
-    // 32-bit index math throughout (n <= 2^30): a 64-bit min() here was
-    // miscompiled by hipcc 7.2 (v_cmp_*_u64 + s_cselect on a stale SCC).
     const uint32_t B0 = blockIdx.x * (uint32_t)T;
     const uint32_t B1 = (n - B0) < (uint32_t)T ? n : B0 + (uint32_t)T;
     const uint32_t k = B0 + tid;
     const bool valid = k < B1;
+    uint32_t cslot = RT_SENT;
+    if (tid == 0) s_ncross = 0u;
+    RT_STAMP(0);
 
     Aabb box = aabb_empty();
     uint4 tp = make_uint4(0, 0, 0, 0);
     if (valid) {
-        const uint32_t prim = svals[k];
-        float t[9];
-        const float* src = tris + (uint64_t)prim * 9;
-#pragma unroll
-        for (int c = 0; c < 9; ++c) t[c] = src[c];
-        tri_bounds(t, box.lo, box.hi);
-        const uint32_t e = (k == n - 1) ? RT_SENT : lesc[k];
-        store_node(nodes, L0 + (uint32_t)k, box, prim, e);
+        const float4* np = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)(L0 + k) * 32);
+        const float4 A = np[0], B = np[1];
+        box.lo[0] = A.x; box.lo[1] = A.y; box.lo[2] = A.z;
+        box.hi[0] = A.w; box.hi[1] = B.x; box.hi[2] = B.y;
         s_box[tid] = box;
-        s_par[tid] = (n > 1) ? parent[L0 + k] : RT_SENT;
+        s_par[tid] = parent[L0 + k];
         if (k + 1 < n) {  // internal node k exists
             tp = topo[k];
             s_topo[tid] = tp;
@@ -460,6 +389,7 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(const float* __restrict
         }
     }
     s_cnt[tid] = 0u;
+    RT_STAMP(1);
     // ---- block prefix / suffix scans of leaf AABBs (exact min/max)
     Aabb pre = box, suf = box;
 #pragma unroll
@@ -470,47 +400,59 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(const float* __restrict
     for (uint32_t q = 0; q < wv; ++q) aabb_union(pre, s_wpre[q]);
     for (uint32_t q = wv + 1; q < NW; ++q) aabb_union(suf, s_wsuf[q]);
     if (valid) {
-        // crossing ends (see DESIGN.md "refit"): the topmost node starting at
-        // leaf k is internal k iff its range starts at k; the topmost node
-        // ending at k is internal k iff its range ends at k; the root ends at n-1.
+        // crossing ends (DESIGN.md "refit"): the topmost node starting at leaf
+        // k is internal k iff its range starts at k; the topmost node ending at
+        // k is internal k iff its range ends at k; the root ends at n-1.
         const bool has_int = k + 1 < n;
         const bool need_suf = has_int && tp.z == k && tp.w >= B1;
         const bool need_pre = (has_int && tp.w == k && tp.z < B0) || (k == n - 1 && B0 > 0);
         if (need_suf) store_aabb(sufbuf, k, suf);
         if (need_pre) store_aabb(prebuf, k, pre);
         if (k == B1 - 1) store_aabb(totals, blockIdx.x, pre);
-        if (has_int && (tp.z < B0 || tp.w >= B1)) {
-            const uint32_t slot = atomicAdd(cross_ctr, 1u);
-            cross[slot] = (uint32_t)k;
+        if (has_int && (tp.z < B0 || tp.w >= B1)) cslot = atomicAdd(&s_ncross, 1u);  // LDS
+    }
+    __syncthreads();
+    RT_STAMP(2);
+    // one aggregated reservation per block on one of kCrossShards counters
+    // (a single global counter hit by every wave serialises at ~90 ops/us)
+    if (tid == 0 && s_ncross)
+        s_cbase = (blockIdx.x % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[blockIdx.x % kCrossShards], s_ncross);
+    // ---- bottom-up climb inside the block, LDS only.  LDS instructions of a
+    // wave execute in order, so its s_box write lands before its own arrival
+    // add; the second arriver reads the sibling's box after its add returns.
+    // The asm statements only stop the compiler moving LDS accesses across
+    // the add (no global fence: node stores happen after the climb, coalesced).
+    if (valid && n > 1) {
+        uint32_t node = L0 + k;
+        uint32_t slot = tid;
+        for (uint32_t depth = 0; depth < (uint32_t)T; ++depth) {  // local depth < T
+            const uint32_t p = s_par[slot];
+            if (p == RT_SENT || p < B0 || p >= B1) break;
+            const uint4 pt = s_topo[p - B0];
+            if (pt.z < B0 || pt.w >= B1) break;  // p crosses the block: K6t's job
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const uint32_t old = __hip_atomic_fetch_add(&s_cnt[p - B0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            asm volatile("" ::: "memory");
+            if (old == 0u) break;  // first arrival: the sibling finishes p
+            const uint32_t left = pt.x;
+            const uint32_t g = left >= L0 ? left - L0 : left;
+            const uint32_t right = (pt.w == g + 1) ? L0 + g + 1 : g + 1;
+            const uint32_t sib = (left == node) ? right : left;
+            const uint32_t sslot = sib >= L0 ? (sib - L0 - B0) : (T + sib - B0);
+            aabb_union(box, s_box[sslot]);
+            slot = T + (p - B0);
+            s_box[slot] = box;
+            node = p;
         }
     }
     __syncthreads();
-    if (!valid || n == 1) return;
-    // ---- bottom-up climb inside the block (LDS arrival counters)
-    uint32_t node = L0 + (uint32_t)k;
-    uint32_t slot = tid;
-    for (uint32_t depth = 0; depth < (uint32_t)T; ++depth) {  // local depth < T
-        const uint32_t p = s_par[slot];
-        if (p == RT_SENT || p < B0 || p >= B1) break;
-        const uint4 pt = s_topo[p - B0];
-        if (pt.z < B0 || pt.w >= B1) break;  // p crosses the block: K6t's job
-        const uint32_t old = __hip_atomic_fetch_add(&s_cnt[p - B0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (old == 0u) break;  // first arrival: the sibling finishes p
-        const uint32_t left = pt.x;
-        const uint32_t g = left >= L0 ? left - L0 : left;
-        const uint32_t right = (pt.w == g + 1) ? L0 + g + 1 : g + 1;
-        const uint32_t sib = (left == node) ? right : left;
-        const uint32_t sslot = sib >= L0 ? (sib - L0 - (uint32_t)B0) : (T + sib - (uint32_t)B0);
-        aabb_union(box, s_box[sslot]);
-        slot = T + (p - (uint32_t)B0);
-        s_box[slot] = box;
-        store_node(nodes, p, box, pt.x, pt.y);
-        node = p;
-    }
+    RT_STAMP(3);
+    if (cslot != RT_SENT) cross[s_cbase + cslot] = k;
+    // ---- coalesced store of this block's local internal nodes [B0, B1)
+    if (valid && k + 1 < n && tp.z >= B0 && tp.w < B1) store_node(nodes, k, s_box[T + tid], tp.x, tp.y);
+    RT_STAMP(4);
 }
 
-// LDS segment tree over the M per-block totals (M <= kLdsTreeMaxBlocks) or a
-// global sparse table (levels built by k_sparse_level) for larger M.
 __global__ __launch_bounds__(256) void k_sparse_level(const float* __restrict__ src, float* __restrict__ dst, uint32_t m, uint32_t half) {
     const uint32_t b = blockIdx.x * 256 + threadIdx.x;
     if (b >= m) return;
@@ -519,13 +461,15 @@ __global__ __launch_bounds__(256) void k_sparse_level(const float* __restrict__ 
     store_aabb(dst, b, a);
 }
 
+// LDS segment tree over the M per-block totals (M <= kLdsTreeMaxBlocks) or a
+// global sparse table (levels built by k_sparse_level) for larger M.
 template <bool LDS_TREE>
 __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ topo,
                                                      const float* __restrict__ prebuf, const float* __restrict__ sufbuf,
                                                      const float* __restrict__ table /* totals, or sparse levels */,
                                                      uint32_t m, const uint32_t* __restrict__ cross,
-                                                     const uint32_t* __restrict__ cross_ctr, void* __restrict__ nodes,
-                                                     uint32_t n) {
+                                                     const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
+                                                     void* __restrict__ nodes, uint32_t n) {
     constexpr uint32_t T = kRefitT;
     extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
     Aabb* tree = reinterpret_cast<Aabb*>(s_raw);
@@ -543,9 +487,16 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
             __syncthreads();
         }
     }
-    const uint32_t count = *cross_ctr;
+    uint32_t pre[kCrossShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t sh = 0; sh < kCrossShards; ++sh) pre[sh + 1] = pre[sh] + cross_ctr[sh];
+    const uint32_t count = pre[kCrossShards];
     for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < count; q += gridDim.x * 256) {
-        const uint32_t i = cross[q];
+        uint32_t sh = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kCrossShards; ++j) sh += (q >= pre[j]) ? 1u : 0u;
+        const uint32_t i = cross[sh * cross_cap + (q - pre[sh])];
         const uint4 tp = topo[i];
         const uint32_t l = tp.z, r = tp.w;
         if (l >= n || r >= n || l > r) continue;  // malformed topology: never read out of bounds
@@ -573,35 +524,16 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
     }
 }
 
-template __global__ void k_onesweep<0>(const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t, const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*);
-template __global__ void k_onesweep<8>(const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t, const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*);
-template __global__ void k_onesweep<16>(const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t, const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*);
-template __global__ void k_onesweep<24>(const uint32_t*, const uint32_t*, uint32_t*, uint32_t*, uint32_t, const uint32_t*, uint32_t*, uint32_t, uint32_t*, uint32_t*);
-template __global__ void k_refit_cross<true>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, void*, uint32_t);
-template __global__ void k_refit_cross<false>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, void*, uint32_t);
-
-// Stand-alone digit histogram (rt_stage_sort on caller keys; the build fuses
-// this into K1).
-__global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t hist[4 * 256];
-    for (int j = threadIdx.x; j < 1024; j += 256) hist[j] = 0u;
-    __syncthreads();
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        const uint32_t key = keys[i];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((key >> (8 * d)) & 0xFFu)], 1u);
-    }
-    __syncthreads();
-    for (int j = threadIdx.x; j < 1024; j += 256) {
-        const uint32_t v = hist[j];
-        if (v) atomicAdd(&ghist[j], v);
-    }
-}
+template __global__ void k_refit_cross<true>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
+template __global__ void k_refit_cross<false>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
 
 // ================================================================ launchers
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
-uint32_t sort_tiles(uint32_t n) { return n ? cdiv(n, kSortTile) : 0u; }
+uint32_t bounds_grid(uint32_t n) { return n ? cdiv(n, 256 * kTrisPerThread) : 1u; }
+
+// crossing-list shard capacity: blocks b = s (mod S) each own <= kRefitT entries
+static uint32_t cross_cap(uint32_t m) { return cdiv(m, kCrossShards) * (uint32_t)kRefitT; }
 
 static uint32_t sparse_levels(uint32_t m) {
     uint32_t L = 1;
@@ -616,7 +548,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     b.ntiles = sort_tiles((uint32_t)N);
     b.m_blocks = cdiv(N, kRefitT);
     b.levels = sparse_levels(b.m_blocks);
-    b.nzero = kZStatus + 4u * 256u * b.ntiles;
+    b.nzero = kZEnd;
     hipError_t e;
 #define RT_ALLOC(ptr, bytes) \
     if ((e = hipMalloc((void**)&(ptr), (bytes))) != hipSuccess) { free_build(b); return e; }
@@ -626,14 +558,15 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.vals[0], N * 4);
     RT_ALLOC(b.vals[1], N * 4);
     RT_ALLOC(b.nodes, (2 * N - 1) * 32);
+    RT_ALLOC(b.tri_s, N * 48);
     RT_ALLOC(b.parent, (2 * N - 1) * 4);
     RT_ALLOC(b.topo, N * 16);
-    RT_ALLOC(b.lesc, N * 4);
     RT_ALLOC(b.prebuf, N * 24);
     RT_ALLOC(b.sufbuf, N * 24);
     RT_ALLOC(b.table, (uint64_t)b.levels * b.m_blocks * 24);
-    RT_ALLOC(b.cross, N * 4);
-    RT_ALLOC(b.partials, kBoundsGrid * 24);
+    RT_ALLOC(b.cross, (uint64_t)cross_cap(b.m_blocks) * kCrossShards * 4);
+    RT_ALLOC(b.counts, (uint64_t)4 * b.ntiles * 256 * 4);
+    RT_ALLOC(b.partials, (uint64_t)bounds_grid((uint32_t)N) * 24);
     RT_ALLOC(b.ticket, 256);
     RT_ALLOC(b.params, sizeof(BuildParams));
     RT_ALLOC(b.zero, (uint64_t)b.nzero * 4);
@@ -644,8 +577,8 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
 }
 
 void free_build(BuildBufs& b) {
-    void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.parent, b.topo, b.lesc,
-                  b.prebuf, b.sufbuf, b.table, b.cross, b.partials, b.ticket, b.params, b.zero};
+    void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.tri_s, b.parent, b.topo,
+                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.partials, b.ticket, b.params, b.zero};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = BuildBufs{};
@@ -653,55 +586,37 @@ void free_build(BuildBufs& b) {
 
 hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, uint32_t* ticket,
                               BuildParams* params, hipStream_t s) {
-    const uint32_t g = std::max(1u, std::min<uint32_t>(kBoundsGrid, cdiv(n, 256)));
-    hipLaunchKernelGGL(k_bounds, dim3(g), dim3(256), 0, s, tris, n, partials, ticket, params, (uint32_t*)nullptr, 0u);
+    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, tris, n, partials, ticket, params,
+                       (uint32_t*)nullptr, 0u);
     return hipGetLastError();
 }
 
 hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,
-                         uint32_t* vals, uint32_t* ghist, hipStream_t s) {
+                         uint32_t* vals, uint32_t* ghist, uint32_t* counts0, hipStream_t s) {
     if (!n) return hipSuccess;
-    const uint32_t g = std::min<uint32_t>(512, cdiv(n, 256));
-    hipLaunchKernelGGL(k_morton, dim3(g), dim3(256), 0, s, tris, n, params, keys, vals, ghist);
+    hipLaunchKernelGGL(k_morton, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, keys, vals, ghist,
+                       counts0);
     return hipGetLastError();
 }
 
-hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s) {
+hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, float4* tri_s, hipStream_t s) {
     if (!n) return hipSuccess;
-    const uint32_t g = std::min<uint32_t>(512, cdiv(n, 256));
-    hipLaunchKernelGGL(k_digit_hist, dim3(g), dim3(256), 0, s, keys, n, ghist);
+    hipLaunchKernelGGL(k_leaf_tris, dim3(cdiv(n, 256)), dim3(256), 0, s, nodes, tris, n, tri_s);
     return hipGetLastError();
 }
 
-// 4 onesweep passes, ping-pong 0->1->0->1->0; zero = control words (zeroed).
-hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, uint32_t* zero, hipStream_t s) {
-    if (n <= 1) return hipSuccess;
-    const uint32_t nt = sort_tiles(n);
-    uint32_t* hist = zero + kZHist;
-    uint32_t* st = zero + kZStatus;
-    const uint64_t sstride = 256ull * nt;
-    hipLaunchKernelGGL(k_onesweep<0>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n,
-                       hist + 0, st + 0 * sstride, nt, zero + kZTileCtr + 0, zero + kZErr);
-    hipLaunchKernelGGL(k_onesweep<8>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], vals[1], keys[0], vals[0], n,
-                       hist + 256, st + 1 * sstride, nt, zero + kZTileCtr + 1, zero + kZErr);
-    hipLaunchKernelGGL(k_onesweep<16>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n,
-                       hist + 512, st + 2 * sstride, nt, zero + kZTileCtr + 2, zero + kZErr);
-    hipLaunchKernelGGL(k_onesweep<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], vals[1], keys[0], vals[0], n,
-                       hist + 768, st + 3 * sstride, nt, zero + kZTileCtr + 3, zero + kZErr);
-    return hipGetLastError();
-}
-
-hipError_t launch_karras(const uint32_t* keys, uint32_t n, uint4* topo, uint32_t* parent, uint32_t* lesc,
-                         hipStream_t s) {
-    if (n < 2) return hipSuccess;
-    hipLaunchKernelGGL(k_karras, dim3(cdiv(n - 1, 256)), dim3(256), 0, s, keys, n, topo, parent, lesc);
+hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const float* tris, uint32_t n, uint4* topo,
+                         uint32_t* parent, void* nodes, float4* tri_s, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_karras_leaves, dim3(cdiv(n, 256)), dim3(256), 0, s, keys, svals, tris, n, topo, parent, nodes,
+                       tri_s);
     return hipGetLastError();
 }
 
 static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
-    hipLaunchKernelGGL(k_refit_local, dim3(m), dim3(kRefitT), 0, s, b.tris, n, b.vals[0], b.topo, b.parent, b.lesc,
-                       b.nodes, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr);
+    hipLaunchKernelGGL(k_refit_local, dim3(m), dim3(kRefitT), 0, s, n, b.topo, b.parent, b.nodes, b.prebuf, b.sufbuf,
+                       b.table, b.cross, b.zero + kZCrossCtr, cross_cap(m));
     if (m <= 1) return hipGetLastError();
     if (m <= (uint32_t)kLdsTreeMaxBlocks) {
         uint32_t P = 1;
@@ -716,7 +631,7 @@ static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
             attr_set = true;
         }
         hipLaunchKernelGGL(k_refit_cross<true>, dim3(64), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
-                           b.cross, b.zero + kZCrossCtr, b.nodes, n);
+                           b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
         const uint32_t L = sparse_levels(m);
         for (uint32_t lv = 1; lv < L; ++lv) {
@@ -724,7 +639,7 @@ static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
                                b.table + (uint64_t)lv * m * 6, m, 1u << (lv - 1));
         }
         hipLaunchKernelGGL(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
-                           b.cross, b.zero + kZCrossCtr, b.nodes, n);
+                           b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     return hipGetLastError();
 }
@@ -733,20 +648,21 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     hipError_t e;
     auto rec = [&](int i) -> hipError_t { return ev ? hipEventRecord(ev->e[i], s) : hipSuccess; };
     if ((e = rec(0)) != hipSuccess) return e;
-    const uint32_t g = std::max(1u, std::min<uint32_t>(kBoundsGrid, cdiv(n, 256)));
-    hipLaunchKernelGGL(k_bounds, dim3(g), dim3(256), 0, s, b.tris, n, b.partials, b.ticket, b.params, b.zero,
-                       kZStatus + 4u * 256u * sort_tiles(n));
+    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.ticket, b.params,
+                       b.zero, kZEnd);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = rec(1)) != hipSuccess) return e;
-    if ((e = launch_morton(b.tris, n, b.params, b.keys[0], b.vals[0], b.zero + kZHist, s)) != hipSuccess) return e;
+    const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
+    uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
+    if ((e = launch_morton(b.tris, n, b.params, b.keys[0], b.vals[0], b.zero + kZHist, counts[0], s)) != hipSuccess)
+        return e;
     if ((e = rec(2)) != hipSuccess) return e;
     uint32_t* K[2] = {b.keys[0], b.keys[1]};
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
-    if ((e = launch_sort(K, V, n, b.zero, s)) != hipSuccess) return e;
+    if ((e = launch_sort(K, V, n, b.zero + kZHist, counts, s)) != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;
-    if ((e = launch_karras(b.keys[0], n, b.topo, b.parent, b.lesc, s)) != hipSuccess) return e;
-    // n == 1: no internal node, K4 is not launched; the root is leaf 0.
-    if (n == 1 && (e = hipMemsetAsync(b.parent, 0xFF, 4, s)) != hipSuccess) return e;
+    if ((e = launch_karras(b.keys[0], b.vals[0], b.tris, n, b.topo, b.parent, b.nodes, b.tri_s, s)) != hipSuccess)
+        return e;
     if ((e = rec(4)) != hipSuccess) return e;
     if (n && (e = launch_refit(b, n, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;

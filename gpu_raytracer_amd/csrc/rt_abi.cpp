@@ -269,9 +269,6 @@ rt_status rt_bvh_build(rt_scene* s, double* ms_out) {
     hipError_t e = rt::launch_build(s->bufs, s->n, s->stream, &s->ev);
     if (e != hipSuccess) return hip_fail(e, "launch_build");
     HIPR(hipStreamSynchronize(s->stream));
-    uint32_t err = 0;
-    HIPR(hipMemcpy(&err, s->bufs.zero + rt::kZErr, 4, hipMemcpyDeviceToHost));
-    if (err) return fail(RT_EDEVICE, "radix-sort look-back timed out (device error flag set)");
     float t[5];
     for (int i = 0; i < 5; ++i) HIPR(hipEventElapsedTime(&t[i], s->ev.e[i], s->ev.e[i + 1]));
     s->times.bounds = t[0];
@@ -321,7 +318,7 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     if (hits_out && (st = grow(&s->d_hits, &s->hits_cap, nh * 16))) return st;
     if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
     HIPR(hipEventRecord(s->r0, s->stream));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tris, s->n, camf(cam), w, h, spp, 0, 1, false,
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
                                     hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipEventRecord(s->r1, s->stream));
@@ -343,7 +340,7 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     if (st) return st;
     if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 16));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tris, s->n, camf(cam), w, h, spp, rank, nranks, packed,
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks, packed,
                                     nullptr, nullptr, s->d_ctr, s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(s->stream));
@@ -370,7 +367,7 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     if (st) return st;
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tris, s->n, camf(cam), w, h, spp, 0, 1, false, d_hits,
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false, d_hits,
                                     d_rgba, nullptr, hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     if (ms_out) {
@@ -396,7 +393,7 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     if (st) return st;
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tris, s->n, camf(cam), w, h, spp, rank, nranks, true,
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks, true,
                                     d_packed_hits, d_packed_rgba, nullptr, hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     if (ms_out) {
@@ -426,7 +423,7 @@ rt_status rt_stage_bounds(int device, const float* tris, uint32_t n, float bound
     if (st) return st;
     DevBuf dt, dp, dk, dpar;
     HIPR(dt.alloc((size_t)n * 36));
-    HIPR(dp.alloc(rt::kBoundsGrid * 24));
+    HIPR(dp.alloc((size_t)rt::bounds_grid(n) * 24));
     HIPR(dk.alloc(256));
     HIPR(dpar.alloc(sizeof(rt::BuildParams)));
     HIPR(hipMemset(dk.p, 0, 256));
@@ -443,19 +440,20 @@ rt_status rt_stage_morton(int device, const float* tris, uint32_t n, const float
     rt_status st = ensure_device(device);
     if (st) return st;
     if (!n) return RT_OK;
-    DevBuf dt, dpar, dk, dv, dh;
+    DevBuf dt, dpar, dk, dv, dh, dc;
     HIPR(dt.alloc((size_t)n * 36));
     HIPR(dpar.alloc(sizeof(rt::BuildParams)));
     HIPR(dk.alloc((size_t)n * 4));
     HIPR(dv.alloc((size_t)n * 4));
     HIPR(dh.alloc(4096));
+    HIPR(dc.alloc((size_t)rt::sort_tiles(n) * 1024));
     HIPR(hipMemset(dh.p, 0, 4096));
     rt::BuildParams p{};
     for (int c = 0; c < 3; ++c) { p.lo[c] = lo[c]; p.inv[c] = inv[c]; }
     HIPR(hipMemcpy(dpar.p, &p, sizeof(p), hipMemcpyHostToDevice));
     HIPR(hipMemcpy(dt.p, tris, (size_t)n * 36, hipMemcpyHostToDevice));
     HIPR(rt::launch_morton(dt.as<float>(), n, dpar.as<rt::BuildParams>(), dk.as<uint32_t>(), dv.as<uint32_t>(),
-                           dh.as<uint32_t>(), 0));
+                           dh.as<uint32_t>(), dc.as<uint32_t>(), 0));
     HIPR(hipDeviceSynchronize());
     HIPR(hipMemcpy(keys, dk.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     HIPR(hipMemcpy(vals, dv.p, (size_t)n * 4, hipMemcpyDeviceToHost));
@@ -468,24 +466,25 @@ rt_status rt_stage_sort(int device, uint32_t* keys, uint32_t* vals, uint32_t n) 
     rt_status st = ensure_device(device);
     if (st) return st;
     if (n <= 1) return RT_OK;
-    DevBuf k0, k1, v0, v1, z;
-    const size_t nz = rt::kZStatus + 4ull * 256 * rt::sort_tiles(n);
+    DevBuf k0, k1, v0, v1, gh, cnt;
+    const size_t cs = (size_t)rt::sort_tiles(n) * 256;
     HIPR(k0.alloc((size_t)n * 4));
     HIPR(k1.alloc((size_t)n * 4));
     HIPR(v0.alloc((size_t)n * 4));
     HIPR(v1.alloc((size_t)n * 4));
-    HIPR(z.alloc(nz * 4));
-    HIPR(hipMemset(z.p, 0, nz * 4));
+    HIPR(gh.alloc(4096));
+    HIPR(cnt.alloc(4 * cs * 4));
+    HIPR(hipMemset(gh.p, 0, 4096));
     HIPR(hipMemcpy(k0.p, keys, (size_t)n * 4, hipMemcpyHostToDevice));
     HIPR(hipMemcpy(v0.p, vals, (size_t)n * 4, hipMemcpyHostToDevice));
-    HIPR(rt::launch_digit_hist(k0.as<uint32_t>(), n, z.as<uint32_t>() + rt::kZHist, 0));
+    uint32_t* C[4] = {cnt.as<uint32_t>(), cnt.as<uint32_t>() + cs, cnt.as<uint32_t>() + 2 * cs,
+                      cnt.as<uint32_t>() + 3 * cs};
+    HIPR(rt::launch_digit_hist(k0.as<uint32_t>(), n, gh.as<uint32_t>(), 0));
+    HIPR(rt::launch_tile_hist0(k0.as<uint32_t>(), n, C[0], 0));
     uint32_t* K[2] = {k0.as<uint32_t>(), k1.as<uint32_t>()};
     uint32_t* V[2] = {v0.as<uint32_t>(), v1.as<uint32_t>()};
-    HIPR(rt::launch_sort(K, V, n, z.as<uint32_t>(), 0));
+    HIPR(rt::launch_sort(K, V, n, gh.as<uint32_t>(), C, 0));
     HIPR(hipDeviceSynchronize());
-    uint32_t err = 0;
-    HIPR(hipMemcpy(&err, z.as<uint32_t>() + rt::kZErr, 4, hipMemcpyDeviceToHost));
-    if (err) return fail(RT_EDEVICE, "radix-sort look-back timed out");
     HIPR(hipMemcpy(keys, k0.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     HIPR(hipMemcpy(vals, v0.p, (size_t)n * 4, hipMemcpyDeviceToHost));
     return RT_OK;
@@ -496,24 +495,31 @@ rt_status rt_stage_topology(int device, const uint32_t* sorted_keys, uint32_t n,
     if (n && !sorted_keys) return fail(RT_EINVAL, "null argument");
     rt_status st = ensure_device(device);
     if (st) return st;
-    if (n < 2) {
-        if (n == 1) {
-            if (parent) parent[0] = RT_SENTINEL;
-            if (leaf_esc) leaf_esc[0] = RT_SENTINEL;
-        }
-        return RT_OK;
-    }
-    DevBuf dk, dt, dp, dl;
+    if (!n) return RT_OK;
+    // K4 also emits the leaves; feed it identity indices and a zero soup
+    DevBuf dk, dv, dtr, dt, dp, dn, dts;
     HIPR(dk.alloc((size_t)n * 4));
-    HIPR(dt.alloc((size_t)(n - 1) * 16));
+    HIPR(dv.alloc((size_t)n * 4));
+    HIPR(dtr.alloc((size_t)n * 36));
+    HIPR(dt.alloc((size_t)n * 16));
     HIPR(dp.alloc((size_t)(2 * n - 1) * 4));
-    HIPR(dl.alloc((size_t)n * 4));
+    HIPR(dn.alloc((size_t)(2 * n - 1) * 32));
+    HIPR(dts.alloc((size_t)n * 48));
+    std::vector<uint32_t> iota(n);
+    for (uint32_t i = 0; i < n; ++i) iota[i] = i;
     HIPR(hipMemcpy(dk.p, sorted_keys, (size_t)n * 4, hipMemcpyHostToDevice));
-    HIPR(rt::launch_karras(dk.as<uint32_t>(), n, dt.as<uint4>(), dp.as<uint32_t>(), dl.as<uint32_t>(), 0));
+    HIPR(hipMemcpy(dv.p, iota.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPR(hipMemset(dtr.p, 0, (size_t)n * 36));
+    HIPR(rt::launch_karras(dk.as<uint32_t>(), dv.as<uint32_t>(), dtr.as<float>(), n, dt.as<uint4>(), dp.as<uint32_t>(),
+                           dn.p, dts.as<float4>(), 0));
     HIPR(hipDeviceSynchronize());
-    if (topo) HIPR(hipMemcpy(topo, dt.p, (size_t)(n - 1) * 16, hipMemcpyDeviceToHost));
+    if (topo && n > 1) HIPR(hipMemcpy(topo, dt.p, (size_t)(n - 1) * 16, hipMemcpyDeviceToHost));
     if (parent) HIPR(hipMemcpy(parent, dp.p, (size_t)(2 * n - 1) * 4, hipMemcpyDeviceToHost));
-    if (leaf_esc) HIPR(hipMemcpy(leaf_esc, dl.p, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (leaf_esc) {
+        std::vector<uint32_t> nd((size_t)n * 8);
+        HIPR(hipMemcpy(nd.data(), (char*)dn.p + (size_t)(n - 1) * 32, (size_t)n * 32, hipMemcpyDeviceToHost));
+        for (uint32_t k = 0; k < n; ++k) leaf_esc[k] = nd[(size_t)k * 8 + 7];
+    }
     return RT_OK;
 }
 
@@ -534,7 +540,10 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
         HIPR(hipMemcpy(dn.p, nodes, tot * 32, hipMemcpyHostToDevice));
         HIPR(hipMemcpy(dt.p, tris, (size_t)n * 36, hipMemcpyHostToDevice));
     }
-    HIPR(rt::launch_trace(dn.p, dt.as<float>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
+    DevBuf dts;
+    HIPR(dts.alloc((size_t)(n ? n : 1) * 48));
+    HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
+    HIPR(rt::launch_trace(dn.p, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
                           counters ? dc.as<unsigned long long>() : nullptr, 0));
     HIPR(hipDeviceSynchronize());
     if (hits) HIPR(hipMemcpy(hits, dh.p, nh * 16, hipMemcpyDeviceToHost));
@@ -610,5 +619,15 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path) {
     if (std::fclose(f) != 0) ok = false;
     return ok ? RT_OK : fail(RT_EIO, std::string("write failed: ") + path);
 }
+
+#ifdef RT_STAMPS
+// diagnostic build only: copy the per-block phase stamps (8 x u64 per block)
+// of the build kernels (which = 0) or the sort kernels (which = 1)
+rt_status rt_debug_stamps(int which, void* out, size_t bytes) {
+    HIPR(hipDeviceSynchronize());
+    HIPR(which ? rt::read_stamps_sort(out, bytes) : rt::read_stamps_build(out, bytes));
+    return RT_OK;
+}
+#endif
 
 }  // extern "C"

@@ -65,15 +65,35 @@ struct BuildParams {
 };
 
 // Morton/sort geometry shared by host and device.
-constexpr int kSortThreads = 256;
-constexpr int kSortItems = 16;
+constexpr int kSortThreads = 512;
+constexpr int kSortItems = 8;
 constexpr int kSortTile = kSortThreads * kSortItems;   // 4096 keys / tile
+constexpr uint32_t kPrefixInKernelMaxTiles = 256;      // <= 1M keys: cross-tile prefix inside k_scatter
 constexpr int kRefitT = 1024;                          // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
 
-// Onesweep decoupled look-back status word: [31:30] flag, [29:0] count.
-constexpr uint32_t kFlagAgg = 1u << 30;
-constexpr uint32_t kFlagInc = 2u << 30;
-constexpr uint32_t kCountMask = (1u << 30) - 1u;
 
 }  // namespace rt
+
+// ---- diagnostic phase stamps (separate -DRT_STAMPS build only; the shipped
+// library executes none).  Thread 0 of each block writes s_memrealtime
+// (100 MHz, chip-wide clock) into slot s of its 8-word record.
+#ifdef RT_STAMPS
+// one stamp array per translation unit (no relocatable device code)
+static __device__ unsigned long long g_rt_stamps[1u << 20];
+#define RT_STAMP(s)                                                          \
+    do {                                                                     \
+        if (threadIdx.x == 0) {                                              \
+            __builtin_amdgcn_sched_barrier(0);                               \
+            g_rt_stamps[(uint64_t)blockIdx.x * 8 + (s)] = __builtin_amdgcn_s_memrealtime(); \
+            __builtin_amdgcn_sched_barrier(0);                               \
+        }                                                                    \
+    } while (0)
+#define RT_STAMP_VAL(s, v)                                                   \
+    do {                                                                     \
+        if (threadIdx.x == 0) g_rt_stamps[(uint64_t)blockIdx.x * 8 + (s)] = (v); \
+    } while (0)
+#else
+#define RT_STAMP(s) do {} while (0)
+#define RT_STAMP_VAL(s, v) do {} while (0)
+#endif

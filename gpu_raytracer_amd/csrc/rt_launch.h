@@ -17,9 +17,10 @@ struct BuildBufs {
     uint32_t* keys[2] = {nullptr, nullptr};
     uint32_t* vals[2] = {nullptr, nullptr};
     void* nodes = nullptr;          // (2n-1) x 32 B {lo[3], hi[3], a, esc}
+    float4* tri_s = nullptr;        // n x 48 B leaf-ordered {v0, e1, e2} for the trace
     uint32_t* parent = nullptr;     // 2n-1, unified index space
     uint4* topo = nullptr;          // n-1 x {left, esc, range_lo, range_hi}
-    uint32_t* lesc = nullptr;       // n leaf escape links
+    uint32_t* counts = nullptr;     // 4 x [tile][256] radix-sort tile digit counts
     float* prebuf = nullptr;        // n x 6: block-prefix AABB at crossing ends
     float* sufbuf = nullptr;        // n x 6: block-suffix AABB at crossing ends
     float* table = nullptr;         // sparse table over refit-block totals, levels x M x 6
@@ -37,11 +38,11 @@ struct BuildBufs {
 // zero region layout (uint32 words)
 constexpr uint32_t kZHist = 0;          // [4][256] digit histograms
 constexpr uint32_t kZTileCtr = 1024;    // [4] onesweep tile tickets
-constexpr uint32_t kZCrossCtr = 1028;   // crossing-list length
-constexpr uint32_t kZErr = 1029;        // sticky error bits (look-back timeout)
-constexpr uint32_t kZStatus = 1040;     // [4][256][ntiles] look-back words
+constexpr uint32_t kZErr = 1028;        // sticky error bits (reserved)
+constexpr uint32_t kZCrossCtr = 1040;   // [kCrossShards] crossing-list shard lengths
+constexpr uint32_t kCrossShards = 16;
+constexpr uint32_t kZEnd = 1056;        // words zeroed by K0 every build
 
-constexpr uint32_t kBoundsGrid = 1024;
 
 hipError_t alloc_build(BuildBufs& b, uint32_t n);
 void free_build(BuildBufs& b);
@@ -56,16 +57,22 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, Buil
 hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, uint32_t* ticket,
                               BuildParams* params, hipStream_t s);
 hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,
-                         uint32_t* vals, uint32_t* ghist, hipStream_t s);
+                         uint32_t* vals, uint32_t* ghist, uint32_t* counts0, hipStream_t s);
 hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s);
-hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, uint32_t* zero, hipStream_t s);
-hipError_t launch_karras(const uint32_t* keys, uint32_t n, uint4* topo, uint32_t* parent, uint32_t* lesc,
-                         hipStream_t s);
+hipError_t launch_tile_hist0(const uint32_t* keys, uint32_t n, uint32_t* counts0, hipStream_t s);
+// 4 passes 0->1->0->1->0; ghist = [4][256] digit totals; counts[p] = [tile][256]
+// (counts[0] filled by K1 or launch_tile_hist0, counts[1..3] scratch).
+hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts[4],
+                       hipStream_t s);
+hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const float* tris, uint32_t n, uint4* topo,
+                         uint32_t* parent, void* nodes, float4* tri_s, hipStream_t s);
 uint32_t sort_tiles(uint32_t n);
+uint32_t bounds_grid(uint32_t n);  // K0/K1 workgroups (8 tris per thread)
+hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, float4* tri_s, hipStream_t s);
 
 struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 
-hipError_t launch_trace(const void* nodes, const float* tris, uint32_t n, const CamF& cam, uint32_t w,
+hipError_t launch_trace(const void* nodes, const float4* tri_s, uint32_t n, const CamF& cam, uint32_t w,
                         uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
                         void* hits, void* rgba, unsigned long long* counters, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
@@ -73,6 +80,10 @@ hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w,
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);
 hipError_t launch_intersect(uint32_t count, const float* o, const float* d, const float* tri, const float* tb,
                             uint32_t* hit, float* tuv, hipStream_t s);
+#ifdef RT_STAMPS
+hipError_t read_stamps_build(void* out, size_t bytes);
+hipError_t read_stamps_sort(void* out, size_t bytes);
+#endif
 hipError_t launch_minmax(uint32_t count, const float* a, const float* b, float* out, hipStream_t s);
 
 }  // namespace rt

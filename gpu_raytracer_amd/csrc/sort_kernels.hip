@@ -1,0 +1,308 @@
+// sort_kernels.hip -- stable 32-bit LSB radix sort (4 x 8-bit digits) of
+// Morton key / prim-index pairs for gfx950 (§9.4).
+//
+// Per digit pass, two launches and no intra-launch inter-workgroup traffic:
+//   k_tile_hist<S>  per-tile (4096 keys) digit counts -> counts[tile][256]
+//                   (pass 0's counts come from K1, whose block is one tile)
+//   k_scatter<S>    ranks the tile's keys stably (wave64 ballot match-any,
+//                   per-wave LDS digit counters), buckets them in LDS, then
+//                   writes each digit run coalesced to
+//                   digit_base[d] + sum_{tiles i < t} counts[i][d] + local.
+// digit_base comes from the 4 global histograms K1 builds once (exact
+// totals for every pass).  The cross-tile prefix is summed inside the
+// scatter kernel from plain loads of the previous launch's counts (<= 256
+// tiles, i.e. <= 1M keys); above that k_scan_tiles turns counts into
+// exclusive offsets first.  Why not single-pass decoupled look-back: every
+// poll of another CU's status word is a device-scope (L2-bypassing) load, and
+// the measured chain cost ~2.5 us per hop on MI355X (tools/diag_stamps.py).
+#include "rt_device.h"
+#include "rt_launch.h"
+
+#include <algorithm>
+
+namespace rt {
+
+#ifdef RT_STAMPS
+hipError_t read_stamps_sort(void* out, size_t bytes) { return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stamps), bytes); }
+#endif
+
+__device__ __forceinline__ uint32_t sort_count_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// exclusive scan of one value per thread over threads [0,256) of a block of
+// kSortThreads (others pass 0); returns the prefix for threads < 256.
+__device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* sw /* [4] */) {
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    if (l == 63 && w < 4) sw[w] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t k = 0; k < w && k < 4; ++k) pre += sw[k];
+    __syncthreads();
+    return pre + x - v;
+}
+
+// ---------------------------------------------------------------- histogram
+template <int SHIFT>
+__global__ __launch_bounds__(kSortThreads) void k_tile_hist(const uint32_t* __restrict__ keys, uint32_t n,
+                                                            uint32_t* __restrict__ counts /* [tile][256] */) {
+    __shared__ uint32_t h[256];
+    if (threadIdx.x < 256) h[threadIdx.x] = 0u;
+    __syncthreads();
+    const uint32_t base = blockIdx.x * (uint32_t)kSortTile + threadIdx.x * (uint32_t)kSortItems;
+    if (base + kSortItems <= n) {
+        const uint4* p = reinterpret_cast<const uint4*>(keys + base);
+        const uint4 a = p[0], b = p[1];
+        const uint32_t k[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int i = 0; i < 8; ++i) atomicAdd(&h[(k[i] >> SHIFT) & 0xFFu], 1u);
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < (uint32_t)kSortItems; ++i)
+            if (base + i < n) atomicAdd(&h[(keys[base + i] >> SHIFT) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) counts[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+}
+
+// In-place exclusive scan of counts[tile][d] over tiles, one workgroup per
+// digit (used when tiles > kPrefixInKernelMaxTiles).
+__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ counts, uint32_t ntiles) {
+    __shared__ uint32_t sw[4];
+    __shared__ uint32_t s_carry;
+    const uint32_t d = blockIdx.x;
+    if (threadIdx.x == 0) s_carry = 0u;
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 256 * 8) {
+        uint32_t v[8], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t i = c0 + threadIdx.x * 8 + j;
+            v[j] = i < ntiles ? counts[(uint64_t)i * 256 + d] : 0u;
+            sum += v[j];
+        }
+        const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (l >= (uint32_t)o) x += y;
+        }
+        if (l == 63) sw[w] = x;
+        __syncthreads();
+        uint32_t pre = s_carry;
+        for (uint32_t k = 0; k < w; ++k) pre += sw[k];
+        pre += x - sum;
+        const uint32_t total = sw[0] + sw[1] + sw[2] + sw[3];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const uint32_t i = c0 + threadIdx.x * 8 + j;
+            if (i < ntiles) counts[(uint64_t)i * 256 + d] = pre;
+            pre += v[j];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_carry += total;
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------- scatter
+template <int SHIFT, bool PREFIX_IN_KERNEL>
+__global__ __launch_bounds__(kSortThreads) void k_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                          uint32_t n, const uint32_t* __restrict__ ghist /* this digit's 256 */,
+                                                          const uint32_t* __restrict__ counts /* [tile][256] counts or offsets */) {
+    constexpr int W = kSortThreads / 64;  // 8 waves
+    __shared__ uint32_t s_wc[W][256];
+    __shared__ uint32_t s_key[kSortTile];
+    __shared__ uint32_t s_val[kSortTile];
+    __shared__ uint32_t s_lstart[256];
+    __shared__ uint32_t s_gofs[256];
+    __shared__ uint32_t s_part[8][256];
+    __shared__ uint32_t s_sw[4];
+
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t base = tile * (uint32_t)kSortTile;
+    RT_STAMP(0);
+    for (uint32_t j = tid; j < W * 256; j += kSortThreads) (&s_wc[0][0])[j] = 0u;
+
+    // ---- cross-tile prefix of this tile's digit offsets (independent of the
+    // ranking below: issue it first so its loads overlap the key loads)
+    uint4 part = make_uint4(0, 0, 0, 0);
+    if (PREFIX_IN_KERNEL) {
+        // thread t: digits 4q..4q+3 (q = t & 63), tiles i = p (mod 8) (p = t >> 6)
+        const uint32_t q = tid & 63, p = tid >> 6;
+        const uint4* c4 = reinterpret_cast<const uint4*>(counts);
+        for (uint32_t i = p; i < tile; i += 8 * 4) {
+            uint4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t ii = i + 8 * u;
+                v[u] = ii < tile ? c4[(uint64_t)ii * 64 + q] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) { part.x += v[u].x; part.y += v[u].y; part.z += v[u].z; part.w += v[u].w; }
+        }
+    }
+
+    uint32_t k[kSortItems], v[kSortItems], r[kSortItems];
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) {
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
+        const bool ok = idx < n;
+        k[i] = ok ? kin[idx] : 0u;
+        v[i] = ok ? vin[idx] : 0u;
+    }
+    if (PREFIX_IN_KERNEL) {
+        const uint32_t q = tid & 63, p = tid >> 6;
+        s_part[p][4 * q] = part.x; s_part[p][4 * q + 1] = part.y;
+        s_part[p][4 * q + 2] = part.z; s_part[p][4 * q + 3] = part.w;
+    }
+    __syncthreads();
+    RT_STAMP(1);
+    // ---- stable per-wave ranking: order (wave, item, lane) == index order
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) {
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
+        const bool ok = idx < n;
+        const uint32_t d = (k[i] >> SHIFT) & 0xFFu;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(ok && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t below = sort_count_below(peers);
+        const uint32_t cur = s_wc[w][d];
+        r[i] = cur + below;
+        if (ok && below == 0) s_wc[w][d] = cur + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    RT_STAMP(2);
+    // ---- per-digit tile count, per-wave exclusive prefix (in place)
+    uint32_t cnt = 0;
+    if (tid < 256) {
+#pragma unroll
+        for (int ww = 0; ww < W; ++ww) {
+            const uint32_t c = s_wc[ww][tid];
+            s_wc[ww][tid] = cnt;
+            cnt += c;
+        }
+    }
+    const uint32_t lstart = scan256(tid < 256 ? cnt : 0u, s_sw);
+    const uint32_t dbase = scan256(tid < 256 ? ghist[tid & 255] : 0u, s_sw);
+    if (tid < 256) {
+        s_lstart[tid] = lstart;
+        uint32_t pre;
+        if (PREFIX_IN_KERNEL) {
+            pre = 0;
+#pragma unroll
+            for (int p = 0; p < 8; ++p) pre += s_part[p][tid];
+        } else {
+            pre = counts[(uint64_t)tile * 256 + tid];  // exclusive offsets from k_scan_tiles
+        }
+        s_gofs[tid] = dbase + pre;
+    }
+    __syncthreads();
+    RT_STAMP(3);
+    // ---- local scatter into LDS buckets
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) {
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
+        if (idx < n) {
+            const uint32_t dd = (k[i] >> SHIFT) & 0xFFu;
+            const uint32_t pos = s_lstart[dd] + s_wc[w][dd] + r[i];
+            s_key[pos] = k[i];
+            s_val[pos] = v[i];
+        }
+    }
+    __syncthreads();
+    RT_STAMP(4);
+    const uint32_t trem = n - base;
+    const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const uint32_t pidx = tid + m * kSortThreads;
+        if (pidx < tcount) {
+            const uint32_t key = s_key[pidx];
+            const uint32_t dd = (key >> SHIFT) & 0xFFu;
+            const uint32_t o = s_gofs[dd] + (pidx - s_lstart[dd]);
+            kout[o] = key;
+            vout[o] = s_val[pidx];
+        }
+    }
+    RT_STAMP(5);
+}
+
+// Stand-alone 4-digit global histogram (rt_stage_sort on caller keys; the
+// build gets it from K1).
+__global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t hist[4 * 256];
+    for (int j = threadIdx.x; j < 1024; j += 256) hist[j] = 0u;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        const uint32_t key = keys[i];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((key >> (8 * d)) & 0xFFu)], 1u);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 1024; j += 256) {
+        const uint32_t v = hist[j];
+        if (v) atomicAdd(&ghist[j], v);
+    }
+}
+
+// ================================================================ launchers
+static inline uint32_t sdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+
+uint32_t sort_tiles(uint32_t n) { return n ? sdiv(n, kSortTile) : 0u; }
+
+hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_digit_hist, dim3(std::min<uint32_t>(512, sdiv(n, 256))), dim3(256), 0, s, keys, n, ghist);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_hist0(const uint32_t* keys, uint32_t n, uint32_t* counts, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_tile_hist<0>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, keys, n, counts);
+    return hipGetLastError();
+}
+
+template <int SHIFT>
+static void scatter_pass(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n,
+                         const uint32_t* gh, uint32_t* counts, hipStream_t s) {
+    const uint32_t nt = sort_tiles(n);
+    if (nt <= kPrefixInKernelMaxTiles) {
+        hipLaunchKernelGGL((k_scatter<SHIFT, true>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
+    } else {
+        hipLaunchKernelGGL(k_scan_tiles, dim3(256), dim3(256), 0, s, counts, nt);
+        hipLaunchKernelGGL((k_scatter<SHIFT, false>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
+    }
+}
+
+// 4 passes, ping-pong 0->1->0->1->0.  Needs: ghist [4][256] (all digits) and
+// counts0 = pass-0 tile counts; counts[1..3] are scratch of ntiles*256 words.
+hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts[4],
+                       hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    const uint32_t nt = sort_tiles(n);
+    scatter_pass<0>(keys[0], vals[0], keys[1], vals[1], n, ghist + 0, counts[0], s);
+    hipLaunchKernelGGL(k_tile_hist<8>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[1]);
+    scatter_pass<8>(keys[1], vals[1], keys[0], vals[0], n, ghist + 256, counts[1], s);
+    hipLaunchKernelGGL(k_tile_hist<16>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], n, counts[2]);
+    scatter_pass<16>(keys[0], vals[0], keys[1], vals[1], n, ghist + 512, counts[2], s);
+    hipLaunchKernelGGL(k_tile_hist<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[3]);
+    scatter_pass<24>(keys[1], vals[1], keys[0], vals[0], n, ghist + 768, counts[3], s);
+    return hipGetLastError();
+}
+
+}  // namespace rt

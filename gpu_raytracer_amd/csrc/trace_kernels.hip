@@ -22,18 +22,17 @@ __device__ __forceinline__ void cross3(const float* a, const float* b, float* o)
     o[2] = a[0] * b[1] - a[1] * b[0];
 }
 
-// §9.7 Moller-Trumbore, two-sided, no epsilon; writes t/u/v on a closer hit.
-__device__ __forceinline__ bool intersect_tri(const float* o, const float* d, const float* tri, float tb,
-                                              float& tout, float& uout, float& vout) {
-    float e1[3], e2[3], p[3], s[3], q[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) { e1[c] = tri[3 + c] - tri[c]; e2[c] = tri[6 + c] - tri[c]; }
+// §9.7 Moller-Trumbore, two-sided, no epsilon, on precomputed edges
+// e1 = v1-v0, e2 = v2-v0; writes t/u/v on a closer hit.
+__device__ __forceinline__ bool intersect_e(const float* o, const float* d, const float* v0, const float* e1,
+                                            const float* e2, float tb, float& tout, float& uout, float& vout) {
+    float p[3], s[3], q[3];
     cross3(d, e2, p);
     const float det = dot3(e1, p);
     if (det == 0.0f) return false;
     const float inv = 1.0f / det;
 #pragma unroll
-    for (int c = 0; c < 3; ++c) s[c] = o[c] - tri[c];
+    for (int c = 0; c < 3; ++c) s[c] = o[c] - v0[c];
     const float u = dot3(s, p) * inv;
     if (u < 0.0f || u > 1.0f) return false;
     cross3(s, e1, q);
@@ -46,8 +45,16 @@ __device__ __forceinline__ bool intersect_tri(const float* o, const float* d, co
     return true;
 }
 
+__device__ __forceinline__ bool intersect_tri(const float* o, const float* d, const float* tri, float tb,
+                                              float& tout, float& uout, float& vout) {
+    float e1[3], e2[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { e1[c] = tri[3 + c] - tri[c]; e2[c] = tri[6 + c] - tri[c]; }
+    return intersect_e(o, d, tri, e1, e2, tb, tout, uout, vout);
+}
+
 template <bool COUNT>
-__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float* __restrict__ tris, uint32_t n,
+__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float4* __restrict__ tri_s, uint32_t n,
                                           const float* o, const float* d, float& tb, float& hu, float& hv,
                                           uint32_t& hp, uint32_t& cn, uint32_t& ct) {
     float invd[3];
@@ -72,12 +79,14 @@ __device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const 
         if (!(tn <= tf)) { idx = esc; continue; }
         if (idx >= L0) {
             if (COUNT) ++ct;
-            const float* tp = tris + (uint64_t)na * 9;
-            float tri[9];
-#pragma unroll
-            for (int c = 0; c < 9; ++c) tri[c] = tp[c];
+            // leaf-ordered {v0, e1, e2}: three aligned 16-B loads
+            const float4* tp = tri_s + (uint64_t)(idx - L0) * 3;
+            const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
+            const float v0[3] = {T0.x, T0.y, T0.z};
+            const float e1[3] = {T0.w, T1.x, T1.y};
+            const float e2[3] = {T1.z, T1.w, T2.x};
             float t, u, v;
-            if (intersect_tri(o, d, tri, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = na; }
+            if (intersect_e(o, d, v0, e1, e2, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = na; }
             idx = esc;
         } else {
             idx = na;
@@ -88,7 +97,7 @@ __device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const 
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
 
 template <bool COUNT, bool PACKED>
-__global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, const float* __restrict__ tris, uint32_t n,
+__global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
@@ -116,7 +125,7 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
             for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
             float tb, hu, hv;
             uint32_t hp;
-            trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tris, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
+            trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
             if (hits) {
                 const uint64_t hi = PACKED ? ((uint64_t)blockIdx.x * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
                 hits[hi] = make_float4(tb, hu, hv, __uint_as_float(hp));
@@ -188,10 +197,10 @@ __global__ void k_minmax(uint32_t count, const float* __restrict__ a, const floa
     out[2 * i + 1] = fmaxf(a[i], b[i]);
 }
 
-template __global__ void k_trace<false, false>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_trace<true, false>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_trace<false, true>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_trace<true, true>(const void*, const float*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<false, false>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<true, false>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<false, true>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
+template __global__ void k_trace<true, true>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
 
 // ================================================================ launchers
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
@@ -200,7 +209,7 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) 
     return (nt - rank + nranks - 1) / nranks;
 }
 
-hipError_t launch_trace(const void* nodes, const float* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
+hipError_t launch_trace(const void* nodes, const float4* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
                         uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits, void* rgba,
                         unsigned long long* counters, hipStream_t s) {
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
