@@ -7,7 +7,7 @@ contains no compute and no CPU fallback.
 """
 from ._lib import RtError, build_library, lib, SENTINEL  # noqa: F401
 from .scene import (  # noqa: F401
-    HIT_DTYPE, NODE_DTYPE, Scene, camera_array, camera_look_at, device_count, dump_hits, dump_ppm,
+    HIT_DTYPE, NODE_DTYPE, Scene, camera_array, config_set, camera_look_at, device_count, dump_hits, dump_ppm,
     stage_bounds, stage_intersect, stage_minmax, stage_morton, stage_sort, stage_topology, stage_trace,
     tiles_for_rank, unpack_tiles_device,
 )

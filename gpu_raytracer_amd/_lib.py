@@ -39,7 +39,7 @@ EXPORTED = [
     "rt_render_tiles_device", "rt_unpack_tiles_device", "rt_scene_stream", "rt_scene_sync",
     "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_trace",
     "rt_stage_intersect", "rt_stage_minmax", "rt_framebuffer_dump_ppm", "rt_hits_dump",
-    "rt_last_error", "rt_device_count", "rt_version",
+    "rt_config_set", "rt_last_error", "rt_device_count", "rt_version",
 ]
 
 
@@ -108,6 +108,7 @@ def lib() -> C.CDLL:
         "rt_stage_minmax": [i32, u32, P, P, P],
         "rt_framebuffer_dump_ppm": [P, u32, u32, C.c_char_p],
         "rt_hits_dump": [P, C.c_size_t, C.c_char_p],
+        "rt_config_set": [C.c_char_p, C.c_int64],
     }
     for name, args in sig.items():
         f = getattr(L, name)

@@ -36,6 +36,7 @@ struct rt_scene {
     void* d_rgba = nullptr;
     size_t rgba_cap = 0;
     unsigned long long* d_ctr = nullptr;
+    uint32_t* d_work = nullptr;  // persistent-trace tile counter
     hipEvent_t r0 = nullptr, r1 = nullptr;
 };
 
@@ -76,6 +77,7 @@ rt_status ensure_stream(rt_scene* s) {
         s->ev.valid = true;
         HIPR(hipEventCreate(&s->r0));
         HIPR(hipEventCreate(&s->r1));
+        HIPR(hipMalloc((void**)&s->d_work, 256));
     }
     return RT_OK;
 }
@@ -130,6 +132,16 @@ extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
 const char* rt_version(void) { return "gpu_raytracer_amd 0.1 (gfx950)"; }
+
+rt_status rt_config_set(const char* key, int64_t value) {
+    if (!key) return fail(RT_EINVAL, "null key");
+    const std::string k(key);
+    if (k == "trace.variant" && (value == 0 || value == 1)) rt::g_trace_config.variant = (uint32_t)value;
+    else if (k == "trace.blocks" && value >= 1 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
+    else if (k == "trace.refill_min" && value >= 1 && value <= 64) rt::g_trace_config.refill_min = (uint32_t)value;
+    else return fail(RT_EINVAL, "unknown config key or value out of range: " + k);
+    return RT_OK;
+}
 
 int rt_device_count(void) {
     int c = 0;
@@ -205,6 +217,7 @@ void rt_scene_free(rt_scene* s) {
         if (s->d_hits) (void)hipFree(s->d_hits);
         if (s->d_rgba) (void)hipFree(s->d_rgba);
         if (s->d_ctr) (void)hipFree(s->d_ctr);
+        if (s->d_work) (void)hipFree(s->d_work);
         for (auto& e : s->ev.e) (void)hipEventDestroy(e);
         (void)hipEventDestroy(s->r0);
         (void)hipEventDestroy(s->r1);
@@ -319,7 +332,7 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
     HIPR(hipEventRecord(s->r0, s->stream));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
-                                    hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, s->stream);
+                                    hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, s->d_work, s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipEventRecord(s->r1, s->stream));
     HIPR(hipStreamSynchronize(s->stream));
@@ -341,7 +354,7 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 16));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks, packed,
-                                    nullptr, nullptr, s->d_ctr, s->stream);
+                                    nullptr, nullptr, s->d_ctr, s->d_work, s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(s->stream));
     HIPR(hipMemcpy(counters_out, s->d_ctr, 16, hipMemcpyDeviceToHost));
@@ -368,7 +381,7 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false, d_hits,
-                                    d_rgba, nullptr, hs);
+                                    d_rgba, nullptr, s->d_work, hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
@@ -394,7 +407,7 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks, true,
-                                    d_packed_hits, d_packed_rgba, nullptr, hs);
+                                    d_packed_hits, d_packed_rgba, nullptr, s->d_work, hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
@@ -540,11 +553,12 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
         HIPR(hipMemcpy(dn.p, nodes, tot * 32, hipMemcpyHostToDevice));
         HIPR(hipMemcpy(dt.p, tris, (size_t)n * 36, hipMemcpyHostToDevice));
     }
-    DevBuf dts;
+    DevBuf dts, dw;
     HIPR(dts.alloc((size_t)(n ? n : 1) * 48));
+    HIPR(dw.alloc(256));
     HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
     HIPR(rt::launch_trace(dn.p, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
-                          counters ? dc.as<unsigned long long>() : nullptr, 0));
+                          counters ? dc.as<unsigned long long>() : nullptr, dw.as<uint32_t>(), 0));
     HIPR(hipDeviceSynchronize());
     if (hits) HIPR(hipMemcpy(hits, dh.p, nh * 16, hipMemcpyDeviceToHost));
     if (rgba) HIPR(hipMemcpy(rgba, dr.p, (size_t)w * h * 4, hipMemcpyDeviceToHost));

@@ -72,9 +72,20 @@ hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, fl
 
 struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 
+// Trace kernel selection / tuning (rt_config_set): variant 0 = one thread per
+// pixel, one 16x16 tile per workgroup (default); 1 = persistent wave-level
+// tile queue with per-lane refill (work != nullptr required) -- measured 2.4x
+// slower on soup-1M (tools/ab_trace.py), kept for incoherent-ray workloads.
+struct TraceConfig {
+    uint32_t variant = 0;
+    uint32_t blocks = 2048;     // persistent grid: 256 CUs x 8 workgroups of 4 waves
+    uint32_t refill_min = 16;   // refill when at least this many lanes are idle
+};
+extern TraceConfig g_trace_config;
+
 hipError_t launch_trace(const void* nodes, const float4* tri_s, uint32_t n, const CamF& cam, uint32_t w,
                         uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
-                        void* hits, void* rgba, unsigned long long* counters, hipStream_t s);
+                        void* hits, void* rgba, unsigned long long* counters, uint32_t* work, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
                          void* img, hipStream_t s);
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);

@@ -159,6 +159,172 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
     }
 }
 
+// ---------------------------------------------------------------- persistent
+// Persistent wave-level work distribution with per-lane refill.  Each wave
+// pulls 16x16 tiles (this rank's tiles, t = rank + b*nranks) from a work
+// counter; lanes whose pixel is finished take the next pixel of the current
+// tile (row-major, in lane order), so a wave no longer idles behind its
+// slowest ray.  A lane owns a whole pixel (its spp samples in order), which
+// keeps the per-pixel sample average of §9.7 sequential.  The traversal step
+// is the exact §9.7 escape-link loop body: results are bit-identical.
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+struct RayState {
+    float d[3], invd[3];
+    float tb, hu, hv;
+    uint32_t hp, idx, guard;
+};
+
+__device__ __forceinline__ void ray_setup(const Cam& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t spp, uint32_t s,
+                                          uint32_t n, RayState& R) {
+    const uint32_t sidx = (y * W + x) * spp + s;
+    float jx = 0.5f, jy = 0.5f;
+    if (s > 0) {
+        const uint32_t h = pcg_hash(sidx);
+        jx = (float)(h >> 8) * 0x1p-24f;
+        jy = (float)(pcg_hash(h) >> 8) * 0x1p-24f;
+    }
+    const float px = (float)x + jx, py = (float)y + jy;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        R.d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+        R.invd[c] = 1.0f / R.d[c];
+    }
+    R.tb = __builtin_inff(); R.hu = 0.0f; R.hv = 0.0f; R.hp = RT_SENT;
+    R.idx = n ? 0u : RT_SENT;
+    R.guard = 0;
+}
+
+template <bool COUNT, bool PACKED>
+__global__ __launch_bounds__(256) void k_trace_persist(const void* __restrict__ nodes_, const float4* __restrict__ tri_s,
+                                                       uint32_t n, Cam cam, uint32_t W, uint32_t H, uint32_t spp,
+                                                       uint32_t rank, uint32_t nranks, uint32_t tilesX,
+                                                       uint32_t ntiles_rank, uint32_t refill_min,
+                                                       float4* __restrict__ hits, uint32_t* __restrict__ rgba,
+                                                       unsigned long long* __restrict__ counters,
+                                                       uint32_t* __restrict__ work) {
+    const char* __restrict__ nodes = reinterpret_cast<const char*>(nodes_);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t L0 = n ? n - 1 : 0;
+    const uint32_t total = n ? 2 * n - 1 : 0;
+    // lane state
+    bool active = false;
+    uint32_t x = 0, y = 0, lp = 0, tb_idx = 0, s = 0;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    RayState R;
+    R.idx = RT_SENT;
+    // wave-uniform tile cursor
+    uint32_t cur_tile = 0, next = 256;
+    bool more = true;
+    uint32_t cn = 0, ct = 0;
+    const float o[3] = {cam.eye[0], cam.eye[1], cam.eye[2]};
+
+    for (;;) {
+        // ---- refill idle lanes (wave-uniform control flow)
+        uint64_t idle = __ballot(!active);
+        if (more && (uint32_t)__popcll(idle) >= refill_min) {
+            while (idle && more) {
+                if (next >= 256) {
+                    uint32_t t = 0;
+                    if (lane == 0) t = atomicAdd(work, 1u);
+                    t = __shfl(t, 0, 64);
+                    if (t >= ntiles_rank) { more = false; break; }
+                    cur_tile = t;
+                    next = 0;
+                }
+                const uint32_t pos = lanes_below(idle);
+                const uint32_t nidle = (uint32_t)__popcll(idle);
+                const uint32_t take = nidle < 256 - next ? nidle : 256 - next;
+                if (!active && pos < take) {
+                    lp = next + pos;
+                    tb_idx = cur_tile;
+                    const uint32_t t = rank + cur_tile * nranks;
+                    x = (t % tilesX) * 16 + (lp & 15);
+                    y = (t / tilesX) * 16 + (lp >> 4);
+                    if (x < W && y < H) {
+                        active = true;
+                        s = 0;
+                        cr = cg = cb = 0.0f;
+                        ray_setup(cam, x, y, W, spp, 0, n, R);
+                    }
+                }
+                next += take;
+                idle = __ballot(!active);
+            }
+        }
+        if (__ballot(active) == 0) break;  // every lane idle and no work left
+        // ---- one escape-link traversal step (§9.7)
+        if (active) {
+            if (R.idx < total && R.guard < total) {
+                ++R.guard;
+                const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)R.idx * 32);
+                const float4 A = np[0], B = np[1];
+                if (COUNT) ++cn;
+                const float t0x = (A.x - o[0]) * R.invd[0], t1x = (A.w - o[0]) * R.invd[0];
+                const float t0y = (A.y - o[1]) * R.invd[1], t1y = (B.x - o[1]) * R.invd[1];
+                const float t0z = (A.z - o[2]) * R.invd[2], t1z = (B.y - o[2]) * R.invd[2];
+                const float tn = fmaxf(fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z)), 0.0f);
+                const float tf = fminf(fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)), R.tb);
+                const uint32_t na = __float_as_uint(B.z), esc = __float_as_uint(B.w);
+                if (!(tn <= tf)) {
+                    R.idx = esc;
+                } else if (R.idx >= L0) {
+                    if (COUNT) ++ct;
+                    const float4* tp = tri_s + (uint64_t)(R.idx - L0) * 3;
+                    const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
+                    const float v0[3] = {T0.x, T0.y, T0.z};
+                    const float e1[3] = {T0.w, T1.x, T1.y};
+                    const float e2[3] = {T1.z, T1.w, T2.x};
+                    float t, u, v;
+                    if (intersect_e(o, R.d, v0, e1, e2, R.tb, t, u, v)) { R.tb = t; R.hu = u; R.hv = v; R.hp = na; }
+                    R.idx = esc;
+                } else {
+                    R.idx = na;
+                }
+            } else {
+                // sample finished
+                if (hits) {
+                    const uint64_t hi = PACKED ? ((uint64_t)tb_idx * 256 + lp) * spp + s
+                                               : (uint64_t)((y * W + x) * spp + s);
+                    hits[hi] = make_float4(R.tb, R.hu, R.hv, __uint_as_float(R.hp));
+                }
+                if (R.hp != RT_SENT) {
+                    cr = cr + R.hu;
+                    cg = cg + R.hv;
+                    cb = cb + ((1.0f - R.hu) - R.hv);
+                } else {
+                    cr = cr + 0.0f; cg = cg + 0.0f; cb = cb + 0.0f;
+                }
+                if (++s < spp) {
+                    ray_setup(cam, x, y, W, spp, s, n, R);
+                } else {
+                    if (rgba) {
+                        const float sc = 1.0f / (float)spp;
+                        const uint32_t px = q8(cr * sc) | (q8(cg * sc) << 8) | (q8(cb * sc) << 16) | (255u << 24);
+                        const uint64_t pi = PACKED ? (uint64_t)tb_idx * 256 + lp : (uint64_t)y * W + x;
+                        rgba[pi] = px;
+                    }
+                    active = false;
+                }
+            }
+        }
+    }
+    if (COUNT) {
+        unsigned long long a = cn, bsum = ct;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            bsum += __shfl_xor(bsum, off, 64);
+        }
+        if (lane == 0) {
+            atomicAdd(&counters[0], a);
+            atomicAdd(&counters[1], bsum);
+        }
+    }
+}
+
 // Gathered slabs [rank][tile][256 px] -> W x H image.
 __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ slabs, uint32_t tiles_per_slab, uint32_t W,
                                                 uint32_t H, uint32_t nranks, uint32_t tilesX, uint32_t ntiles,
@@ -209,9 +375,11 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) 
     return (nt - rank + nranks - 1) / nranks;
 }
 
+TraceConfig g_trace_config;
+
 hipError_t launch_trace(const void* nodes, const float4* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
                         uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits, void* rgba,
-                        unsigned long long* counters, hipStream_t s) {
+                        unsigned long long* counters, uint32_t* work, hipStream_t s) {
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
     if (!nb) return hipSuccess;
     Cam cam;
@@ -221,6 +389,23 @@ hipError_t launch_trace(const void* nodes, const float4* tris, uint32_t n, const
     const uint32_t tilesX = (w + 15) / 16;
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
+    if (g_trace_config.variant == 1 && work) {
+        hipError_t e = hipMemsetAsync(work, 0, 4, s);
+        if (e != hipSuccess) return e;
+        const uint32_t waves = g_trace_config.blocks * 4;
+        const uint32_t grid = nb < waves ? (nb + 3) / 4 : g_trace_config.blocks;
+        const uint32_t rmin = g_trace_config.refill_min;
+#define RT_PERSIST(C, P)                                                                                          \
+    hipLaunchKernelGGL((k_trace_persist<C, P>), dim3(grid), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, \
+                       nranks, tilesX, nb, rmin, H, R, counters, work)
+        if (counters) {
+            if (packed) RT_PERSIST(true, true); else RT_PERSIST(true, false);
+        } else {
+            if (packed) RT_PERSIST(false, true); else RT_PERSIST(false, false);
+        }
+#undef RT_PERSIST
+        return hipGetLastError();
+    }
     if (counters) {
         if (packed) hipLaunchKernelGGL((k_trace<true, true>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
         else hipLaunchKernelGGL((k_trace<true, false>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);

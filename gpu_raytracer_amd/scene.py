@@ -194,6 +194,11 @@ def dump_hits(hits: np.ndarray, path: str) -> None:
     call("rt_hits_dump", _p(h) if len(h) else None, len(h), path.encode())
 
 
+def config_set(key: str, value: int) -> None:
+    """Process-wide tuning knob (see rt_config_set in the header)."""
+    call("rt_config_set", key.encode(), int(value))
+
+
 def device_count() -> int:
     return int(lib().rt_device_count())
 
@@ -265,6 +270,6 @@ def stage_minmax(a, b, device: int = 0):
     return out[: len(a), 0].copy(), out[: len(a), 1].copy()
 
 
-__all__ = ["Scene", "camera_look_at", "camera_array", "tiles_for_rank", "unpack_tiles_device", "dump_ppm",
+__all__ = ["Scene", "config_set", "camera_look_at", "camera_array", "tiles_for_rank", "unpack_tiles_device", "dump_ppm",
            "dump_hits", "device_count", "stage_bounds", "stage_morton", "stage_sort", "stage_topology",
            "stage_trace", "stage_intersect", "stage_minmax", "NODE_DTYPE", "HIT_DTYPE", "SENTINEL"]

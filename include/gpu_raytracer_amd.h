@@ -146,6 +146,12 @@ rt_status rt_stage_minmax(int device, uint32_t count, const float* a, const floa
 rt_status rt_framebuffer_dump_ppm(const uint8_t* rgba, uint32_t w, uint32_t h, const char* path);
 rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
 
+/* Tuning knobs (process-wide): "trace.variant" 0 = one thread per pixel
+ * (default), 1 = persistent tile queue with per-lane refill; "trace.blocks"
+ * persistent grid size; "trace.refill_min" idle lanes that trigger a refill.
+ * Results are bit-identical for every setting. */
+rt_status rt_config_set(const char* key, int64_t value);
+
 const char* rt_last_error(void);
 int rt_device_count(void);
 const char* rt_version(void);
