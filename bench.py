@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_trace.json"))
     ap.add_argument("--dump", default="", help="write the rank-0 image as PPM")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI) for the benchmark; gloo only to rehearse N>1 on one GPU")
     return ap.parse_args()
 
 
@@ -99,11 +101,17 @@ def main():
     import torch
     import torch.distributed as dist
     import gpu_raytracer_amd as R
+    from gpu_raytracer_amd import dist as D
     from gpu_raytracer_amd import scenes as S
 
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1)  # rehearsal: several ranks may share one GPU (gloo only)
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     cfg = S.CONFIGS[args.config]
     view = S.VIEWS[cfg.scene]
@@ -117,12 +125,13 @@ def main():
     scene.set_device(local)
     cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
 
-    ntiles = R.tiles_for_rank(w, h, rank, world)
-    tmax = max(R.tiles_for_rank(w, h, r, world) for r in range(world))
+    tmax = D.slab_tiles(w, h, world)
     dev = torch.device("cuda", local)
     img = torch.zeros(w * h, dtype=torch.int32, device=dev)
     hits = torch.empty(rays * 4, dtype=torch.float32, device=dev)
     slab = torch.zeros(max(tmax, 1) * 256, dtype=torch.int32, device=dev) if world > 1 else None
+    # every rank writes its hit records too (16 B/ray, part of the byte model); only RGBA is gathered
+    slab_hits = torch.empty(max(tmax, 1) * 256 * spp * 4, dtype=torch.float32, device=dev) if world > 1 else None
     gather_list = [torch.zeros_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
     slabs_all = torch.zeros(world * max(tmax, 1) * 256, dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
 
@@ -131,11 +140,16 @@ def main():
         if world == 1:
             trace_ms = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
             return build_ms, trace_ms, 0.0
-        trace_ms = scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), timed=True)
+        trace_ms = scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
+                                             timed=True)
         t0 = time.perf_counter()
-        dist.gather(slab, gather_list, dst=0)
+        if args.dist_backend == "nccl":
+            D.gather_slabs(slab, rank, world, gather_list, slabs_all)
+        else:  # rehearsal: stage through host memory
+            g = D.gather_slabs(slab.cpu(), rank, world)
+            if rank == 0:
+                slabs_all.copy_(g)
         if rank == 0:
-            torch.cat(gather_list, out=slabs_all)
             R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
                                   torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
@@ -158,10 +172,11 @@ def main():
 
     # max over ranks (per step), then mean over steps
     if world > 1:
-        t = torch.tensor(per, dtype=torch.float64, device=dev)
+        rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+        t = torch.tensor(per, dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         per = t.cpu().numpy()
-        wt = torch.tensor([wall], dtype=torch.float64, device=dev)
+        wt = torch.tensor([wall], dtype=torch.float64, device=rdev)
         dist.all_reduce(wt, op=dist.ReduceOp.MAX)
         wall = float(wt.item())
     build_ms, trace_ms, gather_ms = (float(x) for x in per.mean(axis=0))
@@ -169,15 +184,7 @@ def main():
 
     # work counters of this rank's trace launch (deterministic; untimed)
     cnt = scene.render_tiles_counters(cam, w, h, spp, rank, world) if world > 1 else scene.render_counters(cam, w, h, spp)
-    rank_rays = (ntiles * 256 * spp) if world > 1 else rays  # upper bound incl. padding lanes; exact below
-    if world > 1:
-        # exact ray count of the rank's tiles (edge tiles are partial)
-        tx = (w + 15) // 16
-        rr = 0
-        for t in range(rank, ((h + 15) // 16) * tx, world):
-            x0, y0 = (t % tx) * 16, (t // tx) * 16
-            rr += min(16, w - x0) * min(16, h - y0)
-        rank_rays = rr * spp
+    rank_rays = D.rays_of_rank(w, h, spp, rank, world)
     algo_bytes = 32.0 * float(cnt[0]) + 36.0 * float(cnt[1]) + 16.0 * rank_rays
     rank_trace_ms = float(np.array(rec)[:, 1].mean())
     achieved = algo_bytes / (rank_trace_ms * 1e-3) / 1e9
@@ -211,7 +218,7 @@ def main():
             "config": {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{args.config - 1}])",
                        "n_tris": n_tris, "width": w, "height": h, "spp": spp,
                        "parallelism": f"image tiles 16x16 round-robin over {world} GPU(s), BVH replicated"
-                                      + (", RCCL gather to rank 0" if world > 1 else "")},
+                                      + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else ", gloo gather (rehearsal)") if world > 1 else "")},
             "build_mprims_per_s": round(n_tris / (build_ms * 1e-3) / 1e6, 2),
             "build_ms": round(build_ms, 4),
             "trace_ms": round(trace_ms, 4),
@@ -236,8 +243,11 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
             out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt)
+        host_img = img.cpu().numpy().view(np.uint8)
+        import zlib
+        out["image_crc32"] = zlib.crc32(host_img.tobytes()) & 0xFFFFFFFF  # same for every N (bit-exact tiles)
         if args.dump:
-            R.dump_ppm(img.cpu().numpy().view(np.uint8), w, h, args.dump)
+            R.dump_ppm(host_img, w, h, args.dump)
         print(json.dumps(out), flush=True)
     scene.close()
     if world > 1:
