@@ -639,7 +639,7 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path) {
 // of the build kernels (which = 0) or the sort kernels (which = 1)
 rt_status rt_debug_stamps(int which, void* out, size_t bytes) {
     HIPR(hipDeviceSynchronize());
-    HIPR(which ? rt::read_stamps_sort(out, bytes) : rt::read_stamps_build(out, bytes));
+    HIPR(which == 2 ? rt::read_stamps_trace(out, bytes) : which ? rt::read_stamps_sort(out, bytes) : rt::read_stamps_build(out, bytes));
     return RT_OK;
 }
 #endif

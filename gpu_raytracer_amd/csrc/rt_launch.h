@@ -74,8 +74,10 @@ struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 
 // Trace kernel selection / tuning (rt_config_set): variant 0 = one thread per
 // pixel, one 16x16 tile per workgroup (default); 1 = persistent wave-level
-// tile queue with per-lane refill (work != nullptr required) -- measured 2.4x
-// slower on soup-1M (tools/ab_trace.py), kept for incoherent-ray workloads.
+// queue of 8x8 units with per-lane refill (work != nullptr required) --
+// measured 1.6x slower on soup-1M (profiles/ab_trace_r01_variants.log: lanes
+// at different depths touch more distinct lines per load), kept for
+// incoherent-ray workloads.
 struct TraceConfig {
     uint32_t variant = 0;
     uint32_t blocks = 2048;     // persistent grid: 256 CUs x 8 workgroups of 4 waves
@@ -94,6 +96,7 @@ hipError_t launch_intersect(uint32_t count, const float* o, const float* d, cons
 #ifdef RT_STAMPS
 hipError_t read_stamps_build(void* out, size_t bytes);
 hipError_t read_stamps_sort(void* out, size_t bytes);
+hipError_t read_stamps_trace(void* out, size_t bytes);
 #endif
 hipError_t launch_minmax(uint32_t count, const float* a, const float* b, float* out, hipStream_t s);
 

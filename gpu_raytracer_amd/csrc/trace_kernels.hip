@@ -13,6 +13,10 @@
 
 namespace rt {
 
+#ifdef RT_STAMPS
+hipError_t read_stamps_trace(void* out, size_t bytes) { return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stamps), bytes); }
+#endif
+
 struct Cam { float eye[3], w00[3], du[3], dv[3]; };
 
 __device__ __forceinline__ float dot3(const float* a, const float* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
@@ -53,10 +57,20 @@ __device__ __forceinline__ bool intersect_tri(const float* o, const float* d, co
     return intersect_e(o, d, tri, e1, e2, tb, tout, uout, vout);
 }
 
+// §9.7 stackless escape-link traversal of one ray over the 32-B nodes (two
+// 16-B loads per node), with the leaf's triangle test deferred by one step:
+// after a leaf's box hits, the next node is always its escape, which the
+// leaf record already names, so the next step issues the escape node's
+// loads AND the leaf's triangle loads together, tests the triangle first (it
+// may shrink tb) and the node box second -- the §9.7 order, hence the same
+// tests with the same operands.  A wave step then costs one memory round
+// trip instead of two whenever some lane is at a leaf (+2-4 %,
+// profiles/ab_trace_r01_variants.log).  A well-formed tree visits each node
+// once; the guard and index checks only keep a malformed one from faulting.
 template <bool COUNT>
-__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float4* __restrict__ tri_s, uint32_t n,
-                                          const float* o, const float* d, float& tb, float& hu, float& hv,
-                                          uint32_t& hp, uint32_t& cn, uint32_t& ct) {
+__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float4* __restrict__ tri_s,
+                                                uint32_t n, const float* o, const float* d, float& tb, float& hu,
+                                                float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
     float invd[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) invd[c] = 1.0f / d[c];
@@ -64,11 +78,26 @@ __device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const 
     const uint32_t L0 = n ? n - 1 : 0;
     const uint32_t total = n ? 2 * n - 1 : 0;
     uint32_t idx = n ? 0u : RT_SENT;
-    // A well-formed escape-link tree visits each node at most once; the
-    // bound and the index check only keep a malformed tree from faulting.
-    for (uint32_t guard = 0; idx < total && guard < total; ++guard) {
-        const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)idx * 32);
-        const float4 A = np[0], B = np[1];
+    uint32_t pend = RT_SENT, pprim = 0;  // leaf whose triangle test is due
+    for (uint32_t guard = 0; (idx < total || pend != RT_SENT) && guard <= total; ++guard) {
+        float4 A, B;
+        const bool node = idx < total;
+        if (node) {
+            const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)idx * 32);
+            A = np[0]; B = np[1];
+        }
+        if (pend != RT_SENT) {
+            if (COUNT) ++ct;
+            const float4* tp = tri_s + (uint64_t)pend * 3;
+            const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
+            const float v0[3] = {T0.x, T0.y, T0.z};
+            const float e1[3] = {T0.w, T1.x, T1.y};
+            const float e2[3] = {T1.z, T1.w, T2.x};
+            float t, u, v;
+            if (intersect_e(o, d, v0, e1, e2, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = pprim; }
+            pend = RT_SENT;
+        }
+        if (!node) break;
         if (COUNT) ++cn;
         const float t0x = (A.x - o[0]) * invd[0], t1x = (A.w - o[0]) * invd[0];
         const float t0y = (A.y - o[1]) * invd[1], t1y = (B.x - o[1]) * invd[1];
@@ -76,21 +105,9 @@ __device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const 
         const float tn = fmaxf(fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z)), 0.0f);
         const float tf = fminf(fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)), tb);
         const uint32_t na = __float_as_uint(B.z), esc = __float_as_uint(B.w);
-        if (!(tn <= tf)) { idx = esc; continue; }
-        if (idx >= L0) {
-            if (COUNT) ++ct;
-            // leaf-ordered {v0, e1, e2}: three aligned 16-B loads
-            const float4* tp = tri_s + (uint64_t)(idx - L0) * 3;
-            const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
-            const float v0[3] = {T0.x, T0.y, T0.z};
-            const float e1[3] = {T0.w, T1.x, T1.y};
-            const float e2[3] = {T1.z, T1.w, T2.x};
-            float t, u, v;
-            if (intersect_e(o, d, v0, e1, e2, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = na; }
-            idx = esc;
-        } else {
-            idx = na;
-        }
+        const bool hit = tn <= tf;
+        if (hit && idx >= L0) { pend = idx - L0; pprim = na; }
+        idx = (hit && idx < L0) ? na : esc;
     }
 }
 
@@ -102,13 +119,20 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                unsigned long long* __restrict__ counters) {
-    const uint32_t t = rank + blockIdx.x * nranks;
+    // tile slot = block id: consecutive tiles go to different XCDs under the
+    // round-robin dispatch, which balances the image's cheap and costly
+    // bands over the 8 XCDs (an XCD-banded remap measured 1.2x slower)
+    const uint32_t slot = blockIdx.x;
+    const uint32_t t = rank + slot * nranks;
     const uint32_t tx = t % tilesX, ty = t / tilesX;
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
     uint32_t cn = 0, ct = 0;
+#ifdef RT_STAMPS
+    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (valid) {
         float r = 0.0f, g = 0.0f, b = 0.0f;
         for (uint32_t s = 0; s < spp; ++s) {
@@ -127,7 +151,7 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
             uint32_t hp;
             trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
             if (hits) {
-                const uint64_t hi = PACKED ? ((uint64_t)blockIdx.x * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
+                const uint64_t hi = PACKED ? ((uint64_t)slot * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
                 hits[hi] = make_float4(tb, hu, hv, __uint_as_float(hp));
             }
             if (hp != RT_SENT) {
@@ -141,10 +165,30 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
         if (rgba) {
             const float sc = 1.0f / (float)spp;
             const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
-            const uint64_t pi = PACKED ? (uint64_t)blockIdx.x * 256 + ly * 16 + lx : (uint64_t)y * W + x;
+            const uint64_t pi = PACKED ? (uint64_t)slot * 256 + ly * 16 + lx : (uint64_t)y * W + x;
             rgba[pi] = px;
         }
     }
+#ifdef RT_STAMPS
+    // per-wave {start, end, HW_ID | XCC_ID << 32, max lane nodes | wave nodes << 32}
+    // (tools/diag_trace.py; node counts only in the COUNT variant)
+    {
+        uint32_t mx = cn, sm = cn;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            mx = max(mx, (uint32_t)__shfl_xor(mx, o, 64));
+            sm += __shfl_xor(sm, o, 64);
+        }
+        if (l == 0) {
+            const uint64_t wslot = ((uint64_t)blockIdx.x * 4 + w) * 4;
+            g_rt_stamps[wslot + 0] = st0;
+            g_rt_stamps[wslot + 1] = __builtin_amdgcn_s_memrealtime();
+            g_rt_stamps[wslot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                     ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+            g_rt_stamps[wslot + 3] = (uint64_t)mx | ((uint64_t)sm << 32);
+        }
+    }
+#endif
     if (COUNT) {
         unsigned long long a = cn, bsum = ct;
 #pragma unroll
@@ -161,10 +205,10 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
 
 // ---------------------------------------------------------------- persistent
 // Persistent wave-level work distribution with per-lane refill.  Each wave
-// pulls 16x16 tiles (this rank's tiles, t = rank + b*nranks) from a work
-// counter; lanes whose pixel is finished take the next pixel of the current
-// tile (row-major, in lane order), so a wave no longer idles behind its
-// slowest ray.  A lane owns a whole pixel (its spp samples in order), which
+// pulls units -- 8x8 quarters of this rank's 16x16 tiles (t = rank +
+// b*nranks) -- from a work counter; lanes whose pixel is finished take the
+// next pixel of the current unit (in lane order), so a wave no longer idles
+// behind its slowest ray.  A lane owns a whole pixel (its spp samples in order), which
 // keeps the per-pixel sample average of §9.7 sequential.  The traversal step
 // is the exact §9.7 escape-link loop body: results are bit-identical.
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
@@ -216,7 +260,7 @@ __global__ __launch_bounds__(256) void k_trace_persist(const void* __restrict__ 
     RayState R;
     R.idx = RT_SENT;
     // wave-uniform tile cursor
-    uint32_t cur_tile = 0, next = 256;
+    uint32_t cur_unit = 0, next = 64;
     bool more = true;
     uint32_t cn = 0, ct = 0;
     const float o[3] = {cam.eye[0], cam.eye[1], cam.eye[2]};
@@ -226,21 +270,23 @@ __global__ __launch_bounds__(256) void k_trace_persist(const void* __restrict__ 
         uint64_t idle = __ballot(!active);
         if (more && (uint32_t)__popcll(idle) >= refill_min) {
             while (idle && more) {
-                if (next >= 256) {
-                    uint32_t t = 0;
-                    if (lane == 0) t = atomicAdd(work, 1u);
-                    t = __shfl(t, 0, 64);
-                    if (t >= ntiles_rank) { more = false; break; }
-                    cur_tile = t;
+                if (next >= 64) {
+                    uint32_t u = 0;
+                    if (lane == 0) u = atomicAdd(work, 1u);
+                    u = __shfl(u, 0, 64);
+                    if (u >= ntiles_rank * 4) { more = false; break; }
+                    cur_unit = u;
                     next = 0;
                 }
                 const uint32_t pos = lanes_below(idle);
                 const uint32_t nidle = (uint32_t)__popcll(idle);
-                const uint32_t take = nidle < 256 - next ? nidle : 256 - next;
+                const uint32_t take = nidle < 64 - next ? nidle : 64 - next;
                 if (!active && pos < take) {
-                    lp = next + pos;
-                    tb_idx = cur_tile;
-                    const uint32_t t = rank + cur_tile * nranks;
+                    // unit = one 8x8 quarter of a 16x16 tile
+                    const uint32_t p = next + pos, sub = cur_unit & 3;
+                    lp = ((sub >> 1) * 8 + (p >> 3)) * 16 + (sub & 1) * 8 + (p & 7);
+                    tb_idx = cur_unit >> 2;
+                    const uint32_t t = rank + tb_idx * nranks;
                     x = (t % tilesX) * 16 + (lp & 15);
                     y = (t / tilesX) * 16 + (lp >> 4);
                     if (x < W && y < H) {
@@ -363,10 +409,6 @@ __global__ void k_minmax(uint32_t count, const float* __restrict__ a, const floa
     out[2 * i + 1] = fmaxf(a[i], b[i]);
 }
 
-template __global__ void k_trace<false, false>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_trace<true, false>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_trace<false, true>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
-template __global__ void k_trace<true, true>(const void*, const float4*, uint32_t, Cam, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, float4*, uint32_t*, unsigned long long*);
 
 // ================================================================ launchers
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
@@ -393,7 +435,7 @@ hipError_t launch_trace(const void* nodes, const float4* tris, uint32_t n, const
         hipError_t e = hipMemsetAsync(work, 0, 4, s);
         if (e != hipSuccess) return e;
         const uint32_t waves = g_trace_config.blocks * 4;
-        const uint32_t grid = nb < waves ? (nb + 3) / 4 : g_trace_config.blocks;
+        const uint32_t grid = nb * 4 < waves ? nb : g_trace_config.blocks;  // 4 units (8x8) per tile
         const uint32_t rmin = g_trace_config.refill_min;
 #define RT_PERSIST(C, P)                                                                                          \
     hipLaunchKernelGGL((k_trace_persist<C, P>), dim3(grid), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, \

@@ -1,5 +1,5 @@
 """A/B the trace-kernel variants in ONE process, interleaved rounds (guide
-§5.4 rule 24).  usage: python tools/ab_trace.py [rounds]"""
+§5.4 rule 24).  usage: python tools/ab_trace.py [rounds] [variants, e.g. 0,2]"""
 import os
 import sys
 
@@ -17,10 +17,21 @@ s.build()
 cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
 hits = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
-variants = [("simple", {"trace.variant": 0})]
-for rm in (1, 8, 16, 32, 48):
-    for blocks in (1024, 2048):
-        variants.append((f"persist refill>={rm} blocks={blocks}", {"trace.variant": 1, "trace.refill_min": rm, "trace.blocks": blocks}))
+sel = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "p8-b2048"]
+variants = []
+for v in sel:
+    if v == "0":
+        variants.append(("default (deferred leaf test)", {"trace.variant": 0}))
+    elif v.startswith("p"):  # pR-bB: persistent, refill_min R, B blocks
+        a, b = v[1:].split("-b")
+        variants.append((v, {"trace.variant": 1, "trace.refill_min": int(a), "trace.blocks": int(b)}))
+cnts = {}
+for name, cfg in variants:
+    for k, v in cfg.items():
+        R.config_set(k, v)
+    cnts[name] = tuple(int(c) for c in s.render_counters(cam, w, h, spp))
+print("counters", cnts)
+assert len(set(cnts.values())) == 1, "variants disagree on work counters"
 ref = None
 times = {name: [] for name, _ in variants}
 for r in range(rounds):
@@ -29,7 +40,7 @@ for r in range(rounds):
             R.config_set(k, v)
         ms = [s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True) for _ in range(3)]
         times[name].append(min(ms))
-        out = img.cpu().numpy()
+        out = np.concatenate([img.cpu().numpy().view(np.uint32), hits.cpu().numpy().view(np.uint32)])
         if ref is None:
             ref = out.copy()
         assert np.array_equal(out, ref), name
