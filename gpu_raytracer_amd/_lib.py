@@ -34,7 +34,7 @@ _STATUS_NAMES = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EIO", -4:
 EXPORTED = [
     "rt_scene_from_soup", "rt_scene_load_obj", "rt_scene_generate_soup", "rt_scene_num_tris",
     "rt_scene_get_tris", "rt_scene_set_device", "rt_scene_free", "rt_camera_look_at", "rt_bvh_build",
-    "rt_bvh_build_times", "rt_bvh_read", "rt_render", "rt_render_counters", "rt_render_device",
+    "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_render", "rt_render_counters", "rt_render_work", "rt_render_device",
     "rt_render_tiles_counters", "rt_tiles_for_rank",
     "rt_render_tiles_device", "rt_unpack_tiles_device", "rt_scene_stream", "rt_scene_sync",
     "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_trace",
@@ -54,7 +54,7 @@ class rt_camera(C.Structure):
 
 
 class rt_build_times(C.Structure):
-    _fields_ = [(k, C.c_double) for k in ("bounds", "morton", "sort", "topology", "refit", "total")]
+    _fields_ = [(k, C.c_double) for k in ("bounds", "morton", "sort", "topology", "refit", "wide", "total")]
 
 
 def build_library(verbose: bool = False) -> str:
@@ -91,8 +91,10 @@ def lib() -> C.CDLL:
         "rt_bvh_build": [P, C.POINTER(dbl)],
         "rt_bvh_build_times": [P, C.POINTER(rt_build_times)],
         "rt_bvh_read": [P, P, P, P, P, P],
+        "rt_bvh_read_wide": [P, P],
         "rt_render": [P, cam, u32, u32, u32, P, P, C.POINTER(dbl)],
         "rt_render_counters": [P, cam, u32, u32, u32, P],
+        "rt_render_work": [P, cam, u32, u32, u32, P],
         "rt_render_device": [P, cam, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_tiles_counters": [P, cam, u32, u32, u32, u32, u32, P],
         "rt_render_tiles_device": [P, cam, u32, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],

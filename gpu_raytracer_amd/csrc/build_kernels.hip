@@ -241,14 +241,15 @@ __device__ __forceinline__ void store_node(void* nodes, uint32_t idx, const Aabb
     p[1] = make_float4(b.hi[1], b.hi[2], __uint_as_float(a), __uint_as_float(esc));
 }
 
-// Leaf-ordered triangle record for the trace kernel: {v0, e1 = v1-v0,
-// e2 = v2-v0} in three 16-B words.  The subtractions are the ones the
-// Moller-Trumbore test performs (§9.7), so precomputing them is bit-exact.
-__device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint32_t k, const float* t) {
+// Leaf-ordered triangle record for the trace kernels: {v0, v1, v2, prim} in
+// three aligned 16-B words.  The trace recomputes the leaf box (tri_bounds)
+// and the Moller-Trumbore edges from the exact vertices, with the same fp32
+// operations K4 and §9.7 use.
+__device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint32_t k, const float* t, uint32_t prim) {
     float4* o = tri_s + (uint64_t)k * 3;
-    o[0] = make_float4(t[0], t[1], t[2], t[3] - t[0]);
-    o[1] = make_float4(t[4] - t[1], t[5] - t[2], t[6] - t[0], t[7] - t[1]);
-    o[2] = make_float4(t[8] - t[2], 0.0f, 0.0f, 0.0f);
+    o[0] = make_float4(t[0], t[1], t[2], t[3]);
+    o[1] = make_float4(t[4], t[5], t[6], t[7]);
+    o[2] = make_float4(t[8], __uint_as_float(prim), 0.0f, 0.0f);
 }
 
 // Thread i: internal node i (i < n-1) and leaf i (i < n).
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restric
     Aabb box;
     tri_bounds(tv, box.lo, box.hi);
     store_node(nodes, L0 + i32, box, prim, lesc);
-    store_leaf_tri(tri_s, i32, tv);
+    store_leaf_tri(tri_s, i32, tv, prim);
 }
 
 // Stand-alone leaf-triangle pass (rt_stage_trace on caller nodes).
@@ -317,7 +318,7 @@ __global__ __launch_bounds__(256) void k_leaf_tris(const void* __restrict__ node
     float t[9];
 #pragma unroll
     for (int c = 0; c < 9; ++c) t[c] = tris[(uint64_t)prim * 9 + c];
-    store_leaf_tri(tri_s, k, t);
+    store_leaf_tri(tri_s, k, t, prim);
 }
 
 // ---------------------------------------------------------------- K6 refit
@@ -347,6 +348,128 @@ __device__ __forceinline__ Aabb load_aabb(const float* buf, uint64_t idx) {
     return b;
 }
 
+// ---------------------------------------------------------------- K7w wide tree (the trace-layout pack of SURVEY.md §8(a) a9)
+__device__ __forceinline__ Aabb load_aabb_node(const void* nodes, uint32_t i) {
+    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)i * 32);
+    const float4 A = p[0], B = p[1];
+    Aabb b;
+    b.lo[0] = A.x; b.lo[1] = A.y; b.lo[2] = A.z;
+    b.hi[0] = A.w; b.hi[1] = B.x; b.hi[2] = B.y;
+    return b;
+}
+
+// Children of internal node X from its topology word {left, esc, lo, hi}:
+// the split g is the left child's index (internal g or leaf L0+g); the right
+// child is internal g+1, or leaf L0+g+1 when the range ends at g+1.
+__device__ __forceinline__ void kids_of(const uint4& tp, uint32_t L0, uint32_t& l, uint32_t& r) {
+    l = tp.x;
+    const uint32_t g = l < L0 ? l : l - L0;
+    r = tp.w == g + 1 ? L0 + g + 1 : g + 1;
+}
+
+// One axis of one record: grid step 2^e with 255 * 2^e >= extent, then for
+// each valid child the outward-rounded planes.  (lo - origin) * 2^-e is off
+// by at most one step after rounding, so one check with wide_plane -- the
+// trace kernel's own arithmetic -- makes plane(qlo) <= lo and plane(qhi) >=
+// hi exact.  false: not representable (non-finite values, exponent > 119,
+// or a plane the one correction step cannot fix) -- the record goes wild.
+// Fixed 4 slots, fully unrolled (no dynamic register indexing -> no scratch).
+__device__ bool quant_axis(float olo, float ohi, const float (&clo)[4], const float (&chi)[4], uint32_t valid,
+                           uint32_t& qlo_w, uint32_t& qhi_w, int& e_out) {
+    const float ext = ohi - olo;
+    bool fin = isfinite(olo) && isfinite(ohi) && isfinite(ext) && ext >= 0.0f;
+    float lo[4], hi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // unused slots quantize the origin: always representable
+        const bool v = (valid >> i) & 1u;
+        lo[i] = v ? clo[i] : olo;
+        hi[i] = v ? chi[i] : olo;
+        fin = fin && isfinite(lo[i]) && isfinite(hi[i]);
+    }
+    if (!fin) return false;
+    const uint32_t be = (__float_as_uint(ext) >> 23) & 0xFF;  // ext normal: 2^(be-127) <= ext
+    int e = (ext > 0.0f && be) ? (int)be - 134 : -126;
+    e = e < -126 ? -126 : e;
+    e += (ldexpf(255.0f, e) < ext) ? 1 : 0;
+    if (e > 119) return false;
+    // one pass: a plane that still misses after the one-step correction
+    // (origin + 255 * 2^e rounding below hi: far-apart magnitudes) makes the
+    // record wild instead of retrying with a coarser grid
+    const float sc = wide_scale(e);
+    uint32_t lw = 0, hw = 0;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float fl = fminf(fmaxf(floorf(ldexpf(lo[i] - olo, -e)), 0.0f), 255.0f);
+        fl = (fl > 0.0f && wide_plane(olo, (uint32_t)fl, sc) > lo[i]) ? fl - 1.0f : fl;
+        float fh = fminf(fmaxf(ceilf(ldexpf(hi[i] - olo, -e)), 0.0f), 255.0f);
+        fh = (fh < 255.0f && wide_plane(olo, (uint32_t)fh, sc) < hi[i]) ? fh + 1.0f : fh;
+        ok = ok && !(wide_plane(olo, (uint32_t)fh, sc) < hi[i]) && !(wide_plane(olo, (uint32_t)fl, sc) > lo[i]);
+        const uint32_t v = (valid >> i) & 1u;
+        lw |= (v ? (uint32_t)fl : 0u) << (8 * i);
+        hw |= (v ? (uint32_t)fh : 0u) << (8 * i);
+    }
+    qlo_w = lw; qhi_w = hw; e_out = e;
+    return ok;
+}
+
+// Quantize and store the wide record of internal node X from its box and the
+// boxes of its 2-4 children-or-grandchildren (node[] binary indices in
+// preorder, RT_SENT in unused slots); box_of(slot) fetches a child box (LDS
+// in K6, global in k_wide_cross).
+template <typename BoxOf>
+__device__ __forceinline__ void store_wide(uint4* __restrict__ wnodes, uint32_t X, const Aabb& bx,
+                                           const uint32_t (&node)[4], BoxOf box_of, uint32_t L0) {
+    uint32_t valid = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) valid |= (node[i] != RT_SENT ? 1u : 0u) << i;
+    float bl[3][4], bh[3][4];  // static indices only: no scratch
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const Aabb b = box_of(i);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { bl[c][i] = b.lo[c]; bh[c][i] = b.hi[c]; }
+    }
+    uint32_t q[6] = {0, 0, 0, 0, 0, 0};
+    int e[3] = {0, 0, 0};
+    bool wild = false;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+        if (!quant_axis(bx.lo[c], bx.hi[c], bl[c], bh[c], valid, q[c], q[3 + c], e[c])) wild = true;
+    if (wild) {
+        q[0] = q[1] = q[2] = q[3] = q[4] = q[5] = 0;
+        e[0] = e[1] = e[2] = 0;
+    }
+    uint32_t ref[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        ref[i] = node[i] == RT_SENT ? RT_SENT : node[i] < L0 ? node[i] : (kWideLeaf | (node[i] - L0));
+    const uint32_t meta = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) |
+                          ((valid << 4 | (wild ? kWideWild : 0u)) << 24);
+    uint4* o = wnodes + (uint64_t)X * 4;
+    o[0] = make_uint4(__float_as_uint(bx.lo[0]), __float_as_uint(bx.lo[1]), __float_as_uint(bx.lo[2]), meta);
+    o[1] = make_uint4(q[0], q[1], q[2], q[3]);
+    o[2] = make_uint4(q[4], q[5], ref[0], ref[1]);
+    o[3] = make_uint4(ref[2], ref[3], 0u, 0u);
+}
+
+// The record's entries: X's children, each internal child replaced by its
+// two children (4 slots, RT_SENT-padded); topo_of(i) gives internal node i's
+// topology word.
+template <typename TopoOf>
+__device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoOf topo_of, uint32_t (&node)[4]) {
+    uint32_t l, r;
+    kids_of(tx, L0, l, r);
+    uint32_t a0 = l, a1 = RT_SENT, b0 = r, b1 = RT_SENT;
+    if (l < L0) kids_of(topo_of(l), L0, a0, a1);
+    if (r < L0) kids_of(topo_of(r), L0, b0, b1);
+    // preorder, packed to the front: a0 [a1] b0 [b1]
+    node[0] = a0;
+    node[1] = a1 != RT_SENT ? a1 : b0;
+    node[2] = a1 != RT_SENT ? b0 : b1;
+    node[3] = a1 != RT_SENT ? b1 : RT_SENT;
+}
+
 // One block = kRefitT consecutive sorted leaves [B0, B1), one thread per leaf.
 __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4* __restrict__ topo,
                                                          const uint32_t* __restrict__ parent,
@@ -354,7 +477,7 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
                                                          float* __restrict__ prebuf, float* __restrict__ sufbuf,
                                                          float* __restrict__ totals,
                                                          uint32_t* __restrict__ cross, uint32_t* cross_ctr,
-                                                         uint32_t cross_cap) {
+                                                         uint32_t cross_cap, uint4* __restrict__ wnodes) {
     constexpr int T = kRefitT, NW = T / 64;
     __shared__ Aabb s_box[2 * T];      // [0,T) leaves, [T,2T) internal nodes of the block
     __shared__ uint4 s_topo[T];
@@ -448,8 +571,19 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
     __syncthreads();
     RT_STAMP(3);
     if (cslot != RT_SENT) cross[s_cbase + cslot] = k;
-    // ---- coalesced store of this block's local internal nodes [B0, B1)
-    if (valid && k + 1 < n && tp.z >= B0 && tp.w < B1) store_node(nodes, k, s_box[T + tid], tp.x, tp.y);
+    // ---- coalesced store of this block's local internal nodes [B0, B1), and
+    // their K7w wide records (every box they need is in LDS)
+    if (valid && k + 1 < n && tp.z >= B0 && tp.w < B1) {
+        const Aabb bx = s_box[T + tid];
+        store_node(nodes, k, bx, tp.x, tp.y);
+        uint32_t node[4];
+        wide_entries(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; }, node);
+        uint32_t slot[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            slot[i] = node[i] == RT_SENT ? T + tid : node[i] >= L0 ? node[i] - L0 - B0 : T + node[i] - B0;
+        store_wide(wnodes, k, bx, node, [&](int i) { return s_box[slot[i]]; }, L0);
+    }
     RT_STAMP(4);
 }
 
@@ -524,6 +658,33 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
     }
 }
 
+// K7w records of the crossing internal nodes, once K6t has written their
+// boxes (every box such a record needs is then final in `nodes`).
+__global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ topo, const uint32_t* __restrict__ cross,
+                                                    const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
+                                                    const void* __restrict__ nodes, uint32_t n,
+                                                    uint4* __restrict__ wnodes) {
+    uint32_t pre[kCrossShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t sh = 0; sh < kCrossShards; ++sh) pre[sh + 1] = pre[sh] + cross_ctr[sh];
+    const uint32_t count = pre[kCrossShards];
+    const uint32_t L0 = n - 1;
+    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < count; q += gridDim.x * 256) {
+        uint32_t sh = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kCrossShards; ++j) sh += (q >= pre[j]) ? 1u : 0u;
+        const uint32_t X = cross[sh * cross_cap + (q - pre[sh])];
+        if (X >= L0) continue;
+        const uint4 tx = topo[X];
+        uint32_t node[4];
+        wide_entries(tx, L0, [&](uint32_t i) { return topo[i]; }, node);
+        const Aabb bx = load_aabb_node(nodes, X);
+        store_wide(wnodes, X, bx, node, [&](int i) { return load_aabb_node(nodes, node[i] == RT_SENT ? X : node[i]); },
+                   L0);
+    }
+}
+
 template __global__ void k_refit_cross<true>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
 template __global__ void k_refit_cross<false>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
 
@@ -561,6 +722,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.tri_s, N * 48);
     RT_ALLOC(b.parent, (2 * N - 1) * 4);
     RT_ALLOC(b.topo, N * 16);
+    RT_ALLOC(b.wnodes, N * 64);
     RT_ALLOC(b.prebuf, N * 24);
     RT_ALLOC(b.sufbuf, N * 24);
     RT_ALLOC(b.table, (uint64_t)b.levels * b.m_blocks * 24);
@@ -577,7 +739,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
 }
 
 void free_build(BuildBufs& b) {
-    void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.tri_s, b.parent, b.topo,
+    void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.tri_s, b.parent, b.topo, b.wnodes,
                   b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.partials, b.ticket, b.params, b.zero};
     for (void* p : ps)
         if (p) (void)hipFree(p);
@@ -616,7 +778,7 @@ hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const floa
 static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     hipLaunchKernelGGL(k_refit_local, dim3(m), dim3(kRefitT), 0, s, n, b.topo, b.parent, b.nodes, b.prebuf, b.sufbuf,
-                       b.table, b.cross, b.zero + kZCrossCtr, cross_cap(m));
+                       b.table, b.cross, b.zero + kZCrossCtr, cross_cap(m), b.wnodes);
     if (m <= 1) return hipGetLastError();
     if (m <= (uint32_t)kLdsTreeMaxBlocks) {
         uint32_t P = 1;
@@ -641,6 +803,8 @@ static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
         hipLaunchKernelGGL(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
+    hipLaunchKernelGGL(k_wide_cross, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr, cross_cap(m),
+                       b.nodes, n, b.wnodes);
     return hipGetLastError();
 }
 
@@ -666,6 +830,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     if ((e = rec(4)) != hipSuccess) return e;
     if (n && (e = launch_refit(b, n, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
+    if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K6 (records written with the boxes)
     return hipSuccess;
 }
 

@@ -136,9 +136,9 @@ const char* rt_version(void) { return "gpu_raytracer_amd 0.1 (gfx950)"; }
 rt_status rt_config_set(const char* key, int64_t value) {
     if (!key) return fail(RT_EINVAL, "null key");
     const std::string k(key);
-    if (k == "trace.variant" && (value == 0 || value == 1)) rt::g_trace_config.variant = (uint32_t)value;
-    else if (k == "trace.blocks" && value >= 1 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
-    else if (k == "trace.refill_min" && value >= 1 && value <= 64) rt::g_trace_config.refill_min = (uint32_t)value;
+    if (k == "trace.variant" && value >= 0 && value <= 2) rt::g_trace_config.variant = (uint32_t)value;
+    else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
+    else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
     else return fail(RT_EINVAL, "unknown config key or value out of range: " + k);
     return RT_OK;
 }
@@ -282,15 +282,16 @@ rt_status rt_bvh_build(rt_scene* s, double* ms_out) {
     hipError_t e = rt::launch_build(s->bufs, s->n, s->stream, &s->ev);
     if (e != hipSuccess) return hip_fail(e, "launch_build");
     HIPR(hipStreamSynchronize(s->stream));
-    float t[5];
-    for (int i = 0; i < 5; ++i) HIPR(hipEventElapsedTime(&t[i], s->ev.e[i], s->ev.e[i + 1]));
+    float t[6];
+    for (int i = 0; i < 6; ++i) HIPR(hipEventElapsedTime(&t[i], s->ev.e[i], s->ev.e[i + 1]));
     s->times.bounds = t[0];
     s->times.morton = t[1];
     s->times.sort = t[2];
     s->times.topology = t[3];
     s->times.refit = t[4];
+    s->times.wide = t[5];
     float tot = 0;
-    HIPR(hipEventElapsedTime(&tot, s->ev.e[0], s->ev.e[5]));
+    HIPR(hipEventElapsedTime(&tot, s->ev.e[0], s->ev.e[6]));
     s->times.total = tot;
     if (ms_out) *ms_out = tot;
     s->built = true;
@@ -319,6 +320,15 @@ rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* keys, uint32_
     return RT_OK;
 }
 
+rt_status rt_bvh_read_wide(const rt_scene* s, void* records) {
+    if (!s || !records) return fail(RT_EINVAL, "null argument");
+    if (!s->built) return fail(RT_EINVAL, "scene not built");
+    HIPR(hipSetDevice(s->device));
+    HIPR(hipStreamSynchronize(s->stream));
+    if (s->n >= 2) HIPR(hipMemcpy(records, s->bufs.wnodes, (size_t)(s->n - 1) * 64, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 // ------------------------------------------------------------------ render
 rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits_out,
                     uint8_t* rgba_out, double* ms_out) {
@@ -331,8 +341,9 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     if (hits_out && (st = grow(&s->d_hits, &s->hits_cap, nh * 16))) return st;
     if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
     HIPR(hipEventRecord(s->r0, s->stream));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
-                                    hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, s->d_work, s->stream);
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
+                                    false, hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, false, s->d_work,
+                                    s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipEventRecord(s->r1, s->stream));
     HIPR(hipStreamSynchronize(s->stream));
@@ -345,7 +356,7 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
 }
 
 static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
-                               uint32_t rank, uint32_t nranks, bool packed, uint64_t counters_out[2]) {
+                               uint32_t rank, uint32_t nranks, bool packed, bool binary, uint64_t counters_out[2]) {
     if (!s || !cam || !counters_out || !w || !h || !spp || !nranks || rank >= nranks)
         return fail(RT_EINVAL, "bad arguments");
     if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
@@ -353,8 +364,8 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     if (st) return st;
     if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 16));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks, packed,
-                                    nullptr, nullptr, s->d_ctr, s->d_work, s->stream);
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
+                                    nranks, packed, nullptr, nullptr, s->d_ctr, binary, s->d_work, s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(s->stream));
     HIPR(hipMemcpy(counters_out, s->d_ctr, 16, hipMemcpyDeviceToHost));
@@ -363,12 +374,17 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
 
 rt_status rt_render_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                              uint64_t counters_out[2]) {
-    return counters_impl(s, cam, w, h, spp, 0, 1, false, counters_out);
+    return counters_impl(s, cam, w, h, spp, 0, 1, false, true, counters_out);
+}
+
+rt_status rt_render_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
+                         uint64_t counters_out[2]) {
+    return counters_impl(s, cam, w, h, spp, 0, 1, false, false, counters_out);
 }
 
 rt_status rt_render_tiles_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                                    uint32_t rank, uint32_t nranks, uint64_t counters_out[2]) {
-    return counters_impl(s, cam, w, h, spp, rank, nranks, true, counters_out);
+    return counters_impl(s, cam, w, h, spp, rank, nranks, true, true, counters_out);
 }
 
 rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, void* d_hits,
@@ -380,8 +396,8 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     if (st) return st;
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false, d_hits,
-                                    d_rgba, nullptr, s->d_work, hs);
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
+                                    false, d_hits, d_rgba, nullptr, false, s->d_work, hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
@@ -406,8 +422,8 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     if (st) return st;
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks, true,
-                                    d_packed_hits, d_packed_rgba, nullptr, s->d_work, hs);
+    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
+                                    nranks, true, d_packed_hits, d_packed_rgba, nullptr, false, s->d_work, hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
@@ -557,8 +573,8 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
     HIPR(dts.alloc((size_t)(n ? n : 1) * 48));
     HIPR(dw.alloc(256));
     HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
-    HIPR(rt::launch_trace(dn.p, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
-                          counters ? dc.as<unsigned long long>() : nullptr, dw.as<uint32_t>(), 0));
+    HIPR(rt::launch_trace(dn.p, nullptr, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
+                          counters ? dc.as<unsigned long long>() : nullptr, true, dw.as<uint32_t>(), 0));
     HIPR(hipDeviceSynchronize());
     if (hits) HIPR(hipMemcpy(hits, dh.p, nh * 16, hipMemcpyDeviceToHost));
     if (rgba) HIPR(hipMemcpy(rgba, dr.p, (size_t)w * h * 4, hipMemcpyDeviceToHost));

@@ -72,6 +72,34 @@ constexpr uint32_t kPrefixInKernelMaxTiles = 256;      // <= 1M keys: cross-tile
 constexpr int kRefitT = 1024;                          // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
 
+// ---- K7w wide (4-ary) trace tree, derived from the binary tree after K6.
+// Record X (one per binary internal node X, 64 B) holds X's children with
+// every internal child replaced by its two children: 2-4 entries in §9.7
+// preorder.  Child boxes are quantized to 8 bits per plane on a power-of-two
+// grid anchored at X.lo, rounded OUTWARD and verified at build time with the
+// trace kernel's own arithmetic (wide_plane), so every quantized box
+// contains the exact box.
+//   w0 = {origin.x, origin.y, origin.z, meta}  meta: e+127 per axis in bytes
+//        0..2; byte 3 = valid-child mask << 4 | wild (non-finite: every
+//        valid child counts as hit)
+//   w1 = {qlo.x[4], qlo.y[4], qlo.z[4], qhi.x[4]}  (byte i = child i)
+//   w2 = {qhi.y[4], qhi.z[4], ref0, ref1}
+//   w3 = {ref2, ref3, 0, 0}        ref = internal X, or kWideLeaf | k
+constexpr uint32_t kWideLeaf = 0x80000000u;
+constexpr uint32_t kWideWild = 1u;
+// per-ray LDS stack entries (+1 spare slot, 6 B each, x 256 threads = 22.5 KB
+// per workgroup: the 7 workgroups per CU the kernel's registers allow);
+// overflow -> exact binary traversal from the overflowing record
+constexpr int kWideStack = 14;
+
+// plane = origin + q * 2^e, rounded once: q * 2^e is exact (q < 2^8 and
+// -126 <= e <= 119, so no overflow and an exact denormal at worst), hence
+// the fma equals the separately rounded add.  scale = 2^e as a float.
+__device__ __forceinline__ float wide_plane(float origin, uint32_t q, float scale) {
+    return fmaf((float)q, scale, origin);
+}
+__device__ __forceinline__ float wide_scale(int e) { return __uint_as_float((uint32_t)(e + 127) << 23); }
+
 
 }  // namespace rt
 

@@ -20,6 +20,7 @@ struct BuildBufs {
     float4* tri_s = nullptr;        // n x 48 B leaf-ordered {v0, e1, e2} for the trace
     uint32_t* parent = nullptr;     // 2n-1, unified index space
     uint4* topo = nullptr;          // n-1 x {left, esc, range_lo, range_hi}
+    uint4* wnodes = nullptr;        // n-1 x 64 B wide (4-ary) trace records, K7w
     uint32_t* counts = nullptr;     // 4 x [tile][256] radix-sort tile digit counts
     float* prebuf = nullptr;        // n x 6: block-prefix AABB at crossing ends
     float* sufbuf = nullptr;        // n x 6: block-suffix AABB at crossing ends
@@ -47,10 +48,10 @@ constexpr uint32_t kZEnd = 1056;        // words zeroed by K0 every build
 hipError_t alloc_build(BuildBufs& b, uint32_t n);
 void free_build(BuildBufs& b);
 
-struct BuildEvents { hipEvent_t e[6]; bool valid = false; };
+struct BuildEvents { hipEvent_t e[7]; bool valid = false; };
 
-// K0..K6 on `stream` for the n tris already in b.tris.  Sorted keys/vals end
-// in keys[0]/vals[0].  Records e[0..5] around the stages when ev != nullptr.
+// K0..K7w on `stream` for the n tris already in b.tris.  Sorted keys/vals end
+// in keys[0]/vals[0].  Records e[0..6] around the stages when ev != nullptr.
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev);
 
 // Stage launchers for parity entry points (buffers sized by the caller).
@@ -72,22 +73,23 @@ hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, fl
 
 struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 
-// Trace kernel selection / tuning (rt_config_set): variant 0 = one thread per
-// pixel, one 16x16 tile per workgroup (default); 1 = persistent wave-level
-// queue of 8x8 units with per-lane refill (work != nullptr required) --
-// measured 1.6x slower on soup-1M (profiles/ab_trace_r01_variants.log: lanes
-// at different depths touch more distinct lines per load), kept for
-// incoherent-ray workloads.
+// Trace kernel selection / tuning (rt_config_set); every setting gives
+// bit-identical hits and images.
 struct TraceConfig {
-    uint32_t variant = 0;
-    uint32_t blocks = 2048;     // persistent grid: 256 CUs x 8 workgroups of 4 waves
-    uint32_t refill_min = 16;   // refill when at least this many lanes are idle
+    uint32_t variant = 0;       // 0 wide per-pixel (default), 1 wide pool with refill, 2 binary per-pixel
+    uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
+    uint32_t stack_cap = 14;    // wide stack entries used, <= kWideStack (tests force the overflow path)
 };
 extern TraceConfig g_trace_config;
 
-hipError_t launch_trace(const void* nodes, const float4* tri_s, uint32_t n, const CamF& cam, uint32_t w,
-                        uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
-                        void* hits, void* rgba, unsigned long long* counters, uint32_t* work, hipStream_t s);
+// wnodes: the K7w wide records (nullptr: binary traversal only).  With
+// binary_counts the kernel is the binary one, so `counters` are the §9.7
+// node/triangle counts the oracle reports; otherwise they count the running
+// kernel's own fetches (wide: records and triangle loads).
+hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tri_s, uint32_t n, const CamF& cam,
+                        uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
+                        void* hits, void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
+                        hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
                          void* img, hipStream_t s);
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);

@@ -19,6 +19,7 @@ hipError_t read_stamps_trace(void* out, size_t bytes) { return hipMemcpyFromSymb
 
 struct Cam { float eye[3], w00[3], du[3], dv[3]; };
 
+
 __device__ __forceinline__ float dot3(const float* a, const float* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
 __device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
     o[0] = a[1] * b[2] - a[2] * b[1];
@@ -67,17 +68,21 @@ __device__ __forceinline__ bool intersect_tri(const float* o, const float* d, co
 // trip instead of two whenever some lane is at a leaf (+2-4 %,
 // profiles/ab_trace_r01_variants.log).  A well-formed tree visits each node
 // once; the guard and index checks only keep a malformed one from faulting.
+//
+// trace_ray_from resumes that loop at node `start` with the caller's
+// tb/hu/hv/hp: exact whenever every leaf before `start` in preorder has been
+// tested with §9.7's outcome (the wide traversal's overflow hand-off); a
+// start below a culled ancestor only adds box tests that miss.
 template <bool COUNT>
-__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float4* __restrict__ tri_s,
-                                                uint32_t n, const float* o, const float* d, float& tb, float& hu,
-                                                float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
+__device__ __forceinline__ void trace_ray_from(const char* __restrict__ nodes, const float4* __restrict__ tri_s,
+                                               uint32_t n, const float* o, const float* d, uint32_t start, float& tb,
+                                               float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
     float invd[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) invd[c] = 1.0f / d[c];
-    tb = __builtin_inff(); hu = 0.0f; hv = 0.0f; hp = RT_SENT;
     const uint32_t L0 = n ? n - 1 : 0;
     const uint32_t total = n ? 2 * n - 1 : 0;
-    uint32_t idx = n ? 0u : RT_SENT;
+    uint32_t idx = start;
     uint32_t pend = RT_SENT, pprim = 0;  // leaf whose triangle test is due
     for (uint32_t guard = 0; (idx < total || pend != RT_SENT) && guard <= total; ++guard) {
         float4 A, B;
@@ -90,11 +95,9 @@ __device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const 
             if (COUNT) ++ct;
             const float4* tp = tri_s + (uint64_t)pend * 3;
             const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
-            const float v0[3] = {T0.x, T0.y, T0.z};
-            const float e1[3] = {T0.w, T1.x, T1.y};
-            const float e2[3] = {T1.z, T1.w, T2.x};
+            const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
             float t, u, v;
-            if (intersect_e(o, d, v0, e1, e2, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = pprim; }
+            if (intersect_tri(o, d, tv, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = pprim; }
             pend = RT_SENT;
         }
         if (!node) break;
@@ -111,14 +114,200 @@ __device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const 
     }
 }
 
+template <bool COUNT>
+__device__ __forceinline__ void trace_ray(const char* __restrict__ nodes, const float4* __restrict__ tri_s,
+                                          uint32_t n, const float* o, const float* d, float& tb, float& hu,
+                                          float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
+    tb = __builtin_inff(); hu = 0.0f; hv = 0.0f; hp = RT_SENT;
+    trace_ray_from<COUNT>(nodes, tri_s, n, o, d, n ? 0u : RT_SENT, tb, hu, hv, hp, cn, ct);
+}
+
+// §9.7 slab test of the box lo/hi against [0, tb]; tn out.
+__device__ __forceinline__ bool slab_hit(const float* lo, const float* hi, const float* o, const float* invd, float tb,
+                                         float& tn) {
+    const float t0x = (lo[0] - o[0]) * invd[0], t1x = (hi[0] - o[0]) * invd[0];
+    const float t0y = (lo[1] - o[1]) * invd[1], t1y = (hi[1] - o[1]) * invd[1];
+    const float t0z = (lo[2] - o[2]) * invd[2], t1z = (hi[2] - o[2]) * invd[2];
+    tn = fmaxf(fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z)), 0.0f);
+    const float tf = fminf(fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)), tb);
+    return tn <= tf;
+}
+
+// Wide (4-ary) traversal over the K7w records, same hits as trace_ray.
+//
+// Why the result is identical, not just close: for a ray whose 1/d is
+// finite on every axis the slab interval is monotone in the box, so a box
+// that contains another never misses where the inner one hits (and a larger
+// tb never turns a hit into a miss).  The quantized child boxes contain the
+// exact ones, so every triangle §9.7 reaches is reached here, in the same
+// preorder; the leaf itself is tested with its EXACT box (recomputed from
+// the vertices with tri_bounds) against the current tb before
+// Moller-Trumbore.  By induction over the preorder, each leaf sees the same
+// tb as in §9.7, so the exact leaf test admits exactly the triangles §9.7
+// tests and nothing else; extra subtrees entered through the looser
+// quantized boxes contain only leaves whose exact test fails.  Rays with an
+// infinite 1/d component (d exactly 0 on an axis, where NaN slabs break
+// monotonicity) are traced by trace_ray; a ray whose stack would overflow
+// at record X hands over to trace_ray_from(X) with its current tb -- every
+// leaf before X in preorder is done and everything after X (the pending
+// stack included) is X's subtree or lies on X's escape chain.
+//
+// One wide_step fetches at most one record (cur) and one triangle
+// (pend, the leaf that precedes cur in preorder) with all loads in flight
+// together, tests the triangle first and the record's four children second,
+// so a step costs one memory round trip.  The children are tested without
+// branches; hit children after the first are pushed (in reverse) with
+// unconditional LDS writes into a spare slot and a predicated stack-pointer
+// increment.  Stack entries carry the child's entry distance tn; an entry
+// whose tn exceeds the (since shrunken) tb is skipped -- exactly the miss
+// its re-test would give, since tn <= tf held when it was pushed.
+//
+// The stack lives in LDS, entry-major ([entry][thread], conflict-free):
+// ref (4 B) + tn truncated to its upper 16 bits (2 B; tn >= +0, so the
+// truncation rounds down and the skip test stays conservative).  Slot `cap`
+// is the spare that takes the writes of children that are not pushed.
+struct WRay {
+    float d[3], invd[3];
+    float tb, hu, hv, ctn;
+    uint32_t hp, cur, pend, sp, steps;
+    bool fin;  // 1/d finite on every axis: the wide traversal applies
+};
+
+__device__ __forceinline__ void wray_init(const float* d, WRay& R) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        R.d[c] = d[c];
+        R.invd[c] = 1.0f / d[c];
+    }
+    R.fin = isfinite(R.invd[0]) && isfinite(R.invd[1]) && isfinite(R.invd[2]);
+    R.tb = __builtin_inff(); R.hu = 0.0f; R.hv = 0.0f; R.hp = RT_SENT;
+    R.cur = 0; R.pend = RT_SENT; R.ctn = 0.0f; R.sp = 0; R.steps = 0;
+}
+
+// §9.7 raygen of sample s of pixel (x, y)
+__device__ __forceinline__ void ray_dir(const Cam& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t spp, uint32_t s,
+                                        float* d) {
+    const uint32_t sidx = (y * W + x) * spp + s;
+    float jx = 0.5f, jy = 0.5f;
+    if (s > 0) {
+        const uint32_t h = pcg_hash(sidx);
+        jx = (float)(h >> 8) * 0x1p-24f;
+        jy = (float)(pcg_hash(h) >> 8) * 0x1p-24f;
+    }
+    const float px = (float)x + jx, py = (float)y + jy;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+}
+
+__device__ __forceinline__ void wray_setup(const Cam& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t spp,
+                                           uint32_t s, WRay& R) {
+    float d[3];
+    ray_dir(cam, x, y, W, spp, s, d);
+    wray_init(d, R);
+}
+
+__device__ __forceinline__ uint32_t bin_of(uint32_t ref, uint32_t L0) {
+    return (ref & kWideLeaf) ? L0 + (ref & ~kWideLeaf) : ref;
+}
+
+__device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const uint16_t* stn) {
+    if (R.sp == 0) { R.cur = RT_SENT; return; }
+    --R.sp;
+    R.cur = sref[R.sp * 256];
+    R.ctn = __uint_as_float((uint32_t)stn[R.sp * 256] << 16);
+}
+
+// Returns 0 = more steps, 1 = done, 2 = finish with
+// trace_ray_from(bin_of(R.cur)) (stack overflow at record R.cur, or the step
+// guard of a malformed tree).
+template <bool COUNT>
+__device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
+                                         const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
+                                         uint32_t& cn, uint32_t& ct) {
+    if (++R.steps > limit) return 2;
+    if (R.pend == RT_SENT) {
+        if (R.cur == RT_SENT) wide_pop(R, sref, stn);
+        if (R.cur != RT_SENT && (R.cur & kWideLeaf)) {
+            R.pend = R.cur;
+            wide_pop(R, sref, stn);
+        }
+    }
+    if (R.pend == RT_SENT && R.cur == RT_SENT) return 1;
+    const bool node = R.cur != RT_SENT && !(R.cur & kWideLeaf);
+    uint4 w0, w1, w2, w3;
+    if (node) {
+        const uint4* wp = wnodes + (uint64_t)R.cur * 4;
+        w0 = wp[0]; w1 = wp[1]; w2 = wp[2]; w3 = wp[3];
+    }
+    if (R.pend != RT_SENT) {
+        if (COUNT) ++ct;
+        const float4* tp = tri_s + (uint64_t)(R.pend & ~kWideLeaf) * 3;
+        const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
+        const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
+        float lo[3], hi[3], tn;
+        tri_bounds(tv, lo, hi);
+        if (slab_hit(lo, hi, o, R.invd, R.tb, tn)) {
+            float t, u, v;
+            if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) { R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(T2.y); }
+        }
+        R.pend = RT_SENT;
+    }
+    if (!node) return 0;
+    if (R.ctn > R.tb) { R.cur = RT_SENT; return 0; }
+    if (COUNT) ++cn;
+    const float org[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
+    float scl[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) scl[c] = __uint_as_float(((w0.w >> (8 * c)) & 0xFFu) << 23);  // 2^e
+    const uint32_t flags = w0.w >> 24;
+    const bool wild = flags & kWideWild;
+    const uint32_t qlo[3] = {w1.x, w1.y, w1.z}, qhi[3] = {w1.w, w2.x, w2.y};
+    const uint32_t ref[4] = {w2.z, w2.w, w3.x, w3.y};
+    bool hit[4];
+    float tn[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float lo[3], hi[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            lo[c] = wide_plane(org[c], (qlo[c] >> (8 * i)) & 0xFFu, scl[c]);
+            hi[c] = wide_plane(org[c], (qhi[c] >> (8 * i)) & 0xFFu, scl[c]);
+        }
+        const bool h = slab_hit(lo, hi, o, R.invd, R.tb, tn[i]);
+        hit[i] = ((flags >> (4 + i)) & 1u) && (h || wild);
+        if (wild) tn[i] = 0.0f;
+    }
+    bool earlier[4];
+    earlier[0] = false;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) earlier[i] = earlier[i - 1] || hit[i - 1];
+    bool over = false;
+#pragma unroll
+    for (int i = 3; i >= 1; --i) {
+        const bool push = hit[i] && earlier[i];
+        const uint32_t slot = R.sp < cap ? R.sp : cap;
+        sref[slot * 256] = ref[i];
+        stn[slot * 256] = (uint16_t)(__float_as_uint(tn[i]) >> 16);
+        over = over || (push && R.sp >= cap);
+        R.sp += (push && R.sp < cap) ? 1u : 0u;
+    }
+    if (over) return 2;
+    R.cur = hit[0] ? ref[0] : hit[1] ? ref[1] : hit[2] ? ref[2] : hit[3] ? ref[3] : RT_SENT;
+    R.ctn = hit[0] ? tn[0] : hit[1] ? tn[1] : hit[2] ? tn[2] : tn[3];
+    return 0;
+}
+
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
 
-template <bool COUNT, bool PACKED>
-__global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, const float4* __restrict__ tri_s, uint32_t n,
+template <bool COUNT, bool PACKED, bool WIDE>
+__global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                               uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t s_ref[WIDE ? (kWideStack + 1) * 256 : 1];
+    __shared__ uint16_t s_tn[WIDE ? (kWideStack + 1) * 256 : 1];
     // tile slot = block id: consecutive tiles go to different XCDs under the
     // round-robin dispatch, which balances the image's cheap and costly
     // bands over the 8 XCDs (an XCD-banded remap measured 1.2x slower)
@@ -147,9 +336,24 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
             float d[3];
 #pragma unroll
             for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
-            float tb, hu, hv;
-            uint32_t hp;
-            trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
+            float tb = 0.0f, hu = 0.0f, hv = 0.0f;
+            uint32_t hp = RT_SENT;
+            if (WIDE) {
+                WRay R;
+                wray_init(d, R);
+                int st = R.fin ? 0 : 2;
+                const char* nd = reinterpret_cast<const char*>(nodes);
+                while (st == 0) st = wide_step<COUNT>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16, s_ref + threadIdx.x,
+                                                      s_tn + threadIdx.x, cn, ct);
+                if (st == 2) {
+                    if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
+                    trace_ray_from<COUNT>(nd, tri_s, n, cam.eye, d, R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1),
+                                          R.tb, R.hu, R.hv, R.hp, cn, ct);
+                }
+                tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
+            } else {
+                trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
+            }
             if (hits) {
                 const uint64_t hi = PACKED ? ((uint64_t)slot * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
                 hits[hi] = make_float4(tb, hu, hv, __uint_as_float(hp));
@@ -203,137 +407,90 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
     }
 }
 
-// ---------------------------------------------------------------- persistent
-// Persistent wave-level work distribution with per-lane refill.  Each wave
-// pulls units -- 8x8 quarters of this rank's 16x16 tiles (t = rank +
-// b*nranks) -- from a work counter; lanes whose pixel is finished take the
-// next pixel of the current unit (in lane order), so a wave no longer idles
-// behind its slowest ray.  A lane owns a whole pixel (its spp samples in order), which
-// keeps the per-pixel sample average of §9.7 sequential.  The traversal step
-// is the exact §9.7 escape-link loop body: results are bit-identical.
+// ---------------------------------------------------------------- pool
+// Wide traversal with per-lane refill.  The rank's tiles are cut into 8x8
+// units (unit u = quarter u%4 of tile slot u/4); wave g of the grid owns
+// units g, g+G, g+2G, ... (G = waves in the grid -- a static, strided deal
+// with no atomics, so every wave gets units from all over the image).  A lane
+// whose pixel is finished takes the next pixel of the wave's current unit,
+// then of its next unit, so the wave no longer idles behind its slowest ray
+// until its very last unit.  A lane owns a whole pixel (its spp samples in
+// order), which keeps the §9.7 per-pixel sample average sequential.
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-struct RayState {
-    float d[3], invd[3];
-    float tb, hu, hv;
-    uint32_t hp, idx, guard;
-};
-
-__device__ __forceinline__ void ray_setup(const Cam& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t spp, uint32_t s,
-                                          uint32_t n, RayState& R) {
-    const uint32_t sidx = (y * W + x) * spp + s;
-    float jx = 0.5f, jy = 0.5f;
-    if (s > 0) {
-        const uint32_t h = pcg_hash(sidx);
-        jx = (float)(h >> 8) * 0x1p-24f;
-        jy = (float)(pcg_hash(h) >> 8) * 0x1p-24f;
-    }
-    const float px = (float)x + jx, py = (float)y + jy;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        R.d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
-        R.invd[c] = 1.0f / R.d[c];
-    }
-    R.tb = __builtin_inff(); R.hu = 0.0f; R.hv = 0.0f; R.hp = RT_SENT;
-    R.idx = n ? 0u : RT_SENT;
-    R.guard = 0;
-}
-
 template <bool COUNT, bool PACKED>
-__global__ __launch_bounds__(256) void k_trace_persist(const void* __restrict__ nodes_, const float4* __restrict__ tri_s,
-                                                       uint32_t n, Cam cam, uint32_t W, uint32_t H, uint32_t spp,
-                                                       uint32_t rank, uint32_t nranks, uint32_t tilesX,
-                                                       uint32_t ntiles_rank, uint32_t refill_min,
-                                                       float4* __restrict__ hits, uint32_t* __restrict__ rgba,
-                                                       unsigned long long* __restrict__ counters,
-                                                       uint32_t* __restrict__ work) {
-    const char* __restrict__ nodes = reinterpret_cast<const char*>(nodes_);
+__global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                                    uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
+                                                    Cam cam, uint32_t W, uint32_t H, uint32_t spp, uint32_t rank,
+                                                    uint32_t nranks, uint32_t tilesX, uint32_t nunits,
+                                                    float4* __restrict__ hits, uint32_t* __restrict__ rgba,
+                                                    unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
+    __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
+    uint32_t* sref = s_ref + threadIdx.x;
+    uint16_t* stn = s_tn + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t L0 = n ? n - 1 : 0;
-    const uint32_t total = n ? 2 * n - 1 : 0;
-    // lane state
-    bool active = false;
-    uint32_t x = 0, y = 0, lp = 0, tb_idx = 0, s = 0;
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    RayState R;
-    R.idx = RT_SENT;
-    // wave-uniform tile cursor
-    uint32_t cur_unit = 0, next = 64;
-    bool more = true;
-    uint32_t cn = 0, ct = 0;
+    const uint32_t G = gridDim.x * 4, g = blockIdx.x * 4 + (threadIdx.x >> 6);
     const float o[3] = {cam.eye[0], cam.eye[1], cam.eye[2]};
-
+    const uint32_t limit = 4 * n + 16;
+#ifdef RT_STAMPS
+    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t iters = 0, fb = 0;
+#endif
+    // wave-uniform cursor: current unit and the next pixel in it
+    uint32_t unit = g, next = 0;
+    // lane state
+    bool have = false;
+    uint32_t x = 0, y = 0, slot = 0, pl = 0, s = 0;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    WRay R;
+    uint32_t cn = 0, ct = 0;
     for (;;) {
-        // ---- refill idle lanes (wave-uniform control flow)
-        uint64_t idle = __ballot(!active);
-        if (more && (uint32_t)__popcll(idle) >= refill_min) {
-            while (idle && more) {
-                if (next >= 64) {
-                    uint32_t u = 0;
-                    if (lane == 0) u = atomicAdd(work, 1u);
-                    u = __shfl(u, 0, 64);
-                    if (u >= ntiles_rank * 4) { more = false; break; }
-                    cur_unit = u;
-                    next = 0;
+        // ---- refill: idle lanes take the next pixels, in lane order
+        uint64_t idle = __ballot(!have);
+        while (idle && unit < nunits) {
+            const uint32_t take = min((uint32_t)__popcll(idle), 64u - next);
+            const uint32_t pos = lanes_below(idle);
+            if (!have && pos < take) {
+                const uint32_t p = next + pos, q = unit & 3;
+                slot = unit >> 2;
+                const uint32_t lx = (q & 1) * 8 + (p & 7), ly = (q >> 1) * 8 + (p >> 3);
+                pl = ly * 16 + lx;
+                const uint32_t t = rank + slot * nranks;
+                x = (t % tilesX) * 16 + lx;
+                y = (t / tilesX) * 16 + ly;
+                if (x < W && y < H) {
+                    have = true;
+                    s = 0;
+                    cr = cg = cb = 0.0f;
+                    wray_setup(cam, x, y, W, spp, 0, R);
                 }
-                const uint32_t pos = lanes_below(idle);
-                const uint32_t nidle = (uint32_t)__popcll(idle);
-                const uint32_t take = nidle < 64 - next ? nidle : 64 - next;
-                if (!active && pos < take) {
-                    // unit = one 8x8 quarter of a 16x16 tile
-                    const uint32_t p = next + pos, sub = cur_unit & 3;
-                    lp = ((sub >> 1) * 8 + (p >> 3)) * 16 + (sub & 1) * 8 + (p & 7);
-                    tb_idx = cur_unit >> 2;
-                    const uint32_t t = rank + tb_idx * nranks;
-                    x = (t % tilesX) * 16 + (lp & 15);
-                    y = (t / tilesX) * 16 + (lp >> 4);
-                    if (x < W && y < H) {
-                        active = true;
-                        s = 0;
-                        cr = cg = cb = 0.0f;
-                        ray_setup(cam, x, y, W, spp, 0, n, R);
-                    }
-                }
-                next += take;
-                idle = __ballot(!active);
             }
+            next += take;
+            if (next >= 64) { unit += G; next = 0; }
+            idle = __ballot(!have);
         }
-        if (__ballot(active) == 0) break;  // every lane idle and no work left
-        // ---- one escape-link traversal step (§9.7)
-        if (active) {
-            if (R.idx < total && R.guard < total) {
-                ++R.guard;
-                const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)R.idx * 32);
-                const float4 A = np[0], B = np[1];
-                if (COUNT) ++cn;
-                const float t0x = (A.x - o[0]) * R.invd[0], t1x = (A.w - o[0]) * R.invd[0];
-                const float t0y = (A.y - o[1]) * R.invd[1], t1y = (B.x - o[1]) * R.invd[1];
-                const float t0z = (A.z - o[2]) * R.invd[2], t1z = (B.y - o[2]) * R.invd[2];
-                const float tn = fmaxf(fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z)), 0.0f);
-                const float tf = fminf(fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)), R.tb);
-                const uint32_t na = __float_as_uint(B.z), esc = __float_as_uint(B.w);
-                if (!(tn <= tf)) {
-                    R.idx = esc;
-                } else if (R.idx >= L0) {
-                    if (COUNT) ++ct;
-                    const float4* tp = tri_s + (uint64_t)(R.idx - L0) * 3;
-                    const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
-                    const float v0[3] = {T0.x, T0.y, T0.z};
-                    const float e1[3] = {T0.w, T1.x, T1.y};
-                    const float e2[3] = {T1.z, T1.w, T2.x};
-                    float t, u, v;
-                    if (intersect_e(o, R.d, v0, e1, e2, R.tb, t, u, v)) { R.tb = t; R.hu = u; R.hv = v; R.hp = na; }
-                    R.idx = esc;
-                } else {
-                    R.idx = na;
-                }
-            } else {
-                // sample finished
+        if (__ballot(have) == 0) break;  // no ray in flight and no units left
+#ifdef RT_STAMPS
+        ++iters;
+#endif
+        if (have) {
+            int st = R.fin ? wide_step<COUNT>(R, wnodes, tri_s, o, wcap, limit, sref, stn, cn, ct) : 2;
+            if (st == 2) {
+#ifdef RT_STAMPS
+                fb += 1u << 16;
+#endif
+                if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
+                trace_ray_from<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, o, R.d,
+                                      R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1), R.tb, R.hu, R.hv, R.hp, cn,
+                                      ct);
+                st = 1;
+            }
+            if (st == 1) {
                 if (hits) {
-                    const uint64_t hi = PACKED ? ((uint64_t)tb_idx * 256 + lp) * spp + s
-                                               : (uint64_t)((y * W + x) * spp + s);
+                    const uint64_t hi = PACKED ? ((uint64_t)slot * 256 + pl) * spp + s : (uint64_t)(y * W + x) * spp + s;
                     hits[hi] = make_float4(R.tb, R.hu, R.hv, __uint_as_float(R.hp));
                 }
                 if (R.hp != RT_SENT) {
@@ -344,19 +501,31 @@ __global__ __launch_bounds__(256) void k_trace_persist(const void* __restrict__ 
                     cr = cr + 0.0f; cg = cg + 0.0f; cb = cb + 0.0f;
                 }
                 if (++s < spp) {
-                    ray_setup(cam, x, y, W, spp, s, n, R);
+                    wray_setup(cam, x, y, W, spp, s, R);
                 } else {
                     if (rgba) {
                         const float sc = 1.0f / (float)spp;
                         const uint32_t px = q8(cr * sc) | (q8(cg * sc) << 8) | (q8(cb * sc) << 16) | (255u << 24);
-                        const uint64_t pi = PACKED ? (uint64_t)tb_idx * 256 + lp : (uint64_t)y * W + x;
+                        const uint64_t pi = PACKED ? (uint64_t)slot * 256 + pl : (uint64_t)y * W + x;
                         rgba[pi] = px;
                     }
-                    active = false;
+                    have = false;
                 }
             }
         }
     }
+#ifdef RT_STAMPS
+    uint32_t fbw = fb;
+    for (int off = 32; off >= 1; off >>= 1) fbw += __shfl_xor(fbw, off, 64);
+    if (lane == 0) {
+        const uint64_t wslot = (uint64_t)g * 4;
+        g_rt_stamps[wslot + 0] = st0;
+        g_rt_stamps[wslot + 1] = __builtin_amdgcn_s_memrealtime();
+        g_rt_stamps[wslot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                 ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+        g_rt_stamps[wslot + 3] = iters | ((uint64_t)fbw << 16);
+    }
+#endif
     if (COUNT) {
         unsigned long long a = cn, bsum = ct;
 #pragma unroll
@@ -419,9 +588,9 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) 
 
 TraceConfig g_trace_config;
 
-hipError_t launch_trace(const void* nodes, const float4* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
-                        uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits, void* rgba,
-                        unsigned long long* counters, uint32_t* work, hipStream_t s) {
+hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tris, uint32_t n, const CamF& c,
+                        uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits,
+                        void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work, hipStream_t s) {
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
     if (!nb) return hipSuccess;
     Cam cam;
@@ -431,30 +600,51 @@ hipError_t launch_trace(const void* nodes, const float4* tris, uint32_t n, const
     const uint32_t tilesX = (w + 15) / 16;
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
-    if (g_trace_config.variant == 1 && work) {
-        hipError_t e = hipMemsetAsync(work, 0, 4, s);
-        if (e != hipSuccess) return e;
-        const uint32_t waves = g_trace_config.blocks * 4;
-        const uint32_t grid = nb * 4 < waves ? nb : g_trace_config.blocks;  // 4 units (8x8) per tile
-        const uint32_t rmin = g_trace_config.refill_min;
-#define RT_PERSIST(C, P)                                                                                          \
-    hipLaunchKernelGGL((k_trace_persist<C, P>), dim3(grid), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, \
-                       nranks, tilesX, nb, rmin, H, R, counters, work)
-        if (counters) {
-            if (packed) RT_PERSIST(true, true); else RT_PERSIST(true, false);
-        } else {
-            if (packed) RT_PERSIST(false, true); else RT_PERSIST(false, false);
+    const uint32_t cap = g_trace_config.stack_cap;
+    if (g_trace_config.variant == 1 && wnodes && n >= 2 && !binary_counts) {
+        const uint32_t nunits = nb * 4;
+        uint32_t blocks = g_trace_config.blocks;
+        if (!blocks) {  // auto: exactly the resident capacity (one wave per SIMD slot, no second round)
+            static uint32_t resident = 0;
+            if (!resident) {
+                int per_cu = 0, dev = 0, cus = 0;
+                hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &per_cu, reinterpret_cast<const void*>(k_trace_pool<false, false>), 256, 0);
+                if (e != hipSuccess) return e;
+                if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+                if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+                    return e;
+                resident = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
+            }
+            blocks = resident;
         }
-#undef RT_PERSIST
+        const uint32_t grid = min(blocks, (nunits + 3) / 4);
+#define RT_POOL(C, P)                                                                                               \
+    hipLaunchKernelGGL((k_trace_pool<C, P>), dim3(grid), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
+                       rank, nranks, tilesX, nunits, H, R, counters)
+        if (counters) {
+            if (packed) RT_POOL(true, true); else RT_POOL(true, false);
+        } else {
+            if (packed) RT_POOL(false, true); else RT_POOL(false, false);
+        }
+#undef RT_POOL
         return hipGetLastError();
     }
+    // wide (4-ary) traversal unless asked for the binary one: variant 2, no
+    // K7w records (stage entry points), n < 2, or binary work counters
+    const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2 && !binary_counts;
+#define RT_TRACE(C, P, WI)                                                                                          \
+    hipLaunchKernelGGL((k_trace<C, P, WI>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
+                       rank, nranks, tilesX, H, R, counters)
+#define RT_TRACE_W(C, P) \
+    if (wide) RT_TRACE(C, P, true); else RT_TRACE(C, P, false)
     if (counters) {
-        if (packed) hipLaunchKernelGGL((k_trace<true, true>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
-        else hipLaunchKernelGGL((k_trace<true, false>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
+        if (packed) { RT_TRACE_W(true, true); } else { RT_TRACE_W(true, false); }
     } else {
-        if (packed) hipLaunchKernelGGL((k_trace<false, true>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
-        else hipLaunchKernelGGL((k_trace<false, false>), dim3(nb), dim3(256), 0, s, nodes, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters);
+        if (packed) { RT_TRACE_W(false, true); } else { RT_TRACE_W(false, false); }
     }
+#undef RT_TRACE_W
+#undef RT_TRACE
     return hipGetLastError();
 }
 

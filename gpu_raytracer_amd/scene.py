@@ -45,6 +45,7 @@ class BuildTimes:
     sort: float
     topology: float
     refit: float
+    wide: float
     total: float
 
 
@@ -115,7 +116,14 @@ class Scene:
     def build_times(self) -> BuildTimes:
         t = rt_build_times()
         call("rt_bvh_build_times", self._h, C.byref(t))
-        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.total)
+        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total)
+
+    def read_wide(self) -> np.ndarray:
+        """K7w wide records as uint32[(n-1), 16] (layout: csrc/rt_device.h)."""
+        n = self.num_tris
+        rec = np.zeros((max(n - 1, 1), 16), np.uint32)
+        call("rt_bvh_read_wide", self._h, _p(rec))
+        return rec[: max(n - 1, 0)]
 
     def read_bvh(self) -> dict:
         n = self.num_tris
@@ -140,8 +148,15 @@ class Scene:
         return hb, rb, ms.value
 
     def render_counters(self, cam: rt_camera, w: int, h: int, spp: int = 1) -> np.ndarray:
+        """§9.7 binary-traversal counters (the oracle's): nodes fetched, tris tested."""
         c = np.zeros(2, np.uint64)
         call("rt_render_counters", self._h, C.byref(cam), w, h, spp, _p(c))
+        return c
+
+    def render_work(self, cam: rt_camera, w: int, h: int, spp: int = 1) -> np.ndarray:
+        """The configured trace kernel's own fetches: node records, triangle records."""
+        c = np.zeros(2, np.uint64)
+        call("rt_render_work", self._h, C.byref(cam), w, h, spp, _p(c))
         return c
 
     def render_device(self, cam, w, h, spp, d_rgba: int = 0, d_hits: int = 0, stream: int = 0,

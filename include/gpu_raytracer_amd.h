@@ -56,9 +56,10 @@ typedef enum {
     RT_ECOMM = -5
 } rt_status;
 
-/* per-stage device times of the last build, milliseconds (hipEvents) */
+/* per-stage device times of the last build, milliseconds (hipEvents);
+ * wide = K7w, the 4-ary trace records derived from the binary tree */
 typedef struct {
-    double bounds, morton, sort, topology, refit, total;
+    double bounds, morton, sort, topology, refit, wide, total;
 } rt_build_times;
 
 /* ---- scene ingest (SURVEY.md §8(b) rt_scene_load_obj / rt_scene_from_soup) ---- */
@@ -84,15 +85,23 @@ rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out);
  * sorted keys/vals[n], parent[2n-1], bounds[9] = lo[3], hi[3], inv[3]. */
 rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* sorted_keys,
                       uint32_t* sorted_vals, uint32_t* parent, float* bounds9);
+/* Read back the K7w wide trace records: (n-1) x 64 B, one per binary internal
+ * node (layout: gpu_raytracer_amd/csrc/rt_device.h); nothing for n < 2. */
+rt_status rt_bvh_read_wide(const rt_scene* s, void* records);
 
 /* ---- render (SURVEY.md §8(b) rt_render).  hits_out: w*h*spp records,
  * rgba_out: w*h*4 bytes; either may be NULL.  Single GPU; multi-GPU is the
  * tile API below driven by one process per GPU (bench.py / torch.distributed). */
 rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                     rt_hit* hits_out, uint8_t* rgba_out, double* ms_out);
-/* deterministic work counters of a render: [0] nodes fetched, [1] tris tested */
+/* deterministic work counters of a render with the §9.7 binary traversal
+ * (the oracle's counters): [0] nodes fetched, [1] tris tested */
 rt_status rt_render_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,
                              uint32_t spp, uint64_t counters_out[2]);
+/* work of the configured (default: wide) trace kernel itself: [0] node
+ * records fetched (64 B wide / 32 B binary), [1] triangle records loaded */
+rt_status rt_render_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,
+                         uint32_t spp, uint64_t counters_out[2]);
 /* Device-resident render of the full image into caller device buffers
  * (d_hits: w*h*spp records or NULL; d_rgba: w*h*4 bytes or NULL) on `stream`
  * (NULL = the scene's stream).  Asynchronous unless ms_out != NULL, in which
@@ -146,10 +155,13 @@ rt_status rt_stage_minmax(int device, uint32_t count, const float* a, const floa
 rt_status rt_framebuffer_dump_ppm(const uint8_t* rgba, uint32_t w, uint32_t h, const char* path);
 rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
 
-/* Tuning knobs (process-wide): "trace.variant" 0 = one thread per pixel
- * (default), 1 = persistent tile queue with per-lane refill; "trace.blocks"
- * persistent grid size; "trace.refill_min" idle lanes that trigger a refill.
- * Results are bit-identical for every setting. */
+/* Tuning knobs (process-wide): "trace.variant" 0 = one thread per pixel,
+ * wide (4-ary) traversal over the K7w records (default), 1 = wide traversal
+ * with per-lane refill from 8x8-pixel units dealt statically to a resident
+ * grid, 2 = one thread per pixel, binary traversal; "trace.blocks" variant-1
+ * grid (0 = resident capacity); "trace.stack_cap" (1..14) wide-traversal
+ * stack entries -- rays that need more are re-traced by the binary
+ * traversal.  Results are bit-identical for every setting. */
 rt_status rt_config_set(const char* key, int64_t value);
 
 const char* rt_last_error(void);

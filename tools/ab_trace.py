@@ -17,20 +17,23 @@ s.build()
 cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
 hits = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
-sel = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "p8-b2048"]
+sel = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "2"]
 variants = []
 for v in sel:
     if v == "0":
-        variants.append(("default (deferred leaf test)", {"trace.variant": 0}))
-    elif v.startswith("p"):  # pR-bB: persistent, refill_min R, B blocks
-        a, b = v[1:].split("-b")
-        variants.append((v, {"trace.variant": 1, "trace.refill_min": int(a), "trace.blocks": int(b)}))
+        variants.append(("wide (default)", {"trace.variant": 0}))
+    elif v == "2":
+        variants.append(("binary (deferred leaf test)", {"trace.variant": 2}))
+    elif v.startswith("pool"):  # pool[-bB]: wide with per-lane refill, B blocks (0 = resident capacity)
+        b = int(v.split("-b")[1]) if "-b" in v else 0
+        variants.append((v, {"trace.variant": 1, "trace.blocks": b}))
 cnts = {}
 for name, cfg in variants:
     for k, v in cfg.items():
         R.config_set(k, v)
     cnts[name] = tuple(int(c) for c in s.render_counters(cam, w, h, spp))
-print("counters", cnts)
+    print(name, "kernel work (node records, tri records):", [int(c) for c in s.render_work(cam, w, h, spp)])
+print("binary counters", cnts)
 assert len(set(cnts.values())) == 1, "variants disagree on work counters"
 ref = None
 times = {name: [] for name, _ in variants}

@@ -1,17 +1,19 @@
 #!/bin/bash
-# PMC passes on the trace kernel (tools/trace_only.py); one counter group per pass.
+# PMC passes on the trace kernel (tools/trace_only.py); one counter group per
+# pass.  Usage: bash tools/pmc_trace.sh <tag> [trace.variant]
 set -e
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_${1:-trace}
+VAR=${2:-0}
 mkdir -p $OUT
-i=${2:-1}
+i=0
 for grp in \
+  "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" \
   "TA_TA_BUSY TA_FLAT_READ_WAVEFRONTS GRBM_GUI_ACTIVE" \
-  "TA_ADDR_STALLED_BY_TC_CYCLES TA_DATA_STALLED_BY_TC_CYCLES" \
   "TCP_TOTAL_CACHE_ACCESSES TCP_TCC_READ_REQ" \
   "TCC_HIT TCC_MISS" \
-  "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH"; do
-  timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -- python3 tools/trace_only.py 3 > $OUT/p$i.log 2>&1
+  "SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS"; do
+  timeout -k 10 120 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -- python3 tools/trace_only.py 3 $VAR > $OUT/p$i.log 2>&1
   i=$((i+1))
 done
 echo pmc done

@@ -9,6 +9,8 @@ import gpu_raytracer_amd as R  # noqa: E402
 from gpu_raytracer_amd.scenes import SOUP_VIEW as V  # noqa: E402
 
 k = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+if len(sys.argv) > 2:
+    R.config_set("trace.variant", int(sys.argv[2]))
 w, h = 1920, 1080
 s = R.Scene.generate_soup(1_000_000, 1)
 s.build()
