@@ -36,7 +36,7 @@ struct rt_scene {
     void* d_rgba = nullptr;
     size_t rgba_cap = 0;
     unsigned long long* d_ctr = nullptr;
-    uint32_t* d_work = nullptr;  // persistent-trace tile counter
+    uint32_t* d_work = nullptr;  // pool-trace unit counters
     hipEvent_t r0 = nullptr, r1 = nullptr;
 };
 
@@ -77,7 +77,7 @@ rt_status ensure_stream(rt_scene* s) {
         s->ev.valid = true;
         HIPR(hipEventCreate(&s->r0));
         HIPR(hipEventCreate(&s->r1));
-        HIPR(hipMalloc((void**)&s->d_work, 256));
+        HIPR(hipMalloc((void**)&s->d_work, 4096));  // kPoolCounters x 128 B
     }
     return RT_OK;
 }
@@ -138,6 +138,7 @@ rt_status rt_config_set(const char* key, int64_t value) {
     const std::string k(key);
     if (k == "trace.variant" && value >= 0 && value <= 2) rt::g_trace_config.variant = (uint32_t)value;
     else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
+    else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
     else return fail(RT_EINVAL, "unknown config key or value out of range: " + k);
     return RT_OK;
@@ -571,7 +572,7 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
     }
     DevBuf dts, dw;
     HIPR(dts.alloc((size_t)(n ? n : 1) * 48));
-    HIPR(dw.alloc(256));
+    HIPR(dw.alloc(4096));
     HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
     HIPR(rt::launch_trace(dn.p, nullptr, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
                           counters ? dc.as<unsigned long long>() : nullptr, true, dw.as<uint32_t>(), 0));

@@ -91,6 +91,7 @@ constexpr uint32_t kWideWild = 1u;
 // per workgroup: the 7 workgroups per CU the kernel's registers allow);
 // overflow -> exact binary traversal from the overflowing record
 constexpr int kWideStack = 14;
+constexpr uint32_t kPoolCounters = 32;  // pool-trace unit counters, 128 B apart (work buffer >= 4 KiB)
 
 // plane = origin + q * 2^e, rounded once: q * 2^e is exact (q < 2^8 and
 // -126 <= e <= 119, so no overflow and an exact denormal at worst), hence

@@ -78,6 +78,7 @@ struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 struct TraceConfig {
     uint32_t variant = 0;       // 0 wide per-pixel (default), 1 wide pool with refill, 2 binary per-pixel
     uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
+    uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
     uint32_t stack_cap = 14;    // wide stack entries used, <= kWideStack (tests force the overflow path)
 };
 extern TraceConfig g_trace_config;

@@ -210,26 +210,27 @@ __device__ __forceinline__ uint32_t bin_of(uint32_t ref, uint32_t L0) {
     return (ref & kWideLeaf) ? L0 + (ref & ~kWideLeaf) : ref;
 }
 
+template <int NT>
 __device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const uint16_t* stn) {
     if (R.sp == 0) { R.cur = RT_SENT; return; }
     --R.sp;
-    R.cur = sref[R.sp * 256];
-    R.ctn = __uint_as_float((uint32_t)stn[R.sp * 256] << 16);
+    R.cur = sref[R.sp * NT];
+    R.ctn = __uint_as_float((uint32_t)stn[R.sp * NT] << 16);
 }
 
 // Returns 0 = more steps, 1 = done, 2 = finish with
 // trace_ray_from(bin_of(R.cur)) (stack overflow at record R.cur, or the step
 // guard of a malformed tree).
-template <bool COUNT>
+template <bool COUNT, int NT>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
                                          uint32_t& cn, uint32_t& ct) {
     if (++R.steps > limit) return 2;
     if (R.pend == RT_SENT) {
-        if (R.cur == RT_SENT) wide_pop(R, sref, stn);
+        if (R.cur == RT_SENT) wide_pop<NT>(R, sref, stn);
         if (R.cur != RT_SENT && (R.cur & kWideLeaf)) {
             R.pend = R.cur;
-            wide_pop(R, sref, stn);
+            wide_pop<NT>(R, sref, stn);
         }
     }
     if (R.pend == RT_SENT && R.cur == RT_SENT) return 1;
@@ -286,8 +287,8 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     for (int i = 3; i >= 1; --i) {
         const bool push = hit[i] && earlier[i];
         const uint32_t slot = R.sp < cap ? R.sp : cap;
-        sref[slot * 256] = ref[i];
-        stn[slot * 256] = (uint16_t)(__float_as_uint(tn[i]) >> 16);
+        sref[slot * NT] = ref[i];
+        stn[slot * NT] = (uint16_t)(__float_as_uint(tn[i]) >> 16);
         over = over || (push && R.sp >= cap);
         R.sp += (push && R.sp < cap) ? 1u : 0u;
     }
@@ -299,22 +300,27 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
 
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
 
-template <bool COUNT, bool PACKED, bool WIDE>
-__global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+template <bool COUNT, bool PACKED, bool WIDE, int NT>
+__global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t s_ref[WIDE ? (kWideStack + 1) * 256 : 1];
-    __shared__ uint16_t s_tn[WIDE ? (kWideStack + 1) * 256 : 1];
-    // tile slot = block id: consecutive tiles go to different XCDs under the
-    // round-robin dispatch, which balances the image's cheap and costly
-    // bands over the 8 XCDs (an XCD-banded remap measured 1.2x slower)
-    const uint32_t slot = blockIdx.x;
+    __shared__ uint32_t s_ref[WIDE ? (kWideStack + 1) * NT : 1];
+    __shared__ uint16_t s_tn[WIDE ? (kWideStack + 1) * NT : 1];
+    // tile slot from the block id: consecutive tiles go to different XCDs
+    // under the round-robin dispatch, which balances the image's cheap and
+    // costly bands over the 8 XCDs (an XCD-banded remap measured 1.2x
+    // slower).  NT = 256: one 16x16 tile per block, wave w = quadrant w;
+    // NT = 64: one quadrant (8x8) per block, so a finished wave frees its
+    // slot and LDS at once instead of waiting for the tile's slowest wave.
+    constexpr uint32_t WPB = NT / 64;
+    const uint32_t gw = blockIdx.x * WPB + (threadIdx.x >> 6);  // global wave id
+    const uint32_t slot = gw >> 2;
     const uint32_t t = rank + slot * nranks;
     const uint32_t tx = t % tilesX, ty = t / tilesX;
-    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t l = threadIdx.x & 63, w = gw & 3;
     const uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
@@ -343,8 +349,8 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
                 wray_init(d, R);
                 int st = R.fin ? 0 : 2;
                 const char* nd = reinterpret_cast<const char*>(nodes);
-                while (st == 0) st = wide_step<COUNT>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16, s_ref + threadIdx.x,
-                                                      s_tn + threadIdx.x, cn, ct);
+                while (st == 0) st = wide_step<COUNT, NT>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
+                                                          s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct);
                 if (st == 2) {
                     if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
                     trace_ray_from<COUNT>(nd, tri_s, n, cam.eye, d, R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1),
@@ -384,7 +390,7 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
             sm += __shfl_xor(sm, o, 64);
         }
         if (l == 0) {
-            const uint64_t wslot = ((uint64_t)blockIdx.x * 4 + w) * 4;
+            const uint64_t wslot = (uint64_t)gw * 4;
             g_rt_stamps[wslot + 0] = st0;
             g_rt_stamps[wslot + 1] = __builtin_amdgcn_s_memrealtime();
             g_rt_stamps[wslot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
@@ -409,9 +415,9 @@ __global__ __launch_bounds__(256) void k_trace(const void* __restrict__ nodes, c
 
 // ---------------------------------------------------------------- pool
 // Wide traversal with per-lane refill.  The rank's tiles are cut into 8x8
-// units (unit u = quarter u%4 of tile slot u/4); wave g of the grid owns
-// units g, g+G, g+2G, ... (G = waves in the grid -- a static, strided deal
-// with no atomics, so every wave gets units from all over the image).  A lane
+// units (unit u = quarter u%4 of tile slot u/4), dealt to the waves of a
+// resident grid through sharded atomic counters (a single counter hit by
+// every wave serialises).  A lane
 // whose pixel is finished takes the next pixel of the wave's current unit,
 // then of its next unit, so the wave no longer idles behind its slowest ray
 // until its very last unit.  A lane owns a whole pixel (its spp samples in
@@ -426,21 +432,31 @@ __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nod
                                                     Cam cam, uint32_t W, uint32_t H, uint32_t spp, uint32_t rank,
                                                     uint32_t nranks, uint32_t tilesX, uint32_t nunits,
                                                     float4* __restrict__ hits, uint32_t* __restrict__ rgba,
-                                                    unsigned long long* __restrict__ counters) {
+                                                    unsigned long long* __restrict__ counters,
+                                                    uint32_t* __restrict__ work) {
     __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
     __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
     uint32_t* sref = s_ref + threadIdx.x;
     uint16_t* stn = s_tn + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t G = gridDim.x * 4, g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
     const float o[3] = {cam.eye[0], cam.eye[1], cam.eye[2]};
     const uint32_t limit = 4 * n + 16;
 #ifdef RT_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
     uint32_t iters = 0, fb = 0;
 #endif
-    // wave-uniform cursor: current unit and the next pixel in it
-    uint32_t unit = g, next = 0;
+    // wave-uniform cursor: current unit and the next pixel in it.  Units are
+    // dealt dynamically from kPoolCounters counters (one 128-B line each;
+    // counter c owns units c, c+C, c+2C, ...), wave g drawing from c = g % C.
+    const uint32_t cidx = g % kPoolCounters;
+    auto grab = [&]() -> uint32_t {
+        uint32_t j = 0;
+        if (lane == 0) j = atomicAdd(&work[cidx * 32], 1u);
+        j = __shfl(j, 0, 64);
+        return cidx + kPoolCounters * j;
+    };
+    uint32_t unit = grab(), next = 0;
     // lane state
     bool have = false;
     uint32_t x = 0, y = 0, slot = 0, pl = 0, s = 0;
@@ -469,7 +485,7 @@ __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nod
                 }
             }
             next += take;
-            if (next >= 64) { unit += G; next = 0; }
+            if (next >= 64) { unit = grab(); next = 0; }
             idle = __ballot(!have);
         }
         if (__ballot(have) == 0) break;  // no ray in flight and no units left
@@ -477,7 +493,7 @@ __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nod
         ++iters;
 #endif
         if (have) {
-            int st = R.fin ? wide_step<COUNT>(R, wnodes, tri_s, o, wcap, limit, sref, stn, cn, ct) : 2;
+            int st = R.fin ? wide_step<COUNT, 256>(R, wnodes, tri_s, o, wcap, limit, sref, stn, cn, ct) : 2;
             if (st == 2) {
 #ifdef RT_STAMPS
                 fb += 1u << 16;
@@ -601,8 +617,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     const uint32_t cap = g_trace_config.stack_cap;
-    if (g_trace_config.variant == 1 && wnodes && n >= 2 && !binary_counts) {
+    if (g_trace_config.variant == 1 && wnodes && n >= 2 && !binary_counts && work) {
         const uint32_t nunits = nb * 4;
+        hipError_t me = hipMemsetAsync(work, 0, kPoolCounters * 128, s);
+        if (me != hipSuccess) return me;
         uint32_t blocks = g_trace_config.blocks;
         if (!blocks) {  // auto: exactly the resident capacity (one wave per SIMD slot, no second round)
             static uint32_t resident = 0;
@@ -621,7 +639,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         const uint32_t grid = min(blocks, (nunits + 3) / 4);
 #define RT_POOL(C, P)                                                                                               \
     hipLaunchKernelGGL((k_trace_pool<C, P>), dim3(grid), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
-                       rank, nranks, tilesX, nunits, H, R, counters)
+                       rank, nranks, tilesX, nunits, H, R, counters, work)
         if (counters) {
             if (packed) RT_POOL(true, true); else RT_POOL(true, false);
         } else {
@@ -633,11 +651,18 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     // wide (4-ary) traversal unless asked for the binary one: variant 2, no
     // K7w records (stage entry points), n < 2, or binary work counters
     const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2 && !binary_counts;
-#define RT_TRACE(C, P, WI)                                                                                          \
-    hipLaunchKernelGGL((k_trace<C, P, WI>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
-                       rank, nranks, tilesX, H, R, counters)
-#define RT_TRACE_W(C, P) \
-    if (wide) RT_TRACE(C, P, true); else RT_TRACE(C, P, false)
+    const bool small = g_trace_config.wg == 64;
+#define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
+    hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
+                       cam, w, h, spp, rank, nranks, tilesX, H, R, counters)
+#define RT_TRACE(C, P, WI) \
+    if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
+#define RT_TRACE_W(C, P)           \
+    if (wide) {                    \
+        RT_TRACE(C, P, true);      \
+    } else {                       \
+        RT_TRACE(C, P, false);     \
+    }
     if (counters) {
         if (packed) { RT_TRACE_W(true, true); } else { RT_TRACE_W(true, false); }
     } else {
@@ -645,6 +670,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     }
 #undef RT_TRACE_W
 #undef RT_TRACE
+#undef RT_TRACE_NT
     return hipGetLastError();
 }
 

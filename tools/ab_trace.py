@@ -21,9 +21,13 @@ sel = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "2"]
 variants = []
 for v in sel:
     if v == "0":
-        variants.append(("wide (default)", {"trace.variant": 0}))
+        variants.append(("wide (default)", {"trace.variant": 0, "trace.wg": 256}))
+    elif v == "0s":
+        variants.append(("wide, 64-thread blocks", {"trace.variant": 0, "trace.wg": 64}))
+    elif v == "2s":
+        variants.append(("binary, 64-thread blocks", {"trace.variant": 2, "trace.wg": 64}))
     elif v == "2":
-        variants.append(("binary (deferred leaf test)", {"trace.variant": 2}))
+        variants.append(("binary (deferred leaf test)", {"trace.variant": 2, "trace.wg": 256}))
     elif v.startswith("pool"):  # pool[-bB]: wide with per-lane refill, B blocks (0 = resident capacity)
         b = int(v.split("-b")[1]) if "-b" in v else 0
         variants.append((v, {"trace.variant": 1, "trace.blocks": b}))

@@ -23,17 +23,13 @@ def rows(pattern):
 
 
 def short(name):
-    n = name.split("(")[0]
-    for k in ("k_trace_pool", "k_trace", "k_onesweep", "k_refit_local", "k_refit_cross", "k_karras", "k_morton", "k_bounds",
-              "k_unpack", "k_sparse_level", "k_digit_hist"):
-        if k in n:
-            import re
-            m = re.search(r"k_onesweep<(\d+)>|k_onesweepILi(\d+)E|k_traceILb(\d)ELb(\d)ELb(\d)E|k_trace_poolILb(\d)ELb(\d)E|k_refit_crossILb(\d)E", name)
-            if m:
-                g = [x for x in m.groups() if x is not None]
-                return k + "<" + ",".join(g) + ">"
-            return k
-    return n[:60]
+    """Kernel name without the argument list: 'k_trace<false, false, true, 256>'."""
+    import re
+    m = re.search(r"(k_\w+<[^>]*>)", name)
+    if m:
+        return m.group(1)
+    m = re.search(r"(k_\w+)", name.split("(")[0])
+    return m.group(1) if m else name.split("(")[0][:60]
 
 
 def main():
@@ -64,7 +60,7 @@ def main():
         lines.append(f"| {k} | {f:.1f} | {w:.1f} | {2*f*1024:.3e} | {w*1024:.3e} |")
     os.makedirs("profiles", exist_ok=True)
     open(f"profiles/rocprof_{tag}.md", "w").write("\n".join(lines) + "\n")
-    tk = "k_trace<0,0,1>"  # the timed launch: no counters, full image, wide traversal
+    tk = "k_trace<false, false, true, 256>"  # the timed launch: no counters, full image, wide traversal
     if tk in pm["FETCH_SIZE"] and tk in pm["WRITE_SIZE"]:
         fetch = pm["FETCH_SIZE"][tk] * 1024
         write = pm["WRITE_SIZE"][tk] * 1024
