@@ -32,7 +32,8 @@ _STATUS_NAMES = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EIO", -4:
 
 # every symbol the header declares (checked by tests/test_abi.py)
 EXPORTED = [
-    "rt_scene_from_soup", "rt_scene_load_obj", "rt_scene_generate_soup", "rt_scene_num_tris",
+    "rt_scene_from_soup", "rt_scene_load_obj", "rt_scene_generate_soup", "rt_scene_load_soup",
+    "rt_scene_save_soup", "rt_bvh_save", "rt_bvh_load", "rt_scene_num_tris",
     "rt_scene_get_tris", "rt_scene_set_device", "rt_scene_free", "rt_camera_look_at", "rt_bvh_build",
     "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_render", "rt_render_counters", "rt_render_work", "rt_render_device",
     "rt_render_tiles_counters", "rt_tiles_for_rank",
@@ -83,6 +84,10 @@ def lib() -> C.CDLL:
     sig = {
         "rt_scene_from_soup": [P, u32, PP],
         "rt_scene_load_obj": [C.c_char_p, PP],
+        "rt_scene_load_soup": [C.c_char_p, PP],
+        "rt_scene_save_soup": [P, C.c_char_p],
+        "rt_bvh_save": [P, C.c_char_p],
+        "rt_bvh_load": [P, C.c_char_p],
         "rt_scene_generate_soup": [u32, u64, PP],
         "rt_scene_num_tris": [P, C.POINTER(u32)],
         "rt_scene_get_tris": [P, P],

@@ -18,6 +18,8 @@
 
 namespace rtio {
 bool load_obj(const char* path, std::vector<float>& tris, std::string& err);
+bool load_soup(const char* path, std::vector<float>& tris, std::string& err);
+bool save_soup(const char* path, const float* tris, uint64_t n, std::string& err);
 void soup_generate(uint32_t n, uint64_t seed, float* tris);
 }  // namespace rtio
 
@@ -174,6 +176,21 @@ rt_status rt_scene_load_obj(const char* path, rt_scene** out) {
     return rt_scene_from_soup(t.data(), (uint32_t)(t.size() / 9), out);
 }
 
+rt_status rt_scene_load_soup(const char* path, rt_scene** out) {
+    if (!path || !out) return fail(RT_EINVAL, "null argument");
+    std::vector<float> t;
+    std::string err;
+    if (!rtio::load_soup(path, t, err)) return fail(RT_EIO, err);
+    return rt_scene_from_soup(t.data(), (uint32_t)(t.size() / 9), out);
+}
+
+rt_status rt_scene_save_soup(const rt_scene* s, const char* path) {
+    if (!s || !path) return fail(RT_EINVAL, "null argument");
+    std::string err;
+    if (!rtio::save_soup(path, s->tris.data(), s->n, err)) return fail(RT_EIO, err);
+    return RT_OK;
+}
+
 rt_status rt_scene_generate_soup(uint32_t n, uint64_t seed, rt_scene** out) {
     if (!out) return fail(RT_EINVAL, "null argument");
     if (n > (1u << 30)) return fail(RT_EINVAL, "n exceeds 2^30 triangles");
@@ -327,6 +344,118 @@ rt_status rt_bvh_read_wide(const rt_scene* s, void* records) {
     HIPR(hipSetDevice(s->device));
     HIPR(hipStreamSynchronize(s->stream));
     if (s->n >= 2) HIPR(hipMemcpy(records, s->bufs.wnodes, (size_t)(s->n - 1) * 64, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+// ------------------------------------------------------------------ BVH cache
+// RTBVH1: "RTBVH1\0\0", u32 version, u32 n, u64 FNV-1a hash of the n*36
+// triangle bytes, u64 layout tag, then the device buffers the trace and
+// rt_bvh_read use, in order: BuildParams (64 B), sorted keys and vals (n x 4),
+// nodes ((2n-1) x 32), parent ((2n-1) x 4), tri_s (n x 48), wide records
+// ((n-1) x 64).  The tag changes whenever one of those layouts does.
+extern "C++" {
+namespace {
+const char kBvhMagic[8] = {'R', 'T', 'B', 'V', 'H', '1', 0, 0};
+constexpr uint32_t kBvhVersion = 1;
+constexpr uint64_t kBvhLayout = 0x7274616d64000001ull;  // "rtamd" + layout revision 1
+
+uint64_t fnv1a(const void* p, size_t bytes) {
+    const unsigned char* b = static_cast<const unsigned char*>(p);
+    uint64_t h = 0xcbf29ce484222325ull;
+    for (size_t i = 0; i < bytes; ++i) {
+        h ^= b[i];
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+
+struct BvhSection {
+    void* dev;
+    size_t bytes;
+};
+
+std::vector<BvhSection> bvh_sections(const rt_scene* s) {
+    const size_t n = s->n, tot = n ? 2 * n - 1 : 0;
+    static_assert(sizeof(rt::BuildParams) == 64, "RTBVH1 stores a 64-B BuildParams");
+    return {{s->bufs.params, sizeof(rt::BuildParams)},
+            {s->bufs.keys[0], n * 4},
+            {s->bufs.vals[0], n * 4},
+            {s->bufs.nodes, tot * 32},
+            {s->bufs.parent, tot * 4},
+            {s->bufs.tri_s, n * 48},
+            {s->bufs.wnodes, n >= 2 ? (n - 1) * 64 : 0}};
+}
+}  // namespace
+}  // extern "C++"
+
+rt_status rt_bvh_save(const rt_scene* s, const char* path) {
+    if (!s || !path) return fail(RT_EINVAL, "null argument");
+    if (!s->built) return fail(RT_EINVAL, "scene not built");
+    HIPR(hipSetDevice(s->device));
+    HIPR(hipStreamSynchronize(s->stream));
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(RT_EIO, std::string("cannot create ") + path);
+    const uint32_t hv[2] = {kBvhVersion, s->n};
+    const uint64_t hh[2] = {fnv1a(s->tris.data(), s->tris.size() * sizeof(float)), kBvhLayout};
+    bool ok = std::fwrite(kBvhMagic, 1, 8, f) == 8 && std::fwrite(hv, 4, 2, f) == 2 && std::fwrite(hh, 8, 2, f) == 2;
+    std::vector<unsigned char> host;
+    for (const BvhSection& sec : bvh_sections(s)) {
+        if (!ok || !sec.bytes) continue;
+        host.resize(sec.bytes);
+        if (hipMemcpy(host.data(), sec.dev, sec.bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+            std::fclose(f);
+            return fail(RT_EDEVICE, "device read of the BVH failed");
+        }
+        ok = std::fwrite(host.data(), 1, sec.bytes, f) == sec.bytes;
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RT_OK : fail(RT_EIO, std::string("write error on ") + path);
+}
+
+rt_status rt_bvh_load(rt_scene* s, const char* path) {
+    if (!s || !path) return fail(RT_EINVAL, "null argument");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return fail(RT_EIO, std::string("cannot open ") + path);
+    char magic[8];
+    uint32_t hv[2] = {0, 0};
+    uint64_t hh[2] = {0, 0};
+    const bool hdr = std::fread(magic, 1, 8, f) == 8 && std::fread(hv, 4, 2, f) == 2 && std::fread(hh, 8, 2, f) == 2;
+    if (!hdr || std::memcmp(magic, kBvhMagic, 8) != 0) {
+        std::fclose(f);
+        return fail(RT_EIO, std::string(path) + ": not an RTBVH1 file");
+    }
+    if (hv[0] != kBvhVersion || hh[1] != kBvhLayout) {
+        std::fclose(f);
+        return fail(RT_EIO, std::string(path) + ": BVH cache from another library layout");
+    }
+    if (hv[1] != s->n || hh[0] != fnv1a(s->tris.data(), s->tris.size() * sizeof(float))) {
+        std::fclose(f);
+        return fail(RT_EINVAL, std::string(path) + ": BVH cache was built for different triangles");
+    }
+    rt_status st = upload(s);
+    if (st) {
+        std::fclose(f);
+        return st;
+    }
+    std::vector<unsigned char> host;
+    for (const BvhSection& sec : bvh_sections(s)) {
+        if (!sec.bytes) continue;
+        host.resize(sec.bytes);
+        if (std::fread(host.data(), 1, sec.bytes, f) != sec.bytes) {
+            std::fclose(f);
+            s->built = false;
+            return fail(RT_EIO, std::string(path) + ": truncated BVH cache");
+        }
+        HIPR(hipMemcpy(sec.dev, host.data(), sec.bytes, hipMemcpyHostToDevice));
+    }
+    const bool extra = std::fgetc(f) != EOF;
+    std::fclose(f);
+    if (extra) {
+        s->built = false;
+        return fail(RT_EIO, std::string(path) + ": trailing bytes in BVH cache");
+    }
+    s->times = rt_build_times{};
+    s->built = true;
     return RT_OK;
 }
 

@@ -70,6 +70,16 @@ class Scene:
         return cls(h)
 
     @classmethod
+    def load_soup(cls, path: str) -> "Scene":
+        """RTSOUP1 binary triangle soup."""
+        h = C.c_void_p()
+        call("rt_scene_load_soup", path.encode(), C.byref(h))
+        return cls(h)
+
+    def save_soup(self, path: str) -> None:
+        call("rt_scene_save_soup", self._h, path.encode())
+
+    @classmethod
     def generate_soup(cls, n: int, seed: int = 1) -> "Scene":
         h = C.c_void_p()
         call("rt_scene_generate_soup", int(n), int(seed), C.byref(h))
@@ -112,6 +122,14 @@ class Scene:
         ms = C.c_double()
         call("rt_bvh_build", self._h, C.byref(ms))
         return ms.value
+
+    def save_bvh(self, path: str) -> None:
+        """RTBVH1 cache of the built BVH."""
+        call("rt_bvh_save", self._h, path.encode())
+
+    def load_bvh(self, path: str) -> None:
+        """Restore a cached BVH built for these same triangles (instead of build())."""
+        call("rt_bvh_load", self._h, path.encode())
 
     def build_times(self) -> BuildTimes:
         t = rt_build_times()

@@ -66,6 +66,10 @@ typedef struct {
 rt_status rt_scene_from_soup(const float* tris, uint32_t n, rt_scene** out); /* copies n*9 floats */
 rt_status rt_scene_load_obj(const char* path, rt_scene** out);
 rt_status rt_scene_generate_soup(uint32_t n, uint64_t seed, rt_scene** out); /* SURVEY.md §9.9 */
+/* RTSOUP1 binary soup: "RTSOUP1\0", u32 version 1,
+ * u32 0, u64 n, then n x 9 little-endian float32 -- the rt_scene_from_soup layout. */
+rt_status rt_scene_load_soup(const char* path, rt_scene** out);
+rt_status rt_scene_save_soup(const rt_scene* s, const char* path);
 rt_status rt_scene_num_tris(const rt_scene* s, uint32_t* n_out);
 rt_status rt_scene_get_tris(const rt_scene* s, float* tris_out); /* n*9 floats */
 rt_status rt_scene_set_device(rt_scene* s, int device);          /* default 0; before first build */
@@ -85,6 +89,13 @@ rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out);
  * sorted keys/vals[n], parent[2n-1], bounds[9] = lo[3], hi[3], inv[3]. */
 rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* sorted_keys,
                       uint32_t* sorted_vals, uint32_t* parent, float* bounds9);
+/* BVH cache: rt_bvh_save writes a built scene's
+ * device BVH (RTBVH1: header with a hash of the triangles, then the buffers
+ * the trace reads); rt_bvh_load restores it into a scene with the SAME
+ * triangles instead of rt_bvh_build (RT_EINVAL for other triangles, RT_EIO
+ * for a bad file). */
+rt_status rt_bvh_save(const rt_scene* s, const char* path);
+rt_status rt_bvh_load(rt_scene* s, const char* path);
 /* Read back the K7w wide trace records: (n-1) x 64 B, one per binary internal
  * node (layout: gpu_raytracer_amd/csrc/rt_device.h); nothing for n < 2. */
 rt_status rt_bvh_read_wide(const rt_scene* s, void* records);

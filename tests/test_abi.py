@@ -125,3 +125,64 @@ def test_no_cpu_fallback(rt):
         with pytest.raises(rt.RtError) as e:
             f()
         assert e.value.status == -4
+
+
+def test_obj_loader_robustness(rt, tmp_path):
+    """CRLF, continuation lines, comments after data, long lines, relative
+    indices, polygon fans and every ignored statement."""
+    p = tmp_path / "messy.obj"
+    n = 400  # one polygon with n corners on a single very long line
+    ang = np.linspace(0.0, 2.0 * np.pi, n, endpoint=False)
+    verts = "".join(f"v {np.cos(a):.6f} {np.sin(a):.6f} 0.5 1.0\r\n" for a in ang)
+    face = "f " + " ".join(f"{i + 1}/{i + 1}/1" for i in range(n)) + "   # a comment\r\n"
+    text = ("# header\r\nmtllib scene.mtl\r\ng grp\r\n" + verts + "vt 0 0\r\nvn 0 0 1\r\nusemtl red\r\n" + face +
+            "v 2 0 0\r\nv 2 1 \\\r\n 0\r\nv 3 0 0\r\nf -3//1 -2//1 -1//1\r\nl 1 2\r\np 1\r\ns 1\r\n")
+    p.write_bytes(text.encode())
+    with rt.Scene.load_obj(str(p)) as s:
+        t = s.tris()
+    assert t.shape == (n - 2 + 1, 9)
+    ring = np.array([[float(f"{np.cos(a):.6f}"), float(f"{np.sin(a):.6f}"), 0.5] for a in ang], np.float32)
+    for k in range(1, n - 1):  # fan (0, k, k+1)
+        assert np.array_equal(t[k - 1], np.concatenate([ring[0], ring[k], ring[k + 1]]))
+    assert np.array_equal(t[-1], np.array([2, 0, 0, 2, 1, 0, 3, 0, 0], np.float32))
+    for body, what in [("v 0 0 0\nv 1 0 0\nf 1 2\n", "two corners"), ("v 0 0\n", "short vertex"),
+                       ("v 0 0 0\nf 1 1 x\n", "bad index"), ("v 0 0 0\nf 0 1 1\n", "index 0")]:
+        bad = tmp_path / "bad.obj"
+        bad.write_text(body)
+        with pytest.raises(rt.RtError) as e:
+            rt.Scene.load_obj(str(bad))
+        assert e.value.status == -3, what
+
+
+def test_rtsoup1_roundtrip(rt, tmp_path):
+    t = np.random.default_rng(1).standard_normal((1000, 9)).astype(np.float32)
+    t[3, 4] = np.float32(-0.0)
+    p = tmp_path / "s.rtsoup"
+    with rt.Scene.from_soup(t) as s:
+        s.save_soup(str(p))
+    raw = p.read_bytes()
+    assert raw[:8] == b"RTSOUP1\0" and len(raw) == 24 + 1000 * 36
+    assert np.frombuffer(raw[16:24], np.uint64)[0] == 1000
+    with rt.Scene.load_soup(str(p)) as s:
+        assert np.array_equal(s.tris().view(np.uint32), t.view(np.uint32))
+    empty = tmp_path / "e.rtsoup"
+    with rt.Scene.from_soup(np.zeros((0, 9), np.float32)) as s:
+        s.save_soup(str(empty))
+    with rt.Scene.load_soup(str(empty)) as s:
+        assert s.num_tris == 0
+    for corrupt in (raw[:-4], b"RTSOUP2\0" + raw[8:], raw[:8] + b"\x02" + raw[9:], raw[:20]):
+        q = tmp_path / "bad.rtsoup"
+        q.write_bytes(corrupt)
+        with pytest.raises(rt.RtError) as e:
+            rt.Scene.load_soup(str(q))
+        assert e.value.status == -3
+
+
+def test_bvh_cache_rejects_without_device_work(rt, tmp_path):
+    """A cache that is not RTBVH1 is refused before any device work."""
+    q = tmp_path / "x.rtbvh"
+    q.write_bytes(b"not a cache at all, definitely not")
+    with rt.Scene.from_soup(np.zeros((3, 9), np.float32)) as s:
+        with pytest.raises(rt.RtError) as e:
+            s.load_bvh(str(q))
+        assert e.value.status == -3
