@@ -91,6 +91,29 @@ def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters):
     }
 
 
+def secondary_rays(R, S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev, primary_ms):
+    """SURVEY.md §8(f) row 3, shadow mode: the same frame with one
+    any-hit shadow ray per primary hit.  Untimed by the step contract; its own
+    warm-up and timed launches (hipEvents), median reported."""
+    light = S.LIGHTS[cfg.scene]
+    ms = []
+    for i in range(args.warmup + max(args.steps, 3)):
+        t = scene.render_shadow_device(cam, w, h, spp, light, S.AMBIENT, d_rgba=img.data_ptr(),
+                                       d_hits=hits.data_ptr(), timed=True)
+        if i >= args.warmup:
+            ms.append(t)
+    torch.cuda.synchronize(dev)
+    prim = hits.view(-1, 4)[:, 3].view(torch.int32)
+    shadow_rays = int((prim != -1).sum().item())
+    rays = w * h * spp
+    med = float(np.median(ms))
+    return {"mode": "shadow rays: 1 any-hit ray per primary hit toward a point light (DESIGN.md)",
+            "light": list(light), "ambient": S.AMBIENT, "ms": round(med, 4),
+            "primary_rays": rays, "shadow_rays": shadow_rays,
+            "mrays_per_s": round((rays + shadow_rays) / (med * 1e-3) / 1e6, 2),
+            "shadow_mrays_per_s": round(shadow_rays / (max(med - primary_ms, 1e-6) * 1e-3) / 1e6, 2)}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -252,6 +275,9 @@ def main():
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM},
             "cpu_baseline": None,
         }
+        if world == 1:
+            out["secondary"] = secondary_rays(R, S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev,
+                                              float(np.median(per[:, 1])))
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
             out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt)

@@ -91,6 +91,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
                         uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
                         void* hits, void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
                         hipStream_t s);
+// Shadow mode: primary hits into `hits`, Lambert + shadow-ray
+// shaded image into `rgba`; tris = the scene's AoS triangles (normals).
+hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+                               uint32_t n, const CamF& cam, uint32_t w, uint32_t h, uint32_t spp,
+                               const float light[3], float ambient, void* hits, void* rgba,
+                               unsigned long long* counters, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
                          void* img, hipStream_t s);
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);

@@ -73,7 +73,7 @@ __device__ __forceinline__ bool intersect_tri(const float* o, const float* d, co
 // tb/hu/hv/hp: exact whenever every leaf before `start` in preorder has been
 // tested with §9.7's outcome (the wide traversal's overflow hand-off); a
 // start below a culled ancestor only adds box tests that miss.
-template <bool COUNT>
+template <bool COUNT, bool ANY = false>
 __device__ __forceinline__ void trace_ray_from(const char* __restrict__ nodes, const float4* __restrict__ tri_s,
                                                uint32_t n, const float* o, const float* d, uint32_t start, float& tb,
                                                float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
@@ -97,7 +97,10 @@ __device__ __forceinline__ void trace_ray_from(const char* __restrict__ nodes, c
             const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
             const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
             float t, u, v;
-            if (intersect_tri(o, d, tv, tb, t, u, v)) { tb = t; hu = u; hv = v; hp = pprim; }
+            if (intersect_tri(o, d, tv, tb, t, u, v)) {
+                tb = t; hu = u; hv = v; hp = pprim;
+                if (ANY) return;  // any-hit (shadow ray): the first hit ends the search
+            }
             pend = RT_SENT;
         }
         if (!node) break;
@@ -221,7 +224,7 @@ __device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const ui
 // Returns 0 = more steps, 1 = done, 2 = finish with
 // trace_ray_from(bin_of(R.cur)) (stack overflow at record R.cur, or the step
 // guard of a malformed tree).
-template <bool COUNT, int NT>
+template <bool COUNT, int NT, bool ANY = false>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
                                          uint32_t& cn, uint32_t& ct) {
@@ -249,7 +252,10 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
         tri_bounds(tv, lo, hi);
         if (slab_hit(lo, hi, o, R.invd, R.tb, tn)) {
             float t, u, v;
-            if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) { R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(T2.y); }
+            if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) {
+                R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(T2.y);
+                if (ANY) { R.pend = RT_SENT; return 1; }  // any-hit: done
+            }
         }
         R.pend = RT_SENT;
     }
@@ -300,15 +306,68 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
 
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
 
-template <bool COUNT, bool PACKED, bool WIDE, int NT>
+// Shadow mode [SPEC, DESIGN.md "Shadow mode"]: the lighting factor f of a
+// primary hit -- one any-hit shadow ray from the hit (offset 1e-4 along the
+// viewer-facing geometric normal) toward the point light over t in (0, 1),
+// Lambert term, ambient floor.  Operation order as orc_render_shadow.
+struct Light { float p[3]; float ambient; };
+
+template <bool COUNT, int NT>
+__device__ __forceinline__ float shadow_factor(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                               uint32_t wcap, const float4* __restrict__ tri_s,
+                                               const float* __restrict__ tris, uint32_t n, const float* o,
+                                               const float* d, float t, uint32_t prim, const Light& lt,
+                                               uint32_t* sref, uint16_t* stn, uint32_t& cn, uint32_t& ct) {
+    const float* tri = tris + (uint64_t)prim * 9;
+    float P[3], e1[3], e2[3], nrm[3], N[3], S[3], D[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        P[a] = o[a] + t * d[a];
+        e1[a] = tri[3 + a] - tri[a];
+        e2[a] = tri[6 + a] - tri[a];
+    }
+    cross3(e1, e2, nrm);
+    const float nl = sqrtf(dot3(nrm, nrm));
+#pragma unroll
+    for (int a = 0; a < 3; ++a) N[a] = nl > 0.0f ? nrm[a] / nl : 0.0f;
+    if (dot3(N, d) > 0.0f) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) N[a] = -N[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        S[a] = P[a] + N[a] * 1e-4f;
+        D[a] = lt.p[a] - S[a];
+    }
+    // any-hit over (0, 1): wide traversal when it applies, else binary
+    WRay R;
+    wray_init(D, R);
+    R.tb = 1.0f;
+    int st = (R.fin && wnodes && n >= 2) ? 0 : 2;
+    while (st == 0) st = wide_step<COUNT, NT, true>(R, wnodes, tri_s, S, wcap, 4 * n + 16, sref, stn, cn, ct);
+    if (st == 2) {
+        const bool restart = !(R.fin && wnodes && n >= 2);
+        if (restart) { R.cur = n ? 0u : RT_SENT; R.tb = 1.0f; R.hp = RT_SENT; }
+        trace_ray_from<COUNT, true>(nodes, tri_s, n, S, D,
+                                    R.cur == RT_SENT ? RT_SENT : (restart ? R.cur : bin_of(R.cur, n - 1)), R.tb, R.hu,
+                                    R.hv, R.hp, cn, ct);
+    }
+    const float dl = sqrtf(dot3(D, D));
+    const float cosl = dl > 0.0f ? dot3(N, D) / dl : 0.0f;
+    const float lit = R.hp != RT_SENT ? 0.0f : fmaxf(cosl, 0.0f);
+    return lt.ambient + (1.0f - lt.ambient) * lit;
+}
+
+template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false>
 __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
-                                               unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t s_ref[WIDE ? (kWideStack + 1) * NT : 1];
-    __shared__ uint16_t s_tn[WIDE ? (kWideStack + 1) * NT : 1];
+                                               unsigned long long* __restrict__ counters,
+                                               const float* __restrict__ tris = nullptr, Light lt = Light{}) {
+    __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
+    __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     // tile slot from the block id: consecutive tiles go to different XCDs
     // under the round-robin dispatch, which balances the image's cheap and
     // costly bands over the 8 XCDs (an XCD-banded remap measured 1.2x
@@ -364,7 +423,20 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                 const uint64_t hi = PACKED ? ((uint64_t)slot * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
                 hits[hi] = make_float4(tb, hu, hv, __uint_as_float(hp));
             }
-            if (hp != RT_SENT) {
+            if (SHADOW) {
+                float f = 0.0f;
+                if (hp != RT_SENT)
+                    f = shadow_factor<COUNT, NT>(reinterpret_cast<const char*>(nodes), WIDE ? wnodes : nullptr, wcap,
+                                                 tri_s, tris, n, cam.eye, d, tb, hp, lt, s_ref + threadIdx.x,
+                                                 s_tn + threadIdx.x, cn, ct);
+                if (hp != RT_SENT) {
+                    r = r + hu * f;
+                    g = g + hv * f;
+                    b = b + ((1.0f - hu) - hv) * f;
+                } else {
+                    r = r + 0.0f; g = g + 0.0f; b = b + 0.0f;
+                }
+            } else if (hp != RT_SENT) {
                 r = r + hu;
                 g = g + hv;
                 b = b + ((1.0f - hu) - hv);
@@ -671,6 +743,35 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
 #undef RT_TRACE_W
 #undef RT_TRACE
 #undef RT_TRACE_NT
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+                               uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
+                               float ambient, void* hits, void* rgba, unsigned long long* counters, hipStream_t s) {
+    const uint32_t nb = tiles_for_rank(w, h, 0, 1);
+    if (!nb) return hipSuccess;
+    Cam cam;
+    for (int i = 0; i < 3; ++i) {
+        cam.eye[i] = c.eye[i]; cam.w00[i] = c.w00[i]; cam.du[i] = c.du[i]; cam.dv[i] = c.dv[i];
+    }
+    Light lt;
+    for (int i = 0; i < 3; ++i) lt.p[i] = light[i];
+    lt.ambient = ambient;
+    const uint32_t tilesX = (w + 15) / 16;
+    float4* H = reinterpret_cast<float4*>(hits);
+    uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
+    const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2;
+    const uint32_t cap = g_trace_config.stack_cap;
+#define RT_SHADOW(C, WI)                                                                                        \
+    hipLaunchKernelGGL((k_trace<C, false, WI, 256, true>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, tri_s, \
+                       n, cam, w, h, spp, 0u, 1u, tilesX, H, R, counters, tris, lt)
+    if (counters) {
+        if (wide) RT_SHADOW(true, true); else RT_SHADOW(true, false);
+    } else {
+        if (wide) RT_SHADOW(false, true); else RT_SHADOW(false, false);
+    }
+#undef RT_SHADOW
     return hipGetLastError();
 }
 

@@ -129,6 +129,12 @@ CONFIGS = {
 
 VIEWS = {"cornell": CORNELL_VIEW, "soup": SOUP_VIEW, "bunny": BUNNY_VIEW, "sponza": SPONZA_VIEW}
 
+# Point lights of the shadow mode (DESIGN.md "Shadow mode"), per preset, and
+# its ambient floor.
+LIGHTS = {"cornell": (278.0, 540.0, 279.5), "soup": (2.0, 3.0, -2.0), "bunny": (2.0, 3.0, -3.0),
+          "sponza": (128.0, 120.0, 150.0)}
+AMBIENT = 0.2
+
 
 def tris_for(scene: str, n: int = 0, seed: int = 1) -> np.ndarray | None:
     """Host triangles for a preset (None for 'soup': generated inside the library)."""

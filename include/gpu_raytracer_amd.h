@@ -109,6 +109,20 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
  * (the oracle's counters): [0] nodes fetched, [1] tris tested */
 rt_status rt_render_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,
                              uint32_t spp, uint64_t counters_out[2]);
+/* Shadow mode (contract in DESIGN.md "Shadow mode"):
+ * the §9.7 primary render, then one any-hit shadow ray per primary hit
+ * toward the point light light[3]; the image is (u, v, 1-u-v) scaled by
+ * ambient + (1 - ambient) * Lambert * visibility.  hits_out = primary hits. */
+rt_status rt_render_shadow(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
+                           uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits_out, uint8_t* rgba_out,
+                           double* ms_out);
+rt_status rt_render_shadow_device(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
+                                  uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
+                                  void* stream, double* ms_out);
+/* work of the shadow-mode kernel (primary + shadow rays): [0] node records
+ * fetched, [1] triangle records loaded */
+rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
+                                uint32_t w, uint32_t h, uint32_t spp, uint64_t counters_out[2]);
 /* work of the configured (default: wide) trace kernel itself: [0] node
  * records fetched (64 B wide / 32 B binary), [1] triangle records loaded */
 rt_status rt_render_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,

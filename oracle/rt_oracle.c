@@ -331,11 +331,13 @@ int orc_intersect_tri(const float o[3], const float d[3], const float* tri, floa
     return 1;
 }
 
-static void trace_ray(const orc_node* nodes, uint32_t n, const float* tris, const float o[3],
-                      const float d[3], orc_hit* hit, uint64_t* cn, uint64_t* ct) {
+/* tmax: INFINITY for the §9.7 closest hit; 1.0f with any_hit for the
+ * shadow ray of the shadow mode (the first hit with 0 < t < 1 ends it). */
+static void trace_ray_t(const orc_node* nodes, uint32_t n, const float* tris, const float o[3],
+                        const float d[3], float tmax, int any_hit, orc_hit* hit, uint64_t* cn, uint64_t* ct) {
     float invd[3];
     for (int a = 0; a < 3; ++a) invd[a] = 1.0f / d[a];
-    float tb = INFINITY, hu = 0.0f, hv = 0.0f;
+    float tb = tmax, hu = 0.0f, hv = 0.0f;
     uint32_t hp = ORC_SENTINEL;
     uint32_t idx = n ? 0u : ORC_SENTINEL;
     const uint32_t L0 = n ? n - 1 : 0;
@@ -356,6 +358,7 @@ static void trace_ray(const orc_node* nodes, uint32_t n, const float* tris, cons
             float t, u, v;
             if (orc_intersect_tri(o, d, tris + (size_t)nd->a * 9, tb, &t, &u, &v)) {
                 tb = t; hu = u; hv = v; hp = nd->a;
+                if (any_hit) break;
             }
             idx = nd->esc;
         } else {
@@ -365,6 +368,11 @@ static void trace_ray(const orc_node* nodes, uint32_t n, const float* tris, cons
     hit->t = tb; hit->u = hu; hit->v = hv; hit->prim = hp;
     *cn += nn;
     *ct += nt;
+}
+
+static void trace_ray(const orc_node* nodes, uint32_t n, const float* tris, const float o[3],
+                      const float d[3], orc_hit* hit, uint64_t* cn, uint64_t* ct) {
+    trace_ray_t(nodes, n, tris, o, d, INFINITY, 0, hit, cn, ct);
 }
 
 typedef struct {
@@ -441,4 +449,74 @@ void orc_shade(const orc_hit* hits, uint32_t w, uint32_t h, uint32_t spp, uint8_
         rgba[p * 4 + 2] = q8(b * sc);
         rgba[p * 4 + 3] = 255;
     }
+}
+
+/* ------------------------------------------------------ shadow mode [SPEC] */
+/* DESIGN.md "Shadow mode": one shadow ray per primary hit toward the point
+ * light L, any-hit over (0, 1) of S -> L, Lambert term, ambient floor.
+ * Writes the primary hits and the shaded RGBA8 image. */
+static void shade_sample(const orc_node* nodes, uint32_t n, const float* tris, const float o[3],
+                         const float d[3], const orc_hit* h, const float L[3], float ambient,
+                         float rgb[3], uint64_t* cn, uint64_t* ct) {
+    if (h->prim == ORC_SENTINEL) { rgb[0] = rgb[1] = rgb[2] = 0.0f; return; }
+    const float* tri = tris + (size_t)h->prim * 9;
+    float P[3], e1[3], e2[3], nrm[3], N[3], S[3], D[3];
+    for (int a = 0; a < 3; ++a) {
+        P[a] = o[a] + h->t * d[a];
+        e1[a] = tri[3 + a] - tri[a];
+        e2[a] = tri[6 + a] - tri[a];
+    }
+    cross3(e1, e2, nrm);
+    const float nl = sqrtf(dot3(nrm, nrm));
+    for (int a = 0; a < 3; ++a) N[a] = nl > 0.0f ? nrm[a] / nl : 0.0f;
+    if (dot3(N, d) > 0.0f)
+        for (int a = 0; a < 3; ++a) N[a] = -N[a];
+    for (int a = 0; a < 3; ++a) {
+        S[a] = P[a] + N[a] * 1e-4f;
+        D[a] = L[a] - S[a];
+    }
+    orc_hit sh;
+    trace_ray_t(nodes, n, tris, S, D, 1.0f, 1, &sh, cn, ct);
+    const float dl = sqrtf(dot3(D, D));
+    const float cosl = dl > 0.0f ? dot3(N, D) / dl : 0.0f;
+    const float lit = sh.prim != ORC_SENTINEL ? 0.0f : FMAX(cosl, 0.0f);
+    const float f = ambient + (1.0f - ambient) * lit;
+    rgb[0] = h->u * f;
+    rgb[1] = h->v * f;
+    rgb[2] = ((1.0f - h->u) - h->v) * f;
+}
+
+void orc_render_shadow(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* cam,
+                       uint32_t w, uint32_t h, uint32_t spp, const float light[3], float ambient,
+                       orc_hit* hits, uint8_t* rgba, uint64_t counters[2], int nthreads) {
+    uint64_t c2[2] = {0, 0};
+    orc_trace(nodes, n, tris, cam, w, h, spp, 0, 1, hits, c2, nthreads);
+    uint64_t cn = 0, ct = 0;
+    const float sc = 1.0f / (float)spp;
+    for (uint64_t y = 0; y < h; ++y)
+        for (uint32_t x = 0; x < w; ++x) {
+            float r = 0.0f, g = 0.0f, b = 0.0f;
+            for (uint32_t s = 0; s < spp; ++s) {
+                const uint32_t sidx = (uint32_t)((y * w + x) * spp + s);
+                float jx = 0.5f, jy = 0.5f;
+                if (s > 0) {
+                    const uint32_t hh = orc_pcg_hash(sidx);
+                    jx = (float)(hh >> 8) * 0x1p-24f;
+                    jy = (float)(orc_pcg_hash(hh) >> 8) * 0x1p-24f;
+                }
+                const float px = (float)x + jx, py = (float)y + jy;
+                float d[3], rgb[3];
+                for (int a = 0; a < 3; ++a) d[a] = (cam->w00[a] + px * cam->du[a]) + py * cam->dv[a];
+                shade_sample(nodes, n, tris, cam->eye, d, &hits[sidx], light, ambient, rgb, &cn, &ct);
+                r = r + rgb[0];
+                g = g + rgb[1];
+                b = b + rgb[2];
+            }
+            const uint64_t p = y * w + x;
+            rgba[p * 4 + 0] = q8(r * sc);
+            rgba[p * 4 + 1] = q8(g * sc);
+            rgba[p * 4 + 2] = q8(b * sc);
+            rgba[p * 4 + 3] = 255;
+        }
+    if (counters) { counters[0] = cn; counters[1] = ct; }
 }

@@ -99,6 +99,14 @@ void orc_trace(const orc_node* nodes, uint32_t n, const float* tris, const orc_c
 /* §9.7 shading: rgba[(y*w+x)*4] from hits of that pixel's spp samples. */
 void orc_shade(const orc_hit* hits, uint32_t w, uint32_t h, uint32_t spp, uint8_t* rgba);
 
+/* Shadow mode [SPEC, DESIGN.md "Shadow mode"; SURVEY.md §8(f) row 3]: the
+ * §9.7 primary hits, then one any-hit shadow ray per hit toward the point
+ * light; rgba = Lambert-lit (u, v, 1-u-v) with an ambient floor.  counters
+ * (nullable): shadow-ray nodes fetched / tris tested. */
+void orc_render_shadow(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* cam,
+                       uint32_t w, uint32_t h, uint32_t spp, const float light[3], float ambient,
+                       orc_hit* hits, uint8_t* rgba, uint64_t counters[2], int nthreads);
+
 #ifdef __cplusplus
 }
 #endif
