@@ -538,8 +538,10 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
     RT_STAMP(2);
     // one aggregated reservation per block on one of kCrossShards counters
     // (a single global counter hit by every wave serialises at ~90 ops/us)
+    // (issued here, consumed after the climb: the atomic's latency overlaps it)
+    uint32_t cbase = 0;
     if (tid == 0 && s_ncross)
-        s_cbase = (blockIdx.x % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[blockIdx.x % kCrossShards], s_ncross);
+        cbase = (blockIdx.x % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[blockIdx.x % kCrossShards], s_ncross);
     // ---- bottom-up climb inside the block, LDS only.  LDS instructions of a
     // wave execute in order, so its s_box write lands before its own arrival
     // add; the second arriver reads the sibling's box after its add returns.
@@ -568,6 +570,7 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
             node = p;
         }
     }
+    if (tid == 0) s_cbase = cbase;
     __syncthreads();
     RT_STAMP(3);
     if (cslot != RT_SENT) cross[s_cbase + cslot] = k;

@@ -69,7 +69,7 @@ constexpr int kSortThreads = 512;
 constexpr int kSortItems = 8;
 constexpr int kSortTile = kSortThreads * kSortItems;   // 4096 keys / tile
 constexpr uint32_t kPrefixInKernelMaxTiles = 256;      // <= 1M keys: cross-tile prefix inside k_scatter
-constexpr int kRefitT = 1024;                          // leaves per refit block
+constexpr int kRefitT = 512;                           // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
 
 // ---- K7w wide (4-ary) trace tree, derived from the binary tree after K6.

@@ -39,7 +39,7 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 s = R.Scene.generate_soup(n, 1)
 for _ in range(3):
     s.build()
-M = (n + 1023) // 1024
+M = (n + 511) // 512
 report("k_refit_local", stamps(M)[:, :5], ["leaf/topo/parent loads", "scans+flags+sync", "climb+sync", "node stores"], 5)
 keys = np.random.default_rng(0).integers(0, 2**30, n, dtype=np.uint64).astype(np.uint32)
 for _ in range(2):
