@@ -230,6 +230,28 @@ __device__ __forceinline__ int kdelta(const uint32_t* __restrict__ keys, int64_t
     return __clz((int)(ki ^ kj));
 }
 
+// Sorted keys seen through an LDS window [lo, hi) staged by the block, with
+// global loads outside it: K4's delta searches mostly probe near i (most
+// ranges are short), so most of their dependent loads become LDS reads.
+struct KeyWin {
+    const uint32_t* __restrict__ g;
+    const uint32_t* s;
+    int64_t lo, hi;
+    __device__ __forceinline__ uint32_t operator[](int64_t j) const { return (j >= lo && j < hi) ? s[j - lo] : g[j]; }
+};
+
+__device__ __forceinline__ int kdelta(const KeyWin& keys, int64_t n, int64_t i, uint32_t ki, int64_t j) {
+    if (j < 0 || j >= n) return -1;
+    const uint32_t kj = keys[j];
+    if (ki == kj) return 32 + __clz((int)((uint32_t)i ^ (uint32_t)j));
+    return __clz((int)(ki ^ kj));
+}
+
+__device__ __forceinline__ int kdir(const KeyWin& keys, int64_t n, int64_t i) {
+    const uint32_t ki = keys[i];
+    return (kdelta(keys, n, i, ki, i + 1) - kdelta(keys, n, i, ki, i - 1)) > 0 ? 1 : -1;
+}
+
 __device__ __forceinline__ int kdir(const uint32_t* __restrict__ keys, int64_t n, int64_t i) {
     const uint32_t ki = keys[i];
     return (kdelta(keys, n, i, ki, i + 1) - kdelta(keys, n, i, ki, i - 1)) > 0 ? 1 : -1;
@@ -253,11 +275,19 @@ __device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint3
 }
 
 // Thread i: internal node i (i < n-1) and leaf i (i < n).
-__global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ svals,
+__global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restrict__ keys_g, const uint32_t* __restrict__ svals,
                                                        const float* __restrict__ tris, uint32_t n,
                                                        uint4* __restrict__ topo, uint32_t* __restrict__ parent,
                                                        void* __restrict__ nodes, float4* __restrict__ tri_s) {
+    constexpr int KW = 1024;                      // window margin on each side
+    __shared__ uint32_t s_keys[256 + 2 * KW];
     const uint32_t i32 = blockIdx.x * 256u + threadIdx.x;
+    const int64_t B = (int64_t)blockIdx.x * 256;
+    const int64_t wlo = B - KW < 0 ? 0 : B - KW;
+    const int64_t whi = B + 256 + KW > (int64_t)n ? (int64_t)n : B + 256 + KW;
+    for (int64_t j = wlo + threadIdx.x; j < whi; j += 256) s_keys[j - wlo] = keys_g[j];
+    __syncthreads();
+    const KeyWin keys{keys_g, s_keys, wlo, whi};
     if (i32 >= n) return;
     const int64_t i = i32, N = n;
     const uint32_t L0 = n - 1;
