@@ -158,8 +158,8 @@ def main():
     slab = torch.zeros(max(tmax, 1) * 256, dtype=torch.int32, device=dev) if world > 1 else None
     # every rank writes its hit records too (16 B/ray, part of the byte model); only RGBA is gathered
     slab_hits = torch.empty(max(tmax, 1) * 256 * spp * 4, dtype=torch.float32, device=dev) if world > 1 else None
-    gather_list = [torch.zeros_like(slab) for _ in range(world)] if (world > 1 and rank == 0) else None
     slabs_all = torch.zeros(world * max(tmax, 1) * 256, dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
+    gather_list = None  # gather_slabs receives straight into slabs_all's per-rank rows
 
     def step():
         build_ms = scene.build()

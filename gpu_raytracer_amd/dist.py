@@ -45,12 +45,16 @@ def gather_slabs(slab: torch.Tensor, rank: int, world: int, gather_list=None, ou
     if world == 1:
         return slab
     if rank == 0:
+        if out is not None and gather_list is None:
+            # receive straight into out's [rank] rows (views): no concatenation copy
+            gather_list = list(out.view(world, -1).unbind(0))
         if gather_list is None:
             gather_list = [torch.empty_like(slab) for _ in range(world)]
         dist.gather(slab, gather_list, dst=0)
         if out is None:
             return torch.cat(gather_list)
-        torch.cat(gather_list, out=out)
+        if gather_list[0].data_ptr() != out.data_ptr():
+            torch.cat(gather_list, out=out)
         return out
     dist.gather(slab, None, dst=0)
     return None
