@@ -114,6 +114,32 @@ def secondary_rays(R, S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev
             "shadow_mrays_per_s": round(shadow_rays / (max(med - primary_ms, 1e-6) * 1e-3) / 1e6, 2)}
 
 
+PATH_DEPTH = 2   # bounces after the primary segment
+PATH_SKY = 0.3
+
+
+def path_tracing(R, S, scene, cfg, cam, w, h, spp, img, args, torch, dev):
+    """SURVEY.md §8(f) row 3, path mode: diffuse paths of up to
+    1 + PATH_DEPTH segments with a shadow ray at every hit, same frame.
+    Untimed by the step contract; its own warm-up and timed launches
+    (hipEvents), median reported; the ray count comes from the kernel's own
+    counters (deterministic: the same paths every launch)."""
+    light = S.LIGHTS[cfg.scene]
+    ms = []
+    for i in range(args.warmup + max(args.steps, 3)):
+        t = scene.render_path_device(cam, w, h, spp, light, PATH_SKY, PATH_DEPTH, d_rgba=img.data_ptr(), timed=True)
+        if i >= args.warmup:
+            ms.append(t)
+    torch.cuda.synchronize(dev)
+    work = scene.render_path_work(cam, w, h, spp, light, PATH_SKY, PATH_DEPTH)
+    med = float(np.median(ms))
+    return {"mode": f"diffuse path tracing, max_depth {PATH_DEPTH}, next-event shadow rays (DESIGN.md)",
+            "light": list(light), "sky": PATH_SKY, "ms": round(med, 4), "rays": int(work[2]),
+            "rays_per_pixel": round(int(work[2]) / (w * h * spp), 3),
+            "mrays_per_s": round(int(work[2]) / (med * 1e-3) / 1e6, 2),
+            "node_records": int(work[0]), "tri_records": int(work[1])}
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -275,13 +301,14 @@ def main():
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM},
             "cpu_baseline": None,
         }
+        host_img = img.cpu().numpy().view(np.uint8)   # the primary frame, before the secondary modes reuse img
         if world == 1:
             out["secondary"] = secondary_rays(R, S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev,
                                               float(np.median(per[:, 1])))
+            out["path"] = path_tracing(R, S, scene, cfg, cam, w, h, spp, img, args, torch, dev)
         if world == 1 and not args.no_cpu_baseline:
             threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
             out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt)
-        host_img = img.cpu().numpy().view(np.uint8)
         import zlib
         out["image_crc32"] = zlib.crc32(host_img.tobytes()) & 0xFFFFFFFF  # same for every N (bit-exact tiles)
         if args.dump:

@@ -37,6 +37,7 @@ EXPORTED = [
     "rt_scene_get_tris", "rt_scene_set_device", "rt_scene_free", "rt_camera_look_at", "rt_bvh_build",
     "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_render", "rt_render_counters", "rt_render_work", "rt_render_device",
     "rt_render_shadow", "rt_render_shadow_device", "rt_render_shadow_work",
+    "rt_render_path", "rt_render_path_device", "rt_render_path_work",
     "rt_render_tiles_counters", "rt_tiles_for_rank",
     "rt_render_tiles_device", "rt_unpack_tiles_device", "rt_scene_stream", "rt_scene_sync",
     "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_trace",
@@ -104,6 +105,9 @@ def lib() -> C.CDLL:
         "rt_render_shadow": [P, cam, P, C.c_float, u32, u32, u32, P, P, C.POINTER(dbl)],
         "rt_render_shadow_device": [P, cam, P, C.c_float, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_shadow_work": [P, cam, P, C.c_float, u32, u32, u32, P],
+        "rt_render_path": [P, cam, P, C.c_float, u32, u32, u32, u32, P, P, C.POINTER(dbl)],
+        "rt_render_path_device": [P, cam, P, C.c_float, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],
+        "rt_render_path_work": [P, cam, P, C.c_float, u32, u32, u32, u32, P],
         "rt_render_device": [P, cam, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_tiles_counters": [P, cam, u32, u32, u32, u32, u32, P],
         "rt_render_tiles_device": [P, cam, u32, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],

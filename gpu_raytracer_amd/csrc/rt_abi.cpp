@@ -533,13 +533,73 @@ rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float l
     if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
     rt_status st = ensure_stream(s);
     if (st) return st;
-    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 16));
+    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
     hipError_t e = rt::launch_trace_shadow(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
                                            w, h, spp, light, ambient, nullptr, nullptr, s->d_ctr, s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace_shadow");
     HIPR(hipStreamSynchronize(s->stream));
     HIPR(hipMemcpy(counters_out, s->d_ctr, 16, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_render_path_device(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
+                                uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
+                                void* stream, double* ms_out) {
+    if (!s || !cam || !light || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
+    if (max_depth > 64) return fail(RT_EINVAL, "max_depth exceeds 64");
+    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
+    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
+    rt_status st = ensure_stream(s);
+    if (st) return st;
+    hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
+    if (ms_out) HIPR(hipEventRecord(s->r0, hs));
+    hipError_t e = rt::launch_trace_path(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
+                                         w, h, spp, light, sky, max_depth, d_hits, d_rgba, nullptr, hs);
+    if (e != hipSuccess) return hip_fail(e, "launch_trace_path");
+    if (ms_out) {
+        HIPR(hipEventRecord(s->r1, hs));
+        HIPR(hipEventSynchronize(s->r1));
+        float ms = 0;
+        HIPR(hipEventElapsedTime(&ms, s->r0, s->r1));
+        *ms_out = ms;
+    }
+    return RT_OK;
+}
+
+rt_status rt_render_path(rt_scene* s, const rt_camera* cam, const float light[3], float sky, uint32_t max_depth,
+                         uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
+    if (!s || !cam || !light || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
+    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
+    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
+    rt_status st = ensure_stream(s);
+    if (st) return st;
+    const size_t nh = (size_t)w * h * spp;
+    if (hits_out && (st = grow(&s->d_hits, &s->hits_cap, nh * 16))) return st;
+    if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
+    st = rt_render_path_device(s, cam, light, sky, max_depth, w, h, spp, hits_out ? s->d_hits : nullptr, s->d_rgba,
+                               nullptr, ms_out);
+    if (st) return st;
+    HIPR(hipStreamSynchronize(s->stream));
+    if (hits_out) HIPR(hipMemcpy(hits_out, s->d_hits, nh * 16, hipMemcpyDeviceToHost));
+    if (rgba_out) HIPR(hipMemcpy(rgba_out, s->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_render_path_work(rt_scene* s, const rt_camera* cam, const float light[3], float sky, uint32_t max_depth,
+                              uint32_t w, uint32_t h, uint32_t spp, uint64_t counters_out[3]) {
+    if (!s || !cam || !light || !counters_out || !w || !h || !spp) return fail(RT_EINVAL, "bad arguments");
+    if (max_depth > 64) return fail(RT_EINVAL, "max_depth exceeds 64");
+    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
+    rt_status st = ensure_stream(s);
+    if (st) return st;
+    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
+    HIPR(hipMemsetAsync(s->d_ctr, 0, 32, s->stream));
+    hipError_t e = rt::launch_trace_path(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
+                                         w, h, spp, light, sky, max_depth, nullptr, nullptr, s->d_ctr, s->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_trace_path");
+    HIPR(hipStreamSynchronize(s->stream));
+    HIPR(hipMemcpy(counters_out, s->d_ctr, 24, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
@@ -550,7 +610,7 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
     rt_status st = ensure_stream(s);
     if (st) return st;
-    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 16));
+    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
                                     nranks, packed, nullptr, nullptr, s->d_ctr, binary, s->d_work, s->stream);

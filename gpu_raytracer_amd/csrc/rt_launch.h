@@ -97,6 +97,12 @@ hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const flo
                                uint32_t n, const CamF& cam, uint32_t w, uint32_t h, uint32_t spp,
                                const float light[3], float ambient, void* hits, void* rgba,
                                unsigned long long* counters, hipStream_t s);
+// Path mode: primary hits into `hits`, diffuse-path image into
+// `rgba`; counters (nullable): [0] node records, [1] tri records, [2] rays.
+hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+                             uint32_t n, const CamF& cam, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
+                             float sky, uint32_t max_depth, void* hits, void* rgba, unsigned long long* counters,
+                             hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
                          void* img, hipStream_t s);
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);

@@ -76,7 +76,8 @@ __device__ __forceinline__ bool intersect_tri(const float* o, const float* d, co
 template <bool COUNT, bool ANY = false>
 __device__ __forceinline__ void trace_ray_from(const char* __restrict__ nodes, const float4* __restrict__ tri_s,
                                                uint32_t n, const float* o, const float* d, uint32_t start, float& tb,
-                                               float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
+                                               float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct,
+                                               bool any = ANY) {
     float invd[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) invd[c] = 1.0f / d[c];
@@ -99,7 +100,7 @@ __device__ __forceinline__ void trace_ray_from(const char* __restrict__ nodes, c
             float t, u, v;
             if (intersect_tri(o, d, tv, tb, t, u, v)) {
                 tb = t; hu = u; hv = v; hp = pprim;
-                if (ANY) return;  // any-hit (shadow ray): the first hit ends the search
+                if (any) return;  // any-hit (shadow ray): the first hit ends the search
             }
             pend = RT_SENT;
         }
@@ -227,7 +228,7 @@ __device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const ui
 template <bool COUNT, int NT, bool ANY = false>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
-                                         uint32_t& cn, uint32_t& ct) {
+                                         uint32_t& cn, uint32_t& ct, bool any = ANY) {
     if (++R.steps > limit) return 2;
     if (R.pend == RT_SENT) {
         if (R.cur == RT_SENT) wide_pop<NT>(R, sref, stn);
@@ -254,7 +255,7 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
             float t, u, v;
             if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) {
                 R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(T2.y);
-                if (ANY) { R.pend = RT_SENT; return 1; }  // any-hit: done
+                if (any) { R.pend = RT_SENT; return 1; }  // any-hit: done
             }
         }
         R.pend = RT_SENT;
@@ -304,7 +305,60 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     return 0;
 }
 
+// One ray from o along d over (0, tmax): the wide traversal when it applies
+// (finite 1/d, K7w records present), with the binary hand-off on overflow;
+// the binary traversal from the root otherwise.  any: the first hit ends it.
+template <bool COUNT, int NT>
+__device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                          uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n, const float* o,
+                                          const float* d, float tmax, bool any, uint32_t* sref, uint16_t* stn,
+                                          float& tb, float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
+    WRay R;
+    wray_init(d, R);
+    R.tb = tmax;
+    const bool wide = R.fin && wnodes && n >= 2;
+    int st = wide ? 0 : 2;
+    while (st == 0) st = wide_step<COUNT, NT>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any);
+    if (st == 2) {
+        const uint32_t start = !wide ? (n ? 0u : RT_SENT) : (R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1));
+        trace_ray_from<COUNT>(nodes, tri_s, n, o, R.d, start, R.tb, R.hu, R.hv, R.hp, cn, ct, any);
+    }
+    tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
+}
+
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
+
+// Shading frame of a hit (shadow and path modes): P = o + t d,
+// unit geometric normal N flipped to face the incoming ray, S = P + 1e-4 N,
+// D = light - S, cosl = N.D/|D|.  Operation order as the oracle's.
+struct Surf { float N[3], S[3], D[3], cosl; };
+
+__device__ __forceinline__ void surface(const float* __restrict__ tris, uint32_t prim, const float* o, const float* d,
+                                        float t, const float* lp, Surf& f) {
+    const float* tri = tris + (uint64_t)prim * 9;
+    float P[3], e1[3], e2[3], nrm[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        P[a] = o[a] + t * d[a];
+        e1[a] = tri[3 + a] - tri[a];
+        e2[a] = tri[6 + a] - tri[a];
+    }
+    cross3(e1, e2, nrm);
+    const float nl = sqrtf(dot3(nrm, nrm));
+#pragma unroll
+    for (int a = 0; a < 3; ++a) f.N[a] = nl > 0.0f ? nrm[a] / nl : 0.0f;
+    if (dot3(f.N, d) > 0.0f) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) f.N[a] = -f.N[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        f.S[a] = P[a] + f.N[a] * 1e-4f;
+        f.D[a] = lp[a] - f.S[a];
+    }
+    const float dl = sqrtf(dot3(f.D, f.D));
+    f.cosl = dl > 0.0f ? dot3(f.N, f.D) / dl : 0.0f;
+}
 
 // Shadow mode [SPEC, DESIGN.md "Shadow mode"]: the lighting factor f of a
 // primary hit -- one any-hit shadow ray from the hit (offset 1e-4 along the
@@ -318,43 +372,12 @@ __device__ __forceinline__ float shadow_factor(const char* __restrict__ nodes, c
                                                const float* __restrict__ tris, uint32_t n, const float* o,
                                                const float* d, float t, uint32_t prim, const Light& lt,
                                                uint32_t* sref, uint16_t* stn, uint32_t& cn, uint32_t& ct) {
-    const float* tri = tris + (uint64_t)prim * 9;
-    float P[3], e1[3], e2[3], nrm[3], N[3], S[3], D[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        P[a] = o[a] + t * d[a];
-        e1[a] = tri[3 + a] - tri[a];
-        e2[a] = tri[6 + a] - tri[a];
-    }
-    cross3(e1, e2, nrm);
-    const float nl = sqrtf(dot3(nrm, nrm));
-#pragma unroll
-    for (int a = 0; a < 3; ++a) N[a] = nl > 0.0f ? nrm[a] / nl : 0.0f;
-    if (dot3(N, d) > 0.0f) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) N[a] = -N[a];
-    }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        S[a] = P[a] + N[a] * 1e-4f;
-        D[a] = lt.p[a] - S[a];
-    }
-    // any-hit over (0, 1): wide traversal when it applies, else binary
-    WRay R;
-    wray_init(D, R);
-    R.tb = 1.0f;
-    int st = (R.fin && wnodes && n >= 2) ? 0 : 2;
-    while (st == 0) st = wide_step<COUNT, NT, true>(R, wnodes, tri_s, S, wcap, 4 * n + 16, sref, stn, cn, ct);
-    if (st == 2) {
-        const bool restart = !(R.fin && wnodes && n >= 2);
-        if (restart) { R.cur = n ? 0u : RT_SENT; R.tb = 1.0f; R.hp = RT_SENT; }
-        trace_ray_from<COUNT, true>(nodes, tri_s, n, S, D,
-                                    R.cur == RT_SENT ? RT_SENT : (restart ? R.cur : bin_of(R.cur, n - 1)), R.tb, R.hu,
-                                    R.hv, R.hp, cn, ct);
-    }
-    const float dl = sqrtf(dot3(D, D));
-    const float cosl = dl > 0.0f ? dot3(N, D) / dl : 0.0f;
-    const float lit = R.hp != RT_SENT ? 0.0f : fmaxf(cosl, 0.0f);
+    Surf f;
+    surface(tris, prim, o, d, t, lt.p, f);
+    float tb, hu, hv;
+    uint32_t hp;
+    trace_gen<COUNT, NT>(nodes, wnodes, wcap, tri_s, n, f.S, f.D, 1.0f, true, sref, stn, tb, hu, hv, hp, cn, ct);
+    const float lit = hp != RT_SENT ? 0.0f : fmaxf(f.cosl, 0.0f);
     return lt.ambient + (1.0f - lt.ambient) * lit;
 }
 
@@ -481,6 +504,152 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
         if (l == 0) {
             atomicAdd(&counters[0], a);
             atomicAdd(&counters[1], bsum);
+        }
+    }
+}
+
+// ---------------------------------------------------------------- path mode
+// Path mode [SPEC, DESIGN.md "Path mode"; SURVEY.md §8(f) row 3]: per
+// sample a diffuse path of up to 1 + max_depth segments; at every hit a
+// shadow ray toward the point light when it is above the surface (next-event
+// estimation) and, below max_depth, a cosine-weighted bounce.  Operation
+// order as orc_render_path.
+//
+// Megakernel with ONE trace call site: each lane runs a small state machine
+// (segment / shadow ray / next sample) around a single trace_gen, so lanes
+// whose next ray is a shadow ray and lanes whose next ray is a bounce share
+// the same traversal loop instead of running two divergent loops in turn.
+__device__ __forceinline__ uint32_t path_next(uint32_t& st) { st = pcg_hash(st); return st; }
+__device__ __forceinline__ float path_u01(uint32_t& st) { return (float)(path_next(st) >> 8) * 0x1p-24f; }
+
+struct PathCfg { float light[3]; float sky; uint32_t max_depth; };
+
+template <bool COUNT, int NT>
+__global__ __launch_bounds__(NT) void k_path(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                              uint32_t wcap, const float4* __restrict__ tri_s,
+                                              const float* __restrict__ tris, uint32_t n, Cam cam, uint32_t W,
+                                              uint32_t H, uint32_t spp, uint32_t tilesX, PathCfg pc,
+                                              float4* __restrict__ hits, uint32_t* __restrict__ rgba,
+                                              unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t s_ref[(kWideStack + 1) * NT];
+    __shared__ uint16_t s_tn[(kWideStack + 1) * NT];
+    constexpr uint32_t WPB = NT / 64;
+    const uint32_t gw = blockIdx.x * WPB + (threadIdx.x >> 6);
+    const uint32_t t = gw >> 2;
+    const uint32_t l = threadIdx.x & 63, w = gw & 3;
+    const uint32_t x = (t % tilesX) * 16 + (w & 1) * 8 + (l & 7), y = (t / tilesX) * 16 + (w >> 1) * 8 + (l >> 3);
+    const char* nd = reinterpret_cast<const char*>(nodes);
+    uint32_t cn = 0, ct = 0, crays = 0;
+    if (x < W && y < H) {
+        float r = 0.0f, g = 0.0f, b = 0.0f;
+        float o[3], d[3], L[3], beta[3], alb[3], N[3], S[3], cosl = 0.0f, tmax = 0.0f;
+        uint32_t s = 0, depth = 0, st = 0, sidx = 0;
+        bool shadow = false;
+        auto start_sample = [&]() {
+            sidx = (y * W + x) * spp + s;
+            ray_dir(cam, x, y, W, spp, s, d);
+#pragma unroll
+            for (int a = 0; a < 3; ++a) { o[a] = cam.eye[a]; L[a] = 0.0f; beta[a] = 1.0f; }
+            st = pcg_hash(sidx ^ 0x5bd1e995u);
+            depth = 0; shadow = false; tmax = __builtin_inff();
+        };
+        start_sample();
+        for (;;) {
+            float tb, hu, hv;
+            uint32_t hp;
+            trace_gen<COUNT, NT>(nd, wnodes, wcap, tri_s, n, o, d, tmax, shadow, s_ref + threadIdx.x,
+                                 s_tn + threadIdx.x, tb, hu, hv, hp, cn, ct);
+            ++crays;
+            bool bounce = false, done = false;
+            if (!shadow) {
+                if (depth == 0 && hits) hits[sidx] = make_float4(tb, hu, hv, __uint_as_float(hp));
+                if (hp == RT_SENT) {
+                    if (depth > 0) {
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) L[a] = L[a] + beta[a] * pc.sky;
+                    }
+                    done = true;
+                } else {
+                    Surf f;
+                    surface(tris, hp, o, d, tb, pc.light, f);
+                    const uint32_t ha = pcg_hash(hp ^ 0x27d4eb2fu);
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        N[a] = f.N[a];
+                        S[a] = f.S[a];
+                        alb[a] = 0.25f + (float)((ha >> (8 * a)) & 0xFFu) * 0x1p-9f;
+                    }
+                    cosl = f.cosl;
+                    if (cosl > 0.0f) {  // next: the shadow ray
+                        shadow = true;
+                        tmax = 1.0f;
+#pragma unroll
+                        for (int a = 0; a < 3; ++a) { o[a] = S[a]; d[a] = f.D[a]; }
+                    } else {
+                        bounce = true;
+                    }
+                }
+            } else {
+                if (hp == RT_SENT) {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) L[a] = L[a] + (beta[a] * alb[a]) * cosl;
+                }
+                bounce = true;
+            }
+            if (bounce) {
+                if (depth == pc.max_depth) {
+                    done = true;
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) beta[a] = beta[a] * alb[a];
+                    float px = 0.0f, py = 0.0f, r2 = 0.0f;
+                    for (int k = 0; k < 16; ++k) {
+                        const float qx = path_u01(st) * 2.0f - 1.0f;
+                        const float qy = path_u01(st) * 2.0f - 1.0f;
+                        const float q2 = qx * qx + qy * qy;
+                        if (q2 < 1.0f) { px = qx; py = qy; r2 = q2; break; }
+                    }
+                    const float z = sqrtf(1.0f - r2);
+                    const float sg = N[2] >= 0.0f ? 1.0f : -1.0f;
+                    const float ia = -1.0f / (sg + N[2]);
+                    const float ib = (N[0] * N[1]) * ia;
+                    const float T[3] = {1.0f + ((sg * N[0]) * N[0]) * ia, sg * ib, -(sg * N[0])};
+                    const float B[3] = {ib, sg + (N[1] * N[1]) * ia, -N[1]};
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        d[a] = (px * T[a] + py * B[a]) + z * N[a];
+                        o[a] = S[a];
+                    }
+                    shadow = false;
+                    tmax = __builtin_inff();
+                    ++depth;
+                }
+            }
+            if (done) {
+                r = r + L[0];
+                g = g + L[1];
+                b = b + L[2];
+                if (++s == spp) break;
+                start_sample();
+            }
+        }
+        if (rgba) {
+            const float sc = 1.0f / (float)spp;
+            rgba[(uint64_t)y * W + x] = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+        }
+    }
+    if (COUNT) {
+        unsigned long long a = cn, bsum = ct, c = crays;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            bsum += __shfl_xor(bsum, off, 64);
+            c += __shfl_xor(c, off, 64);
+        }
+        if (l == 0) {
+            atomicAdd(&counters[0], a);
+            atomicAdd(&counters[1], bsum);
+            atomicAdd(&counters[2], c);
         }
     }
 }
@@ -772,6 +941,39 @@ hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const flo
         if (wide) RT_SHADOW(false, true); else RT_SHADOW(false, false);
     }
 #undef RT_SHADOW
+    return hipGetLastError();
+}
+
+hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+                             uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
+                             float sky, uint32_t max_depth, void* hits, void* rgba, unsigned long long* counters,
+                             hipStream_t s) {
+    const uint32_t nb = tiles_for_rank(w, h, 0, 1);
+    if (!nb) return hipSuccess;
+    Cam cam;
+    for (int i = 0; i < 3; ++i) {
+        cam.eye[i] = c.eye[i]; cam.w00[i] = c.w00[i]; cam.du[i] = c.du[i]; cam.dv[i] = c.dv[i];
+    }
+    PathCfg pc;
+    for (int i = 0; i < 3; ++i) pc.light[i] = light[i];
+    pc.sky = sky;
+    pc.max_depth = max_depth;
+    const uint32_t tilesX = (w + 15) / 16;
+    float4* H = reinterpret_cast<float4*>(hits);
+    uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
+    // K7w records unless the binary traversal is asked for (variant 2)
+    const uint4* wn = (g_trace_config.variant != 2) ? wnodes : nullptr;
+    const uint32_t cap = g_trace_config.stack_cap;
+    const bool small = g_trace_config.wg == 64;
+#define RT_PATH(C, NT)                                                                                            \
+    hipLaunchKernelGGL((k_path<C, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, cam, \
+                       w, h, spp, tilesX, pc, H, R, counters)
+    if (counters) {
+        if (small) RT_PATH(true, 64); else RT_PATH(true, 256);
+    } else {
+        if (small) RT_PATH(false, 64); else RT_PATH(false, 256);
+    }
+#undef RT_PATH
     return hipGetLastError();
 }
 

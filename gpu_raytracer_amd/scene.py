@@ -191,6 +191,33 @@ class Scene:
         call("rt_render_shadow_work", self._h, C.byref(cam), _p(L), float(ambient), w, h, spp, _p(c))
         return c
 
+    def render_path(self, cam: rt_camera, w: int, h: int, spp: int, light, sky: float, max_depth: int,
+                    hits: bool = True):
+        """Path mode: (primary hits or None, path-traced rgba, ms)."""
+        hb = np.zeros(w * h * spp, HIT_DTYPE) if hits else None
+        rb = np.zeros(w * h * 4, np.uint8)
+        L = np.ascontiguousarray(light, np.float32).reshape(3)
+        ms = C.c_double()
+        call("rt_render_path", self._h, C.byref(cam), _p(L), float(sky), int(max_depth), w, h, spp,
+             _p(hb) if hits else None, _p(rb), C.byref(ms))
+        return hb, rb, ms.value
+
+    def render_path_device(self, cam, w, h, spp, light, sky, max_depth, d_rgba: int = 0, d_hits: int = 0,
+                           stream: int = 0, timed: bool = False):
+        L = np.ascontiguousarray(light, np.float32).reshape(3)
+        ms = C.c_double()
+        call("rt_render_path_device", self._h, C.byref(cam), _p(L), float(sky), int(max_depth), w, h, spp,
+             C.c_void_p(d_hits) if d_hits else None, C.c_void_p(d_rgba) if d_rgba else None,
+             C.c_void_p(stream) if stream else None, C.byref(ms) if timed else None)
+        return ms.value if timed else None
+
+    def render_path_work(self, cam, w, h, spp, light, sky, max_depth) -> np.ndarray:
+        """Path-mode kernel work: node records, tri records, rays traced."""
+        c = np.zeros(3, np.uint64)
+        L = np.ascontiguousarray(light, np.float32).reshape(3)
+        call("rt_render_path_work", self._h, C.byref(cam), _p(L), float(sky), int(max_depth), w, h, spp, _p(c))
+        return c
+
     def render_counters(self, cam: rt_camera, w: int, h: int, spp: int = 1) -> np.ndarray:
         """§9.7 binary-traversal counters (the oracle's): nodes fetched, tris tested."""
         c = np.zeros(2, np.uint64)

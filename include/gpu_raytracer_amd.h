@@ -123,6 +123,23 @@ rt_status rt_render_shadow_device(rt_scene* s, const rt_camera* cam, const float
  * fetched, [1] triangle records loaded */
 rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
                                 uint32_t w, uint32_t h, uint32_t spp, uint64_t counters_out[2]);
+/* Path mode (SURVEY.md §8(f) row 3 "simple path tracing"; contract in
+ * DESIGN.md "Path mode"): per sample a diffuse path of up to 1 + max_depth
+ * segments (max_depth <= 64) with next-event estimation toward the point
+ * light light[3] and sky radiance `sky` for escaped bounce rays; per-triangle
+ * albedo from pcg_hash(prim).  hits_out = primary hits.  Bit-identical to the
+ * oracle's orc_render_path. */
+rt_status rt_render_path(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
+                         uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits_out,
+                         uint8_t* rgba_out, double* ms_out);
+rt_status rt_render_path_device(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
+                                uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, void* d_hits,
+                                void* d_rgba, void* stream, double* ms_out);
+/* work of the path-mode kernel: [0] node records fetched, [1] triangle
+ * records loaded, [2] rays traced (primary + bounce + shadow) */
+rt_status rt_render_path_work(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
+                              uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp,
+                              uint64_t counters_out[3]);
 /* work of the configured (default: wide) trace kernel itself: [0] node
  * records fetched (64 B wide / 32 B binary), [1] triangle records loaded */
 rt_status rt_render_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,

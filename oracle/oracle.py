@@ -78,6 +78,7 @@ def lib():
         L.orc_trace.argtypes = [P, u32, P, C.POINTER(Camera), u32, u32, u32, u32, u32, P, P, i32]
         L.orc_shade.argtypes = [P, u32, u32, u32, P]
         L.orc_render_shadow.argtypes = [P, u32, P, C.POINTER(Camera), u32, u32, u32, P, f32, P, P, P, i32]
+        L.orc_render_path.argtypes = [P, u32, P, C.POINTER(Camera), u32, u32, u32, P, f32, u32, P, P, P, i32]
         _lib = L
     return _lib
 
@@ -197,6 +198,22 @@ def render_shadow(nodes, tris, cam: Camera, w, h, spp, light, ambient, nthreads=
     nthreads = nthreads or (os.cpu_count() or 1)
     lib().orc_render_shadow(_p(nd), n, _p(tr), C.byref(cam), w, h, spp, _p(L), float(ambient), _p(hits), _p(rgba),
                             _p(cnt), int(nthreads))
+    return hits[: w * h * spp], rgba[: w * h * 4], cnt
+
+
+def render_path(nodes, tris, cam: Camera, w, h, spp, light, sky, max_depth, nthreads=None):
+    """Path mode: returns (primary hits, rgba, counters[nodes, tris, rays])."""
+    tris = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 9)
+    n = tris.shape[0]
+    hits = np.zeros(max(w * h * spp, 1), HIT_DTYPE)
+    rgba = np.zeros(max(w * h * 4, 1), np.uint8)
+    cnt = np.zeros(3, np.uint64)
+    nd = np.ascontiguousarray(nodes) if len(nodes) else np.zeros(1, NODE_DTYPE)
+    tr = tris if n else np.zeros((1, 9), np.float32)
+    L = np.ascontiguousarray(light, np.float32).reshape(3)
+    nthreads = nthreads or (os.cpu_count() or 1)
+    lib().orc_render_path(_p(nd), n, _p(tr), C.byref(cam), w, h, spp, _p(L), float(sky), int(max_depth), _p(hits),
+                          _p(rgba), _p(cnt), int(nthreads))
     return hits[: w * h * spp], rgba[: w * h * 4], cnt
 
 

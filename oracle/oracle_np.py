@@ -284,13 +284,21 @@ def rays(cam, w, h, spp):
 
 def trace(b, tris, cam, w, h, spp=1):
     """Vectorised over rays.  Returns (t, u, v, prim, nodes_fetched, tris_tested)."""
+    o, d = rays(np.asarray(cam, f32), w, h, spp)
+    return trace_rays(b, tris, o, d)
+
+
+def trace_rays(b, tris, o, d, tmax=np.inf, any_hit=False):
+    """§9.7 escape-link traversal of arbitrary rays over (0, tmax); any_hit
+    ends a ray at its first hit (shadow rays)."""
     tris = np.asarray(tris, f32).reshape(-1, 9)
     n = len(tris)
-    o, d = rays(np.asarray(cam, f32), w, h, spp)
+    o = np.asarray(o, f32)
+    d = np.asarray(d, f32)
     R = len(d)
     with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
         invd = f32(1) / d
-    tb = np.full(R, np.inf, f32)
+    tb = np.full(R, tmax, f32)
     hu = np.zeros(R, f32)
     hv = np.zeros(R, f32)
     hp = np.full(R, SENTINEL, np.uint32)
@@ -336,9 +344,127 @@ def trace(b, tris, cam, w, h, spp=1):
                 ok = (det != 0) & ~((u < 0) | (u > 1)) & ~((v < 0) | (u + v > 1)) & ~(t <= 0) & (t < tb[lr])
                 w_ = lr[ok]
                 tb[w_] = t[ok]; hu[w_] = u[ok]; hv[w_] = v[ok]; hp[w_] = prim[ok]
+                if any_hit:
+                    new[np.nonzero(leaf)[0][ok]] = -1
             idx[r] = new
             act = idx >= 0
     return tb, hu, hv, hp, nn, nt
+
+
+def _q8(x):
+    return fmin(fmax(x * f32(255) + f32(0.5), f32(0)), f32(255)).astype(np.uint8)
+
+
+def _surface(tris, prim, o, d, t, light):
+    """Shading frame of hits (DESIGN.md shadow/path modes): unit geometric
+    normal facing the ray, S = P + 1e-4 N, D = light - S, cos to the light."""
+    V = np.asarray(tris, f32).reshape(-1, 3, 3)[prim]
+    P = o + t[:, None] * d
+    e1 = V[:, 1] - V[:, 0]
+    e2 = V[:, 2] - V[:, 0]
+    nrm = cross(e1, e2)
+    nl = np.sqrt(dot(nrm, nrm))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        N = np.where((nl > 0)[:, None], nrm / nl[:, None], f32(0)).astype(f32)
+    N = np.where((dot(N, d) > 0)[:, None], -N, N).astype(f32)
+    S = P + N * f32(1e-4)
+    D = np.asarray(light, f32)[None, :] - S
+    dl = np.sqrt(dot(D, D))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        cosl = np.where(dl > 0, dot(N, D) / dl, f32(0)).astype(f32)
+    return N, S, D, cosl
+
+
+def render_shadow(b, tris, cam, w, h, spp, light, ambient):
+    """Shadow mode: (t, u, v, prim, rgba)."""
+    o, d = rays(np.asarray(cam, f32), w, h, spp)
+    t, u, v, p, _, _ = trace_rays(b, tris, o, d)
+    hit = np.nonzero(p != SENTINEL)[0]
+    f = np.zeros(len(d), f32)
+    if len(hit):
+        N, S, D, cosl = _surface(tris, p[hit], o[hit], d[hit], t[hit], light)
+        _, _, _, sp, _, _ = trace_rays(b, tris, S, D, f32(1), True)
+        lit = np.where(sp != SENTINEL, f32(0), fmax(cosl, f32(0)))
+        f[hit] = f32(ambient) + (f32(1) - f32(ambient)) * lit
+    rgb = np.stack([u * f, v * f, ((f32(1) - u) - v) * f], 1).astype(f32)
+    rgb[p == SENTINEL] = 0
+    return t, u, v, p, _mean_q8(rgb, spp)
+
+
+def _mean_q8(rgb, spp):
+    rgb = rgb.reshape(-1, spp, 3)
+    acc = np.zeros((rgb.shape[0], 3), f32)
+    for s in range(spp):
+        acc = acc + rgb[:, s]
+    out = np.empty((rgb.shape[0], 4), np.uint8)
+    out[:, :3] = _q8(acc * (f32(1) / f32(spp)))
+    out[:, 3] = 255
+    return out.reshape(-1)
+
+
+def render_path(b, tris, cam, w, h, spp, light, sky, max_depth):
+    """Path mode, advanced as a wavefront: every live path traces
+    its next segment together.  Returns (t, u, v, prim of the primary rays,
+    rgba, rays traced)."""
+    o, d = rays(np.asarray(cam, f32), w, h, spp)
+    R = len(d)
+    st = pcg_hash(np.arange(R, dtype=np.uint64) ^ np.uint64(0x5BD1E995))
+    L = np.zeros((R, 3), f32)
+    beta = np.ones((R, 3), f32)
+    live = np.arange(R)
+    nrays = 0
+    sky = f32(sky)
+    for depth in range(max_depth + 1):
+        t, u, v, p, _, _ = trace_rays(b, tris, o[live], d[live])
+        nrays += len(live)
+        if depth == 0:
+            prim0 = (t, u, v, p)
+        miss = p == SENTINEL
+        if depth > 0:
+            L[live[miss]] = L[live[miss]] + beta[live[miss]] * sky
+        hm = ~miss
+        live, t, p = live[hm], t[hm], p[hm]
+        if not len(live):
+            break
+        N, S, D, cosl = _surface(tris, p, o[live], d[live], t, light)
+        ha = pcg_hash(p.astype(np.uint64) ^ np.uint64(0x27D4EB2F))
+        alb = np.stack([f32(0.25) + ((ha >> np.uint32(8 * c)) & np.uint32(255)).astype(f32) * f32(2.0 ** -9)
+                        for c in range(3)], 1).astype(f32)
+        sh = cosl > 0
+        if sh.any():
+            _, _, _, sp, _, _ = trace_rays(b, tris, S[sh], D[sh], f32(1), True)
+            nrays += int(sh.sum())
+            vis = np.nonzero(sh)[0][sp == SENTINEL]
+            r = live[vis]
+            L[r] = L[r] + (beta[r] * alb[vis]) * cosl[vis][:, None]
+        if depth == max_depth:
+            break
+        beta[live] = beta[live] * alb
+        sl = st[live]
+        px = np.zeros(len(live), f32); py = np.zeros(len(live), f32); r2 = np.zeros(len(live), f32)
+        todo = np.ones(len(live), bool)
+        for _k in range(16):
+            i = np.nonzero(todo)[0]
+            if not len(i):
+                break
+            sl[i] = pcg_hash(sl[i])
+            qx = (sl[i] >> np.uint32(8)).astype(f32) * f32(2.0 ** -24) * f32(2) - f32(1)
+            sl[i] = pcg_hash(sl[i])
+            qy = (sl[i] >> np.uint32(8)).astype(f32) * f32(2.0 ** -24) * f32(2) - f32(1)
+            q2 = qx * qx + qy * qy
+            acc = q2 < f32(1)
+            px[i[acc]] = qx[acc]; py[i[acc]] = qy[acc]; r2[i[acc]] = q2[acc]
+            todo[i[acc]] = False
+        st[live] = sl
+        z = np.sqrt(f32(1) - r2)
+        sg = np.where(N[:, 2] >= 0, f32(1), f32(-1)).astype(f32)
+        ia = f32(-1) / (sg + N[:, 2])
+        ib = (N[:, 0] * N[:, 1]) * ia
+        T = np.stack([f32(1) + ((sg * N[:, 0]) * N[:, 0]) * ia, sg * ib, -(sg * N[:, 0])], 1).astype(f32)
+        B = np.stack([ib, sg + (N[:, 1] * N[:, 1]) * ia, -N[:, 1]], 1).astype(f32)
+        d[live] = (px[:, None] * T + py[:, None] * B) + z[:, None] * N
+        o[live] = S
+    return prim0 + (_mean_q8(L, spp), nrays)
 
 
 def shade(tb, hu, hv, hp, w, h, spp):

@@ -520,3 +520,145 @@ void orc_render_shadow(const orc_node* nodes, uint32_t n, const float* tris, con
         }
     if (counters) { counters[0] = cn; counters[1] = ct; }
 }
+
+/* ------------------------------------------------------- path mode [SPEC] */
+/* DESIGN.md "Path mode" ("simple path tracing"):
+ * per sample, a diffuse path of up to 1 + max_depth closest-hit segments.
+ * At every hit: next-event estimation toward the point light (one any-hit
+ * shadow ray over (0, 1), traced only when the light is above the surface),
+ * then -- below max_depth -- a cosine-weighted bounce about the
+ * viewer-facing geometric normal.  Escaped bounce rays add the constant sky
+ * radiance; an escaped primary ray is black.  Albedo per triangle from
+ * pcg_hash(prim).  Every operation is IEEE fp32 (+, -, *, /, sqrtf) in the
+ * order written, so the GPU result is bit-identical. */
+static inline uint32_t path_next(uint32_t* st) { *st = orc_pcg_hash(*st); return *st; }
+static inline float path_u01(uint32_t* st) { return (float)(path_next(st) >> 8) * 0x1p-24f; }
+
+static void path_sample(const orc_node* nodes, uint32_t n, const float* tris, const float eye[3],
+                        const float d0[3], uint32_t sidx, const float Lp[3], float sky, uint32_t max_depth,
+                        orc_hit* primary, float Lo[3], uint64_t cnt[3]) {
+    float o[3] = {eye[0], eye[1], eye[2]}, d[3] = {d0[0], d0[1], d0[2]};
+    float L[3] = {0.0f, 0.0f, 0.0f}, beta[3] = {1.0f, 1.0f, 1.0f};
+    uint32_t st = orc_pcg_hash(sidx ^ 0x5bd1e995u);
+    for (uint32_t depth = 0;; ++depth) {
+        orc_hit h;
+        trace_ray_t(nodes, n, tris, o, d, INFINITY, 0, &h, &cnt[0], &cnt[1]);
+        ++cnt[2];
+        if (depth == 0 && primary) *primary = h;
+        if (h.prim == ORC_SENTINEL) {
+            if (depth > 0)
+                for (int a = 0; a < 3; ++a) L[a] = L[a] + beta[a] * sky;
+            break;
+        }
+        const float* tri = tris + (size_t)h.prim * 9;
+        float P[3], e1[3], e2[3], nrm[3], N[3], S[3], D[3], alb[3];
+        for (int a = 0; a < 3; ++a) {
+            P[a] = o[a] + h.t * d[a];
+            e1[a] = tri[3 + a] - tri[a];
+            e2[a] = tri[6 + a] - tri[a];
+        }
+        cross3(e1, e2, nrm);
+        const float nl = sqrtf(dot3(nrm, nrm));
+        for (int a = 0; a < 3; ++a) N[a] = nl > 0.0f ? nrm[a] / nl : 0.0f;
+        if (dot3(N, d) > 0.0f)
+            for (int a = 0; a < 3; ++a) N[a] = -N[a];
+        const uint32_t ha = orc_pcg_hash(h.prim ^ 0x27d4eb2fu);
+        for (int a = 0; a < 3; ++a) {
+            S[a] = P[a] + N[a] * 1e-4f;
+            D[a] = Lp[a] - S[a];
+            alb[a] = 0.25f + (float)((ha >> (8 * a)) & 0xFFu) * 0x1p-9f;
+        }
+        const float dl = sqrtf(dot3(D, D));
+        const float cosl = dl > 0.0f ? dot3(N, D) / dl : 0.0f;
+        if (cosl > 0.0f) {
+            orc_hit sh;
+            trace_ray_t(nodes, n, tris, S, D, 1.0f, 1, &sh, &cnt[0], &cnt[1]);
+            ++cnt[2];
+            if (sh.prim == ORC_SENTINEL)
+                for (int a = 0; a < 3; ++a) L[a] = L[a] + (beta[a] * alb[a]) * cosl;
+        }
+        if (depth == max_depth) break;
+        for (int a = 0; a < 3; ++a) beta[a] = beta[a] * alb[a];
+        /* cosine-weighted direction: a point of the unit disk by rejection
+         * (16 tries, then the centre), lifted to the hemisphere about N */
+        float px = 0.0f, py = 0.0f, r2 = 0.0f;
+        for (int k = 0; k < 16; ++k) {
+            const float qx = path_u01(&st) * 2.0f - 1.0f;
+            const float qy = path_u01(&st) * 2.0f - 1.0f;
+            const float q2 = qx * qx + qy * qy;
+            if (q2 < 1.0f) { px = qx; py = qy; r2 = q2; break; }
+        }
+        const float z = sqrtf(1.0f - r2);
+        const float sg = N[2] >= 0.0f ? 1.0f : -1.0f;
+        const float ia = -1.0f / (sg + N[2]);
+        const float ib = (N[0] * N[1]) * ia;
+        const float T[3] = {1.0f + ((sg * N[0]) * N[0]) * ia, sg * ib, -(sg * N[0])};
+        const float B[3] = {ib, sg + (N[1] * N[1]) * ia, -N[1]};
+        for (int a = 0; a < 3; ++a) {
+            d[a] = (px * T[a] + py * B[a]) + z * N[a];
+            o[a] = S[a];
+        }
+    }
+    for (int a = 0; a < 3; ++a) Lo[a] = L[a];
+}
+
+typedef struct {
+    const orc_node* nodes; uint32_t n; const float* tris; const orc_camera* cam;
+    uint32_t w, h, spp, max_depth; const float* light; float sky;
+    orc_hit* hits; uint8_t* rgba; int tid, nthreads; uint64_t cnt[3];
+} path_job;
+
+static void* path_worker(void* arg) {
+    path_job* j = (path_job*)arg;
+    const orc_camera* c = j->cam;
+    const float sc = 1.0f / (float)j->spp;
+    for (uint64_t y = (uint64_t)j->tid; y < j->h; y += (uint64_t)j->nthreads)
+        for (uint32_t x = 0; x < j->w; ++x) {
+            float r = 0.0f, g = 0.0f, b = 0.0f;
+            for (uint32_t s = 0; s < j->spp; ++s) {
+                const uint32_t sidx = (uint32_t)((y * j->w + x) * j->spp + s);
+                float jx = 0.5f, jy = 0.5f;
+                if (s > 0) {
+                    const uint32_t hh = orc_pcg_hash(sidx);
+                    jx = (float)(hh >> 8) * 0x1p-24f;
+                    jy = (float)(orc_pcg_hash(hh) >> 8) * 0x1p-24f;
+                }
+                const float px = (float)x + jx, py = (float)y + jy;
+                float d[3], rgb[3];
+                for (int a = 0; a < 3; ++a) d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
+                path_sample(j->nodes, j->n, j->tris, c->eye, d, sidx, j->light, j->sky, j->max_depth,
+                            j->hits ? &j->hits[sidx] : NULL, rgb, j->cnt);
+                r = r + rgb[0];
+                g = g + rgb[1];
+                b = b + rgb[2];
+            }
+            const uint64_t p = y * j->w + x;
+            j->rgba[p * 4 + 0] = q8(r * sc);
+            j->rgba[p * 4 + 1] = q8(g * sc);
+            j->rgba[p * 4 + 2] = q8(b * sc);
+            j->rgba[p * 4 + 3] = 255;
+        }
+    return NULL;
+}
+
+void orc_render_path(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* cam,
+                     uint32_t w, uint32_t h, uint32_t spp, const float light[3], float sky, uint32_t max_depth,
+                     orc_hit* hits, uint8_t* rgba, uint64_t counters[3], int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    path_job* jobs = (path_job*)calloc((size_t)nthreads, sizeof(path_job));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; ++t) {
+        path_job jb = {nodes, n, tris, cam, w, h, spp, max_depth, light, sky, hits, rgba, t, nthreads, {0, 0, 0}};
+        jobs[t] = jb;
+        if (nthreads > 1) pthread_create(&th[t], NULL, path_worker, &jobs[t]);
+    }
+    if (nthreads == 1) path_worker(&jobs[0]);
+    else for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    if (counters) {
+        counters[0] = counters[1] = counters[2] = 0;
+        for (int t = 0; t < nthreads; ++t)
+            for (int k = 0; k < 3; ++k) counters[k] += jobs[t].cnt[k];
+    }
+    free(jobs);
+    free(th);
+}

@@ -107,6 +107,16 @@ void orc_render_shadow(const orc_node* nodes, uint32_t n, const float* tris, con
                        uint32_t w, uint32_t h, uint32_t spp, const float light[3], float ambient,
                        orc_hit* hits, uint8_t* rgba, uint64_t counters[2], int nthreads);
 
+/* Path mode [SPEC, DESIGN.md "Path mode"; SURVEY.md §8(f) row 3]: diffuse
+ * paths of 1 + max_depth segments with next-event estimation toward the point
+ * light and sky radiance `sky` for escaped bounce rays.  hits (nullable): the
+ * primary hits.  counters (nullable): [0] nodes fetched, [1] tris tested,
+ * [2] rays traced (primary + bounce + shadow).  Rows interleaved over
+ * nthreads POSIX threads. */
+void orc_render_path(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* cam,
+                     uint32_t w, uint32_t h, uint32_t spp, const float light[3], float sky, uint32_t max_depth,
+                     orc_hit* hits, uint8_t* rgba, uint64_t counters[3], int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

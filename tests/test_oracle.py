@@ -187,3 +187,59 @@ def test_trace_row_sampling_and_threads(oracle):
     s = sub.reshape(30, 40)
     assert np.array_equal(bits(f["t"][1::3]), bits(s["t"][1::3]))
     assert c_sub[0] < c_full[0]
+
+
+def _secondary_scenes(oracle):
+    from gpu_raytracer_amd import scenes as S
+    return [(np.ascontiguousarray(S.cornell_tris(), np.float32).reshape(-1, 9), S.CORNELL_VIEW, S.LIGHTS["cornell"], 24),
+            (oracle.soup(3000, 41).reshape(-1, 9), S.SOUP_VIEW, S.LIGHTS["soup"], 24)]
+
+
+def test_shadow_oracle_vs_numpy_restatement(oracle):
+    """Shadow mode: the C oracle and the independent wavefront
+    numpy restatement agree bit for bit."""
+    from oracle import oracle_np as NP
+    for tris, V, light, w in _secondary_scenes(oracle):
+        cam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, w, w)
+        b = oracle.build(tris)
+        eh, er, _ = oracle.render_shadow(b["nodes"], tris, cam, w, w, 2, light, 0.2)
+        t, u, v, p, rgba = NP.render_shadow(NP.build(tris), tris, cam.as_array(), w, w, 2, light, 0.2)
+        assert np.array_equal(eh["prim"], p) and np.array_equal(bits(eh["t"]), bits(t))
+        assert np.array_equal(er, rgba)
+
+
+@pytest.mark.parametrize("depth", [0, 1, 3])
+def test_path_oracle_vs_numpy_restatement(oracle, depth):
+    """Path mode: the C oracle (per-pixel recursion) and the numpy
+    restatement (a wavefront over all live paths) agree bit for bit, ray
+    count included."""
+    from oracle import oracle_np as NP
+    for tris, V, light, w in _secondary_scenes(oracle):
+        cam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, w, w)
+        b = oracle.build(tris)
+        eh, er, cnt = oracle.render_path(b["nodes"], tris, cam, w, w, 2, light, 0.3, depth, nthreads=3)
+        t, u, v, p, rgba, nrays = NP.render_path(NP.build(tris), tris, cam.as_array(), w, w, 2, light, 0.3, depth)
+        assert np.array_equal(eh["prim"], p) and np.array_equal(bits(eh["t"]), bits(t))
+        assert np.array_equal(er, rgba)
+        assert int(cnt[2]) == nrays
+        assert nrays > w * w * 2
+
+
+def test_path_oracle_properties(oracle):
+    """Thread-count independence; more sky or more bounces never darkens a
+    pixel (every term is non-negative); depth 0 ignores the sky."""
+    from gpu_raytracer_amd import scenes as S
+    tris = np.ascontiguousarray(S.cornell_tris(), np.float32).reshape(-1, 9)
+    V, light = S.CORNELL_VIEW, S.LIGHTS["cornell"]
+    cam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, 40, 40)
+    b = oracle.build(tris)
+    _, a1, c1 = oracle.render_path(b["nodes"], tris, cam, 40, 40, 2, light, 0.2, 2, nthreads=1)
+    _, a4, c4 = oracle.render_path(b["nodes"], tris, cam, 40, 40, 2, light, 0.2, 2, nthreads=4)
+    assert np.array_equal(a1, a4) and np.array_equal(c1, c4)
+    _, dark, _ = oracle.render_path(b["nodes"], tris, cam, 40, 40, 2, light, 0.0, 2)
+    _, bright, _ = oracle.render_path(b["nodes"], tris, cam, 40, 40, 2, light, 1.0, 2)
+    assert (bright >= dark).all() and (bright > dark).any()
+    _, d0a, _ = oracle.render_path(b["nodes"], tris, cam, 40, 40, 2, light, 0.0, 0)
+    _, d0b, _ = oracle.render_path(b["nodes"], tris, cam, 40, 40, 2, light, 1.0, 0)
+    assert np.array_equal(d0a, d0b)
+    assert (dark >= d0a).all()
