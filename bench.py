@@ -133,7 +133,8 @@ def path_tracing(R, S, scene, cfg, cam, w, h, spp, img, args, torch, dev):
     torch.cuda.synchronize(dev)
     work = scene.render_path_work(cam, w, h, spp, light, PATH_SKY, PATH_DEPTH)
     med = float(np.median(ms))
-    return {"mode": f"diffuse path tracing, max_depth {PATH_DEPTH}, next-event shadow rays (DESIGN.md)",
+    return {"mode": f"diffuse path tracing, max_depth {PATH_DEPTH}, next-event shadow rays (DESIGN.md); "
+                    "wavefront schedule, unsorted ray queues (the default)",
             "light": list(light), "sky": PATH_SKY, "ms": round(med, 4), "rays": int(work[2]),
             "rays_per_pixel": round(int(work[2]) / (w * h * spp), 3),
             "mrays_per_s": round(int(work[2]) / (med * 1e-3) / 1e6, 2),

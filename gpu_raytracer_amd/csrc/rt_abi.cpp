@@ -39,6 +39,7 @@ struct rt_scene {
     size_t rgba_cap = 0;
     unsigned long long* d_ctr = nullptr;
     uint32_t* d_work = nullptr;  // pool-trace unit counters
+    rt::PathBufs path;           // wavefront path-mode state (grown on demand)
     hipEvent_t r0 = nullptr, r1 = nullptr;
 };
 
@@ -142,6 +143,10 @@ rt_status rt_config_set(const char* key, int64_t value) {
     else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
+    else if (k == "path.wavefront" && (value == 0 || value == 1)) rt::g_trace_config.path_wave = (uint32_t)value;
+    else if (k == "path.wg" && (value == 64 || value == 256)) rt::g_trace_config.path_wg = (uint32_t)value;
+    else if (k == "path.sort" && value >= 0 && value <= 4) rt::g_trace_config.path_sort = (uint32_t)value;
+    else if (k == "path.batch" && value >= 0 && value <= (1 << 28)) rt::g_trace_config.path_batch = (uint32_t)value;
     else return fail(RT_EINVAL, "unknown config key or value out of range: " + k);
     return RT_OK;
 }
@@ -232,6 +237,7 @@ void rt_scene_free(rt_scene* s) {
         (void)hipSetDevice(s->device);
         (void)hipStreamSynchronize(s->stream);
         rt::free_build(s->bufs);
+        rt::free_path(s->path);
         if (s->d_hits) (void)hipFree(s->d_hits);
         if (s->d_rgba) (void)hipFree(s->d_rgba);
         if (s->d_ctr) (void)hipFree(s->d_ctr);
@@ -543,6 +549,37 @@ rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float l
     return RT_OK;
 }
 
+// Path mode: the megakernel, or the wavefront schedule with ray reordering
+// (config path.wavefront); the wavefront reads each depth's queue length back
+// to the host, so it synchronizes the stream between depths.
+static rt_status path_launch(rt_scene* s, const rt_camera* cam, const float light[3], float sky, uint32_t max_depth,
+                             uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
+                             unsigned long long* ctr, hipStream_t hs) {
+    hipError_t e;
+    if (rt::g_trace_config.path_wave) {
+        const uint64_t per_tile = 256ull * spp;
+        const uint64_t tiles = rt::tiles_for_rank(w, h, 0, 1);
+        const uint64_t want = rt::g_trace_config.path_batch ? rt::g_trace_config.path_batch : (1u << 22);
+        uint64_t cap = std::min<uint64_t>(tiles * per_tile, std::max<uint64_t>(per_tile, want / per_tile * per_tile));
+        if (cap > (1u << 30)) return fail(RT_EINVAL, "path batch exceeds 2^30 paths (lower spp or path.batch)");
+        if (s->path.cap < cap) {
+            if ((e = rt::alloc_path(s->path, (uint32_t)cap)) != hipSuccess) {
+                rt::free_path(s->path);
+                return hip_fail(e, "alloc_path");
+            }
+        }
+        e = rt::launch_path_wavefront(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->bufs.params, s->n,
+                                      camf(cam), w, h, spp, light, sky, max_depth, d_hits, d_rgba, ctr, s->path,
+                                      rt::g_trace_config.path_sort, hs);
+        if (e != hipSuccess) return hip_fail(e, "launch_path_wavefront");
+        return RT_OK;
+    }
+    e = rt::launch_trace_path(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam), w, h, spp,
+                              light, sky, max_depth, d_hits, d_rgba, ctr, hs);
+    if (e != hipSuccess) return hip_fail(e, "launch_trace_path");
+    return RT_OK;
+}
+
 rt_status rt_render_path_device(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
                                 uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
                                 void* stream, double* ms_out) {
@@ -554,9 +591,7 @@ rt_status rt_render_path_device(rt_scene* s, const rt_camera* cam, const float l
     if (st) return st;
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace_path(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
-                                         w, h, spp, light, sky, max_depth, d_hits, d_rgba, nullptr, hs);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace_path");
+    if ((st = path_launch(s, cam, light, sky, max_depth, w, h, spp, d_hits, d_rgba, nullptr, hs))) return st;
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
         HIPR(hipEventSynchronize(s->r1));
@@ -595,9 +630,7 @@ rt_status rt_render_path_work(rt_scene* s, const rt_camera* cam, const float lig
     if (st) return st;
     if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 32, s->stream));
-    hipError_t e = rt::launch_trace_path(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
-                                         w, h, spp, light, sky, max_depth, nullptr, nullptr, s->d_ctr, s->stream);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace_path");
+    if ((st = path_launch(s, cam, light, sky, max_depth, w, h, spp, nullptr, nullptr, s->d_ctr, s->stream))) return st;
     HIPR(hipStreamSynchronize(s->stream));
     HIPR(hipMemcpy(counters_out, s->d_ctr, 24, hipMemcpyDeviceToHost));
     return RT_OK;

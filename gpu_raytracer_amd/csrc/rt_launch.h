@@ -80,6 +80,10 @@ struct TraceConfig {
     uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
     uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
     uint32_t stack_cap = 14;    // wide stack entries used, <= kWideStack (tests force the overflow path)
+    uint32_t path_wave = 1;     // path mode: 0 megakernel, 1 wavefront (default: faster on soup-1M and Sponza)
+    uint32_t path_wg = 64;      // path megakernel: threads per block (64 = 8x8 quadrant, 256 = 16x16 tile)
+    uint32_t path_sort = 0;     // wavefront: top key bytes the ray queue is sorted by (0 = unsorted, default)
+    uint32_t path_batch = 0;    // wavefront: paths per batch (0 = 4M)
 };
 extern TraceConfig g_trace_config;
 
@@ -103,6 +107,34 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float
                              uint32_t n, const CamF& cam, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
                              float sky, uint32_t max_depth, void* hits, void* rgba, unsigned long long* counters,
                              hipStream_t s);
+// Wavefront path mode (same images as launch_trace_path): per-path state in
+// SoA arrays, a ray queue per depth, optionally sorted by a coherence key.
+struct PathBufs {
+    uint32_t cap = 0;               // paths per batch (a multiple of 256*spp is used)
+    float* f = nullptr;             // [16][cap] o(3) d(3) L(3) beta(3) w(3) seg_t
+    uint32_t* u = nullptr;          // [4][cap] rng state, flags, seg_prim, shadow visibility
+    float4* rays = nullptr;         // [2*cap][2] {o, tmax}, {d, pid | shadow << 31}
+    uint32_t* keys[2] = {nullptr, nullptr};  // [2*cap] ray coherence keys (ping-pong)
+    uint32_t* vals[2] = {nullptr, nullptr};  // [2*cap] queue slots (ping-pong)
+    uint32_t* counts = nullptr;     // [tiles(2*cap)][256] sort tile counts
+    uint32_t* ghist = nullptr;      // [4][256] digit histograms of the keys
+    uint32_t* qcount = nullptr;     // queue length (device word)
+    uint32_t* hq = nullptr;         // pinned host copy of qcount
+};
+hipError_t alloc_path(PathBufs& b, uint32_t cap);
+void free_path(PathBufs& b);
+// sort_digits: 0 = trace the queue in emission order; 1..4 = stable LSB radix
+// sort of the queue by the top `sort_digits` bytes of the ray key first.
+hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+                                 const BuildParams* params, uint32_t n, const CamF& cam, uint32_t w, uint32_t h,
+                                 uint32_t spp, const float light[3], float sky, uint32_t max_depth, void* hits,
+                                 void* rgba, unsigned long long* counters, PathBufs& pb, uint32_t sort_digits,
+                                 hipStream_t s);
+// top `digits` (1..4) bytes of 32-bit keys, stable; returns the buffer index
+// (0 or 1) holding the result.  counts: tiles(n)*256 words; ghist: [4][256]
+// totals of all four digits (launch_digit_hist).
+hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
+                           uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
                          void* img, hipStream_t s);
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);

@@ -305,4 +305,29 @@ hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const u
     return hipGetLastError();
 }
 
+hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
+                           uint32_t digits, uint32_t* out_buf, hipStream_t s) {
+    *out_buf = 0;
+    if (n <= 1 || !digits) return hipSuccess;
+    if (digits > 4) digits = 4;
+    const uint32_t nt = sort_tiles(n);
+    uint32_t src = 0;
+    for (uint32_t dgt = 4 - digits; dgt < 4; ++dgt, src ^= 1u) {
+        const uint32_t dst = src ^ 1u;
+        switch (dgt) {
+#define RT_SORT_PASS(SH)                                                                                            \
+    hipLaunchKernelGGL(k_tile_hist<SH>, dim3(nt), dim3(kSortThreads), 0, s, keys[src], n, counts);                 \
+    scatter_pass<SH>(keys[src], vals[src], keys[dst], vals[dst], n, ghist + 256 * (SH / 8), counts, s);          \
+    break
+            case 0: RT_SORT_PASS(0);
+            case 1: RT_SORT_PASS(8);
+            case 2: RT_SORT_PASS(16);
+            default: RT_SORT_PASS(24);
+#undef RT_SORT_PASS
+        }
+    }
+    *out_buf = src;
+    return hipGetLastError();
+}
+
 }  // namespace rt

@@ -326,6 +326,10 @@ __device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const 
     tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
 }
 
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
 
 // Shading frame of a hit (shadow and path modes): P = o + t d,
@@ -654,6 +658,261 @@ __global__ __launch_bounds__(NT) void k_path(const void* __restrict__ nodes, con
     }
 }
 
+// ------------------------------------------------------ path mode, wavefront
+// The same paths as k_path, advanced depth by depth over all paths of a batch
+// ("ray reordering"): k_pw_primary traces the
+// primary rays tile by tile; k_pw_shade turns every path's pending results
+// into its next rays (shadow ray and/or bounce), appended to a queue with one
+// atomic per 1024-thread block; the queue is sorted by a coherence key (ray
+// kind, direction octant, Morton code of the origin in the scene's centroid
+// box); k_pw_trace traces the sorted queue, one ray per lane, so a wave's
+// rays start close together and head the same way.  Each path's arithmetic
+// is k_path's in the same order -- shadow result of depth k before the
+// segment of depth k+1 -- so the image is bit-identical whatever the queue
+// order (the numpy restatement in oracle/oracle_np.py is this schedule).
+enum : uint32_t { kPfO = 0, kPfD = 3, kPfL = 6, kPfB = 9, kPfW = 12, kPfT = 15, kPathF = 16 };
+enum : uint32_t { kPuSt = 0, kPuFl = 1, kPuPrim = 2, kPuVis = 3, kPathU = 4 };
+enum : uint32_t { kFlShadow = 1, kFlSeg = 2 };
+
+__device__ __forceinline__ uint32_t ray_key(const float* o, const float* d, bool shadow, const BuildParams& bp) {
+    uint32_t q[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) q[a] = (uint32_t)fminf(fmaxf((o[a] - bp.lo[a]) * bp.inv[a] * 512.0f, 0.0f), 511.0f);
+    const uint32_t m = (expand10(q[0]) << 2) | (expand10(q[1]) << 1) | expand10(q[2]);
+    const uint32_t oct = (d[0] < 0.0f ? 1u : 0u) | (d[1] < 0.0f ? 2u : 0u) | (d[2] < 0.0f ? 4u : 0u);
+    return (shadow ? 1u << 30 : 0u) | (oct << 27) | m;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_pw_primary(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                                     uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
+                                                     Cam cam, uint32_t W, uint32_t H, uint32_t spp, uint32_t tilesX,
+                                                     uint32_t t0, float* __restrict__ pf, uint32_t* __restrict__ pu,
+                                                     uint32_t cap, float4* __restrict__ hits,
+                                                     unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
+    __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
+    const uint32_t t = t0 + blockIdx.x;
+    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t lx = (wv & 1) * 8 + (l & 7), ly = (wv >> 1) * 8 + (l >> 3);
+    const uint32_t x = (t % tilesX) * 16 + lx, y = (t / tilesX) * 16 + ly;
+    const uint32_t pbase = (blockIdx.x * 256 + ly * 16 + lx) * spp;
+    uint32_t cn = 0, ct = 0;
+    const bool valid = x < W && y < H;
+    for (uint32_t s = 0; s < spp; ++s) {
+        const uint32_t pid = pbase + s;
+        if (!valid) { pu[kPuFl * cap + pid] = 0u; continue; }
+        const uint32_t sidx = (y * W + x) * spp + s;
+        float d[3], tb, hu, hv;
+        uint32_t hp;
+        ray_dir(cam, x, y, W, spp, s, d);
+        trace_gen<COUNT, 256>(reinterpret_cast<const char*>(nodes), wnodes, wcap, tri_s, n, cam.eye, d,
+                              __builtin_inff(), false, s_ref + threadIdx.x, s_tn + threadIdx.x, tb, hu, hv, hp, cn, ct);
+        if (hits) hits[sidx] = make_float4(tb, hu, hv, __uint_as_float(hp));
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            pf[(kPfO + a) * cap + pid] = cam.eye[a];
+            pf[(kPfD + a) * cap + pid] = d[a];
+            pf[(kPfL + a) * cap + pid] = 0.0f;
+            pf[(kPfB + a) * cap + pid] = 1.0f;
+        }
+        pf[kPfT * cap + pid] = tb;
+        pu[kPuSt * cap + pid] = pcg_hash(sidx ^ 0x5bd1e995u);
+        pu[kPuFl * cap + pid] = kFlSeg;
+        pu[kPuPrim * cap + pid] = hp;
+    }
+    if (COUNT) {
+        unsigned long long a = cn, bsum = ct, c = valid ? spp : 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            bsum += __shfl_xor(bsum, off, 64);
+            c += __shfl_xor(c, off, 64);
+        }
+        if (l == 0) {
+            atomicAdd(&counters[0], a);
+            atomicAdd(&counters[1], bsum);
+            atomicAdd(&counters[2], c);
+        }
+    }
+}
+
+// One path's step at `depth`: the pending shadow result of depth-1, then the
+// pending segment of depth; emits the path's next rays into the queue.
+__global__ __launch_bounds__(1024) void k_pw_shade(float* __restrict__ pf, uint32_t* __restrict__ pu, uint32_t cap,
+                                                   uint32_t np, uint32_t depth, PathCfg pc,
+                                                   const float* __restrict__ tris,
+                                                   const BuildParams* __restrict__ params,
+                                                   float4* __restrict__ rays, uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals, uint32_t* __restrict__ qcount) {
+    __shared__ uint32_t s_wave[16];
+    __shared__ uint32_t s_base;
+    const uint32_t pid = blockIdx.x * 1024 + threadIdx.x;
+    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t fl = pid < np ? pu[kPuFl * cap + pid] : 0u;
+    bool emit_sh = false, emit_bo = false;
+    float S[3], D[3], nd[3];
+    if (fl) {
+        float L[3], beta[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { L[a] = pf[(kPfL + a) * cap + pid]; beta[a] = pf[(kPfB + a) * cap + pid]; }
+        if ((fl & kFlShadow) && pu[kPuVis * cap + pid]) {
+#pragma unroll
+            for (int a = 0; a < 3; ++a) L[a] = L[a] + pf[(kPfW + a) * cap + pid];
+        }
+        if (fl & kFlSeg) {
+            const uint32_t prim = pu[kPuPrim * cap + pid];
+            if (prim == RT_SENT) {
+                if (depth > 0) {
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) L[a] = L[a] + beta[a] * pc.sky;
+                }
+            } else {
+                float o[3], d[3], alb[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) { o[a] = pf[(kPfO + a) * cap + pid]; d[a] = pf[(kPfD + a) * cap + pid]; }
+                Surf f;
+                surface(tris, prim, o, d, pf[kPfT * cap + pid], pc.light, f);
+                const uint32_t ha = pcg_hash(prim ^ 0x27d4eb2fu);
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    alb[a] = 0.25f + (float)((ha >> (8 * a)) & 0xFFu) * 0x1p-9f;
+                    S[a] = f.S[a];
+                    D[a] = f.D[a];
+                }
+                if (f.cosl > 0.0f) {
+                    emit_sh = true;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) pf[(kPfW + a) * cap + pid] = (beta[a] * alb[a]) * f.cosl;
+                }
+                if (depth < pc.max_depth) {
+                    emit_bo = true;
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) beta[a] = beta[a] * alb[a];
+                    uint32_t st = pu[kPuSt * cap + pid];
+                    float px = 0.0f, py = 0.0f, r2 = 0.0f;
+                    for (int k = 0; k < 16; ++k) {
+                        const float qx = path_u01(st) * 2.0f - 1.0f;
+                        const float qy = path_u01(st) * 2.0f - 1.0f;
+                        const float q2 = qx * qx + qy * qy;
+                        if (q2 < 1.0f) { px = qx; py = qy; r2 = q2; break; }
+                    }
+                    pu[kPuSt * cap + pid] = st;
+                    const float* N = f.N;
+                    const float z = sqrtf(1.0f - r2);
+                    const float sg = N[2] >= 0.0f ? 1.0f : -1.0f;
+                    const float ia = -1.0f / (sg + N[2]);
+                    const float ib = (N[0] * N[1]) * ia;
+                    const float T[3] = {1.0f + ((sg * N[0]) * N[0]) * ia, sg * ib, -(sg * N[0])};
+                    const float B[3] = {ib, sg + (N[1] * N[1]) * ia, -N[1]};
+#pragma unroll
+                    for (int a = 0; a < 3; ++a) {
+                        nd[a] = (px * T[a] + py * B[a]) + z * N[a];
+                        pf[(kPfO + a) * cap + pid] = S[a];
+                        pf[(kPfD + a) * cap + pid] = nd[a];
+                        pf[(kPfB + a) * cap + pid] = beta[a];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < 3; ++a) pf[(kPfL + a) * cap + pid] = L[a];
+        pu[kPuFl * cap + pid] = (emit_sh ? kFlShadow : 0u) | (emit_bo ? kFlSeg : 0u);
+    }
+    // queue slots: wave ballots, a block scan over the 16 waves, one atomic
+    const uint64_t bs = __ballot(emit_sh), bb = __ballot(emit_bo);
+    const uint32_t nsh = (uint32_t)__popcll(bs), nw = nsh + (uint32_t)__popcll(bb);
+    if (l == 0) s_wave[wv] = nw;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int k = 0; k < 16; ++k) { const uint32_t c = s_wave[k]; s_wave[k] = tot; tot += c; }
+        s_base = tot ? atomicAdd(qcount, tot) : 0u;
+    }
+    __syncthreads();
+    const uint32_t wbase = s_base + s_wave[wv];
+    const BuildParams bp = *params;
+    if (emit_sh) {
+        const uint32_t slot = wbase + lanes_below(bs);
+        rays[2 * (uint64_t)slot] = make_float4(S[0], S[1], S[2], 1.0f);
+        rays[2 * (uint64_t)slot + 1] = make_float4(D[0], D[1], D[2], __uint_as_float(pid | 0x80000000u));
+        keys[slot] = ray_key(S, D, true, bp);
+        vals[slot] = slot;
+    }
+    if (emit_bo) {
+        const uint32_t slot = wbase + nsh + lanes_below(bb);
+        rays[2 * (uint64_t)slot] = make_float4(S[0], S[1], S[2], __builtin_inff());
+        rays[2 * (uint64_t)slot + 1] = make_float4(nd[0], nd[1], nd[2], __uint_as_float(pid));
+        keys[slot] = ray_key(S, nd, false, bp);
+        vals[slot] = slot;
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(256) void k_pw_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                                   uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
+                                                   const float4* __restrict__ rays, const uint32_t* __restrict__ order,
+                                                   uint32_t count, const uint32_t* __restrict__ count_dev,
+                                                   float* __restrict__ pf, uint32_t* __restrict__ pu,
+                                                   uint32_t cap, unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
+    __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
+    if (count_dev) count = *count_dev;  // grid sized for the bound, queue length read here
+    if (blockIdx.x * 256 >= count) return;
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    uint32_t cn = 0, ct = 0;
+    if (i < count) {
+        const uint32_t r = order ? order[i] : i;
+        const float4 A = rays[2 * (uint64_t)r], B = rays[2 * (uint64_t)r + 1];
+        const float o[3] = {A.x, A.y, A.z}, d[3] = {B.x, B.y, B.z};
+        const uint32_t tag = __float_as_uint(B.w), pid = tag & 0x7FFFFFFFu;
+        const bool shadow = tag >> 31;
+        float tb, hu, hv;
+        uint32_t hp;
+        trace_gen<COUNT, 256>(reinterpret_cast<const char*>(nodes), wnodes, wcap, tri_s, n, o, d, A.w, shadow,
+                              s_ref + threadIdx.x, s_tn + threadIdx.x, tb, hu, hv, hp, cn, ct);
+        if (shadow) {
+            pu[kPuVis * cap + pid] = hp == RT_SENT ? 1u : 0u;
+        } else {
+            pf[kPfT * cap + pid] = tb;
+            pu[kPuPrim * cap + pid] = hp;
+        }
+    }
+    if (COUNT) {
+        unsigned long long a = cn, bsum = ct, c = i < count ? 1u : 0u;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            a += __shfl_xor(a, off, 64);
+            bsum += __shfl_xor(bsum, off, 64);
+            c += __shfl_xor(c, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&counters[0], a);
+            atomicAdd(&counters[1], bsum);
+            atomicAdd(&counters[2], c);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pw_finish(const float* __restrict__ pf, uint32_t cap, uint32_t W, uint32_t H,
+                                                   uint32_t spp, uint32_t tilesX, uint32_t t0,
+                                                   uint32_t* __restrict__ rgba) {
+    const uint32_t t = t0 + blockIdx.x;
+    const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t lx = (wv & 1) * 8 + (l & 7), ly = (wv >> 1) * 8 + (l >> 3);
+    const uint32_t x = (t % tilesX) * 16 + lx, y = (t / tilesX) * 16 + ly;
+    if (x >= W || y >= H) return;
+    const uint32_t pbase = (blockIdx.x * 256 + ly * 16 + lx) * spp;
+    float r = 0.0f, g = 0.0f, b = 0.0f;
+    for (uint32_t s = 0; s < spp; ++s) {
+        r = r + pf[(kPfL + 0) * cap + pbase + s];
+        g = g + pf[(kPfL + 1) * cap + pbase + s];
+        b = b + pf[(kPfL + 2) * cap + pbase + s];
+    }
+    const float sc = 1.0f / (float)spp;
+    rgba[(uint64_t)y * W + x] = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+}
+
 // ---------------------------------------------------------------- pool
 // Wide traversal with per-lane refill.  The rank's tiles are cut into 8x8
 // units (unit u = quarter u%4 of tile slot u/4), dealt to the waves of a
@@ -663,10 +922,6 @@ __global__ __launch_bounds__(NT) void k_path(const void* __restrict__ nodes, con
 // then of its next unit, so the wave no longer idles behind its slowest ray
 // until its very last unit.  A lane owns a whole pixel (its spp samples in
 // order), which keeps the §9.7 per-pixel sample average sequential.
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
 template <bool COUNT, bool PACKED>
 __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
@@ -964,7 +1219,7 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float
     // K7w records unless the binary traversal is asked for (variant 2)
     const uint4* wn = (g_trace_config.variant != 2) ? wnodes : nullptr;
     const uint32_t cap = g_trace_config.stack_cap;
-    const bool small = g_trace_config.wg == 64;
+    const bool small = g_trace_config.path_wg == 64;
 #define RT_PATH(C, NT)                                                                                            \
     hipLaunchKernelGGL((k_path<C, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, cam, \
                        w, h, spp, tilesX, pc, H, R, counters)
@@ -974,6 +1229,110 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float
         if (small) RT_PATH(false, 64); else RT_PATH(false, 256);
     }
 #undef RT_PATH
+    return hipGetLastError();
+}
+
+hipError_t alloc_path(PathBufs& b, uint32_t cap) {
+    free_path(b);
+    const uint64_t q = 2ull * cap;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&b.f, (uint64_t)kPathF * cap * 4)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&b.u, (uint64_t)kPathU * cap * 4)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&b.rays, q * 32)) != hipSuccess) return e;
+    for (int i = 0; i < 2; ++i) {
+        if ((e = hipMalloc((void**)&b.keys[i], q * 4)) != hipSuccess) return e;
+        if ((e = hipMalloc((void**)&b.vals[i], q * 4)) != hipSuccess) return e;
+    }
+    if ((e = hipMalloc((void**)&b.counts, (uint64_t)sort_tiles((uint32_t)q) * 256 * 4 + 1024)) != hipSuccess) return e;
+    if ((e = hipMalloc((void**)&b.ghist, 4096 + 256)) != hipSuccess) return e;
+    b.qcount = b.ghist + 1024;
+    if ((e = hipHostMalloc((void**)&b.hq, 256, hipHostMallocDefault)) != hipSuccess) return e;
+    b.cap = cap;
+    return hipSuccess;
+}
+
+void free_path(PathBufs& b) {
+    (void)hipFree(b.f);
+    (void)hipFree(b.u);
+    (void)hipFree(b.rays);
+    for (int i = 0; i < 2; ++i) { (void)hipFree(b.keys[i]); (void)hipFree(b.vals[i]); }
+    (void)hipFree(b.counts);
+    (void)hipFree(b.ghist);
+    if (b.hq) (void)hipHostFree(b.hq);
+    b = PathBufs{};
+}
+
+hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+                                 const BuildParams* params, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
+                                 uint32_t spp, const float light[3], float sky, uint32_t max_depth, void* hits,
+                                 void* rgba, unsigned long long* counters, PathBufs& pb, uint32_t sort_digits,
+                                 hipStream_t s) {
+    const uint32_t nt = tiles_for_rank(w, h, 0, 1);
+    if (!nt) return hipSuccess;
+    const uint32_t per_tile = 256 * spp;
+    if (pb.cap < per_tile) return hipErrorInvalidValue;
+    Cam cam;
+    for (int i = 0; i < 3; ++i) {
+        cam.eye[i] = c.eye[i]; cam.w00[i] = c.w00[i]; cam.du[i] = c.du[i]; cam.dv[i] = c.dv[i];
+    }
+    PathCfg pc;
+    for (int i = 0; i < 3; ++i) pc.light[i] = light[i];
+    pc.sky = sky;
+    pc.max_depth = max_depth;
+    const uint32_t tilesX = (w + 15) / 16;
+    const uint4* wn = (g_trace_config.variant != 2) ? wnodes : nullptr;
+    const uint32_t wcap = g_trace_config.stack_cap;
+    const uint32_t batch = pb.cap / per_tile;
+    float4* H = reinterpret_cast<float4*>(hits);
+    hipError_t e;
+    for (uint32_t t0 = 0; t0 < nt; t0 += batch) {
+        const uint32_t nb = min(batch, nt - t0);
+        const uint32_t np = nb * per_tile;
+        if (counters)
+            hipLaunchKernelGGL(k_pw_primary<true>, dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h, spp,
+                               tilesX, t0, pb.f, pb.u, pb.cap, H, counters);
+        else
+            hipLaunchKernelGGL(k_pw_primary<false>, dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h,
+                               spp, tilesX, t0, pb.f, pb.u, pb.cap, H, counters);
+        for (uint32_t depth = 0; depth <= max_depth + 1; ++depth) {
+            if ((e = hipMemsetAsync(pb.qcount, 0, 4, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_pw_shade, dim3((np + 1023) / 1024), dim3(1024), 0, s, pb.f, pb.u, pb.cap, np, depth,
+                               pc, tris, params, pb.rays, pb.keys[0], pb.vals[0], pb.qcount);
+            if (depth == max_depth + 1) break;  // only the last shadow results were left to apply
+            uint32_t count = 0, grid = 0;
+            const uint32_t* order = nullptr;
+            const uint32_t* count_dev = nullptr;
+            if (sort_digits) {  // the sort needs the queue length on the host
+                if ((e = hipMemcpyAsync(pb.hq, pb.qcount, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+                if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+                count = *pb.hq;
+                if (!count) break;  // every path has ended
+                grid = (count + 255) / 256;
+                if (count > 1) {
+                    if ((e = hipMemsetAsync(pb.ghist, 0, 4096, s)) != hipSuccess) return e;
+                    if ((e = launch_digit_hist(pb.keys[0], count, pb.ghist, s)) != hipSuccess) return e;
+                    uint32_t ob = 0;
+                    if ((e = launch_sort_top(pb.keys, pb.vals, count, pb.ghist, pb.counts, sort_digits, &ob, s)) !=
+                        hipSuccess)
+                        return e;
+                    order = pb.vals[ob];
+                }
+            } else {  // no host round trip: blocks past the queue length exit at once
+                count_dev = pb.qcount;
+                grid = (2 * np + 255) / 256;
+            }
+            if (counters)
+                hipLaunchKernelGGL(k_pw_trace<true>, dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays,
+                                   order, count, count_dev, pb.f, pb.u, pb.cap, counters);
+            else
+                hipLaunchKernelGGL(k_pw_trace<false>, dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays,
+                                   order, count, count_dev, pb.f, pb.u, pb.cap, counters);
+        }
+        if (rgba)
+            hipLaunchKernelGGL(k_pw_finish, dim3(nb), dim3(256), 0, s, pb.f, pb.cap, w, h, spp, tilesX, t0,
+                               reinterpret_cast<uint32_t*>(rgba));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 

@@ -203,7 +203,14 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * grid, 2 = one thread per pixel, binary traversal; "trace.blocks" variant-1
  * grid (0 = resident capacity); "trace.stack_cap" (1..14) wide-traversal
  * stack entries -- rays that need more are re-traced by the binary
- * traversal.  Results are bit-identical for every setting. */
+ * traversal; "trace.wg" 64/256 threads per block (8x8 quadrant / 16x16
+ * tile).  Path mode: "path.wavefront" 0 = megakernel ("path.wg" 64/256
+ * threads per block), 1 = wavefront schedule with per-depth ray queues
+ * (default); "path.sort" 0..4 = top key bytes each queue is radix-sorted by
+ * for coherence (ray kind, direction octant, Morton code of the origin; 0 =
+ * unsorted, the default; sorting reads each queue length back to the host);
+ * "path.batch" paths per wavefront batch (0 = 4M).  Results are
+ * bit-identical for every setting. */
 rt_status rt_config_set(const char* key, int64_t value);
 
 const char* rt_last_error(void);

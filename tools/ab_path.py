@@ -22,20 +22,31 @@ s.build()
 V, light = S.VIEWS[scene], S.LIGHTS[scene]
 cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
-variants = [("wide, 256-thread tiles", {"trace.variant": 0, "trace.wg": 256}),
-            ("wide, 64-thread quadrants", {"trace.variant": 0, "trace.wg": 64}),
-            ("binary, 256-thread tiles", {"trace.variant": 2, "trace.wg": 256})]
+def cfg(variant=0, wg=256, wave=0, sort=0):
+    return {"trace.variant": variant, "path.wg": wg, "path.wavefront": wave, "path.sort": sort}
+
+
+variants = [("mega wide, 256-thread tiles", cfg()),
+            ("mega wide, 64-thread quadrants", cfg(wg=64)),
+            ("mega binary, 256-thread tiles", cfg(variant=2)),
+            ("wavefront wide, unsorted", cfg(wave=1, sort=0)),
+            ("wavefront wide, sort 1 byte", cfg(wave=1, sort=1)),
+            ("wavefront wide, sort 2 bytes", cfg(wave=1, sort=2)),
+            ("wavefront wide, sort 3 bytes", cfg(wave=1, sort=3)),
+            ("wavefront wide, sort 4 bytes", cfg(wave=1, sort=4))]
+if len(sys.argv) > 4:
+    variants = [variants[int(i)] for i in sys.argv[4].split(",")]
 rays = {}
-for name, cfg in variants:
-    for k, v in cfg.items():
+for name, c in variants:
+    for k, v in c.items():
         R.config_set(k, v)
     rays[name] = [int(c) for c in s.render_path_work(cam, w, h, spp, light, 0.3, depth)]
     print(name, "work (node records, tri records, rays):", rays[name])
 ref = None
 times = {name: [] for name, _ in variants}
 for r in range(rounds):
-    for name, cfg in variants:
-        for k, v in cfg.items():
+    for name, c in variants:
+        for k, v in c.items():
             R.config_set(k, v)
         ms = [s.render_path_device(cam, w, h, spp, light, 0.3, depth, d_rgba=img.data_ptr(), timed=True)
               for _ in range(3)]
@@ -46,7 +57,7 @@ for r in range(rounds):
         assert np.array_equal(out, ref), name
 for name, _ in variants:
     t = np.array(times[name])
-    print(f"{scene} depth {depth} {name:<28s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  "
+    print(f"{scene} depth {depth} {name:<32s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  "
           f"rays {rays[name][2]}  -> {rays[name][2] / np.median(t) / 1e3:8.1f} Mrays/s")
-R.config_set("trace.variant", 0)
-R.config_set("trace.wg", 256)
+for k, v in {"trace.variant": 0, "path.wg": 64, "path.wavefront": 0, "path.sort": 0}.items():
+    R.config_set(k, v)
