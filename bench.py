@@ -221,7 +221,12 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, gather (ms)
+    # per-stage breakdown from one extra, untimed build with the stage events
+    # on (each adds a little to the GPU timeline, so the timed steps run without)
+    R.config_set("build.stage_events", 1)
+    stage_total_ms = scene.build()
     stimes = scene.build_times()
+    R.config_set("build.stage_events", 0)
 
     # max over ranks (per step), then mean over steps
     if world > 1:
@@ -284,7 +289,8 @@ def main():
             "frame_mrays_per_s": round(rays / (wall / args.steps) / 1e6, 2),
             "build_stages_ms_last": {"bounds": round(stimes.bounds, 4), "morton": round(stimes.morton, 4),
                                      "sort": round(stimes.sort, 4), "topology": round(stimes.topology, 4),
-                                     "refit": round(stimes.refit, 4), "wide": round(stimes.wide, 4)},
+                                     "refit": round(stimes.refit, 4), "wide": round(stimes.wide, 4),
+                                     "total_with_stage_events": round(stage_total_ms, 4)},
             "trace_counters_rank0": {"nodes_fetched": int(cnt[0]), "tris_tested": int(cnt[1]), "rays": rank_rays},
             "roofline": {"bound": "hbm", "kernel": "k_trace<wide>", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

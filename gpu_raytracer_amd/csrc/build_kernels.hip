@@ -1,10 +1,11 @@
 // build_kernels.hip -- BVH build hot path for gfx950.
 //
 //   K0 k_bounds         centroid bounds: 8 AoS triangles per thread as 18
-//                       independent 16-B loads, wave/LDS min-max, last-block
-//                       reduction (Guideline 16 release/ticket/acquire) ->
-//                       BuildParams {lo, hi, inv}.  Also zeroes the per-build
-//                       control words (digit histograms, crossing counters).
+//                       independent 16-B loads, wave/LDS min-max -> one
+//                       partial box per block (the second level runs inside
+//                       every K1 block -> BuildParams {lo, hi, inv}).  Also
+//                       zeroes the per-build control words (digit
+//                       histograms, crossing counters).
 //   K1 k_morton         Morton codes (§9.3); one block = one 4096-key sort tile,
 //                       so it also writes the tile's pass-0 digit counts and
 //                       adds the 4 global digit histograms (sort_kernels.hip).
@@ -74,11 +75,9 @@ __device__ __forceinline__ uint32_t load_tri8(const float* __restrict__ tris, ui
 
 // ---------------------------------------------------------------- K0
 __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, uint32_t n,
-                                                float* __restrict__ partials, uint32_t* ticket,
-                                                BuildParams* __restrict__ params,
+                                                float* __restrict__ partials,
                                                 uint32_t* __restrict__ zero_words, uint32_t nzero) {
     __shared__ float red[4][6];
-    __shared__ uint32_t s_last;
     for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nzero; j += gridDim.x * 256u) zero_words[j] = 0u;
 
     float lo[3], hi[3];
@@ -109,31 +108,23 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
         for (int c = 0; c < 3; ++c) { red[w][c] = lo[c]; red[w][3 + c] = hi[c]; }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float r[6];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            r[c] = fminf(fminf(red[0][c], red[1][c]), fminf(red[2][c], red[3][c]));
-            r[3 + c] = fmaxf(fmaxf(red[0][3 + c], red[1][3 + c]), fmaxf(red[2][3 + c], red[3][3 + c]));
-        }
-#pragma unroll
-        for (int c = 0; c < 6; ++c) partials[blockIdx.x * 6 + c] = r[c];
-        // Guideline 16 producer: release (write back L2), explicit wait, ticket.
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = (tk == gridDim.x - 1) ? 1u : 0u;
+    if (threadIdx.x < 6) {
+        const int c = threadIdx.x;
+        partials[blockIdx.x * 6 + c] = c < 3 ? fminf(fminf(red[0][c], red[1][c]), fminf(red[2][c], red[3][c]))
+                                             : fmaxf(fmaxf(red[0][c], red[1][c]), fmaxf(red[2][c], red[3][c]));
     }
-    __syncthreads();
-    if (!s_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
+}
+
+// Second level of K0, run by every block of its consumer (K1) instead of a
+// last-block ticket: the nb partial boxes (a few KB, L2-resident) reduced by
+// the whole block -- exact min/max, so every block gets the same result --
+// then §9.2 inv.  No device-scope fence or atomic on the critical path.
+template <int NT>
+__device__ __forceinline__ BuildParams bounds_final(const float* __restrict__ partials, uint32_t nb, float (*red)[6]) {
+    float lo[3], hi[3];
 #pragma unroll
     for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
-    for (uint32_t b = threadIdx.x; b < gridDim.x; b += 256) {
+    for (uint32_t b = threadIdx.x; b < nb; b += NT) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
             lo[c] = fminf(lo[c], partials[b * 6 + c]);
@@ -142,26 +133,34 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
     }
 #pragma unroll
     for (int c = 0; c < 3; ++c) { lo[c] = wave_min(lo[c]); hi[c] = wave_max(hi[c]); }
-    __syncthreads();
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     if (l == 0) {
 #pragma unroll
         for (int c = 0; c < 3; ++c) { red[w][c] = lo[c]; red[w][3 + c] = hi[c]; }
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        BuildParams p;
+    BuildParams p;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            p.lo[c] = fminf(fminf(red[0][c], red[1][c]), fminf(red[2][c], red[3][c]));
-            p.hi[c] = fmaxf(fmaxf(red[0][3 + c], red[1][3 + c]), fmaxf(red[2][3 + c], red[3][3 + c]));
-            // §9.2: inv = (hi>lo) ? 1/(hi-lo) : 0 -- correctly rounded fp32 division
-            p.inv[c] = (p.hi[c] > p.lo[c]) ? 1.0f / (p.hi[c] - p.lo[c]) : 0.0f;
-        }
+    for (int c = 0; c < 3; ++c) {
+        float a = red[0][c], b = red[0][3 + c];
 #pragma unroll
-        for (int c = 0; c < 7; ++c) p.pad[c] = 0u;
-        *params = p;
-        *ticket = 0u;  // re-arm for the next build (also memset at allocation)
+        for (int k = 1; k < NT / 64; ++k) { a = fminf(a, red[k][c]); b = fmaxf(b, red[k][3 + c]); }
+        p.lo[c] = a;
+        p.hi[c] = b;
+        // §9.2: inv = (hi>lo) ? 1/(hi-lo) : 0 -- correctly rounded fp32 division
+        p.inv[c] = (b > a) ? 1.0f / (b - a) : 0.0f;
     }
+#pragma unroll
+    for (int c = 0; c < 7; ++c) p.pad[c] = 0u;
+    return p;
+}
+
+// stage entry point (rt_stage_bounds): the second level on its own
+__global__ __launch_bounds__(256) void k_bounds_final(const float* __restrict__ partials, uint32_t nb,
+                                                      BuildParams* __restrict__ params) {
+    __shared__ float red[4][6];
+    const BuildParams p = bounds_final<256>(partials, nb, red);
+    if (threadIdx.x == 0) *params = p;
 }
 
 // ---------------------------------------------------------------- K1
@@ -174,16 +173,24 @@ __device__ __forceinline__ uint32_t quant(float c, float lo, float inv) {
 static_assert(kSortThreads * kTrisPerThread == kSortTile, "K1 block must be one sort tile");
 
 __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict__ tris, uint32_t n,
-                                                         const BuildParams* __restrict__ params,
+                                                         BuildParams* __restrict__ params,
+                                                         const float* __restrict__ partials, uint32_t nb,
                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                          uint32_t* __restrict__ ghist /* [4][256] */,
                                                          uint32_t* __restrict__ counts0 /* [tile][256] */) {
     __shared__ uint32_t hist[4 * 256];
+    __shared__ float red[kSortThreads / 64][6];
     for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) hist[j] = 0u;
-    const BuildParams p = *params;
     const uint32_t g = blockIdx.x * (uint32_t)kSortThreads + threadIdx.x;
     float t[72];
-    const uint32_t cnt = load_tri8(tris, n, g, t);
+    const uint32_t cnt = load_tri8(tris, n, g, t);  // in flight while the bounds are reduced
+    BuildParams p;
+    if (partials) {
+        p = bounds_final<kSortThreads>(partials, nb, red);
+        if (blockIdx.x == 0 && threadIdx.x == 0) *params = p;  // for the later stages / readback
+    } else {
+        p = *params;
+    }
     uint32_t k8[kTrisPerThread];
 #pragma unroll
     for (uint32_t q = 0; q < kTrisPerThread; ++q) {
@@ -274,31 +281,41 @@ __device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint3
     o[2] = make_float4(t[8], __uint_as_float(prim), 0.0f, 0.0f);
 }
 
-// Thread i: internal node i (i < n-1) and leaf i (i < n).
-__global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restrict__ keys_g, const uint32_t* __restrict__ svals,
-                                                       const float* __restrict__ tris, uint32_t n,
-                                                       uint4* __restrict__ topo, uint32_t* __restrict__ parent,
-                                                       void* __restrict__ nodes, float4* __restrict__ tri_s) {
-    constexpr int KW = 1024;                      // window margin on each side
-    __shared__ uint32_t s_keys[256 + 2 * KW];
-    const uint32_t i32 = blockIdx.x * 256u + threadIdx.x;
-    const int64_t B = (int64_t)blockIdx.x * 256;
+// Stage the sorted keys [B - KW, B + NT + KW) of a block of NT threads.
+template <int NT, int KW>
+__device__ __forceinline__ KeyWin stage_keys(const uint32_t* __restrict__ keys_g, uint32_t n, uint32_t* s_keys) {
+    const int64_t B = (int64_t)blockIdx.x * NT;
     const int64_t wlo = B - KW < 0 ? 0 : B - KW;
-    const int64_t whi = B + 256 + KW > (int64_t)n ? (int64_t)n : B + 256 + KW;
-    for (int64_t j = wlo + threadIdx.x; j < whi; j += 256) s_keys[j - wlo] = keys_g[j];
+    const int64_t whi = B + NT + KW > (int64_t)n ? (int64_t)n : B + NT + KW;
+    for (int64_t j = wlo + threadIdx.x; j < whi; j += NT) s_keys[j - wlo] = keys_g[j];
     __syncthreads();
-    const KeyWin keys{keys_g, s_keys, wlo, whi};
-    if (i32 >= n) return;
+    return KeyWin{keys_g, s_keys, wlo, whi};
+}
+
+// Thread i: internal node i (i < n-1) and leaf i (i < n).  Writes topo[i],
+// the two parent pointers, leaf node L0+i and tri_s[i]; returns the
+// topology word (zero when node i does not exist) and the leaf box.
+__device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const uint32_t* __restrict__ svals,
+                                                 const float* __restrict__ tris, uint32_t n, uint32_t i32,
+                                                 uint4* __restrict__ topo, uint32_t* __restrict__ parent,
+                                                 void* __restrict__ nodes, float4* __restrict__ tri_s, uint4& tp_out,
+                                                 Aabb& box) {
     const int64_t i = i32, N = n;
     const uint32_t L0 = n - 1;
     // leaf i's triangle: issue the gather first, consume it last
     const uint32_t prim = svals[i32];
     float tv[9];
     const float* src = tris + (uint64_t)prim * 9;
+#ifdef RT_EXP_K4_NOGATHER
+#pragma unroll
+    for (int c = 0; c < 9; ++c) tv[c] = (float)(prim + c);
+#else
 #pragma unroll
     for (int c = 0; c < 9; ++c) tv[c] = src[c];
+#endif
     if (i32 == 0) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
     uint32_t lesc;
+    tp_out = make_uint4(0, 0, 0, 0);
     if (i < N - 1) {
         const uint32_t ki = keys[i];
         const int d = (kdelta(keys, N, i, ki, i + 1) - kdelta(keys, N, i, ki, i - 1)) > 0 ? 1 : -1;
@@ -325,7 +342,8 @@ __global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restric
         if (mx == N - 1) esc = RT_SENT;
         else if (mx + 1 <= N - 2 && kdir(keys, N, mx + 1) > 0) esc = (uint32_t)(mx + 1);
         else esc = (uint32_t)(L0 + mx + 1);
-        topo[i] = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
+        tp_out = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
+        topo[i] = tp_out;
         parent[left] = i32;
         parent[right] = i32;
         // leaf i's range ends at i: same closed form with r = i
@@ -333,10 +351,23 @@ __global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restric
     } else {
         lesc = RT_SENT;  // leaf n-1
     }
-    Aabb box;
     tri_bounds(tv, box.lo, box.hi);
     store_node(nodes, L0 + i32, box, prim, lesc);
     store_leaf_tri(tri_s, i32, tv, prim);
+}
+
+// K4 alone (rt_stage_topology).
+__global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restrict__ keys_g, const uint32_t* __restrict__ svals,
+                                                       const float* __restrict__ tris, uint32_t n,
+                                                       uint4* __restrict__ topo, uint32_t* __restrict__ parent,
+                                                       void* __restrict__ nodes, float4* __restrict__ tri_s) {
+    __shared__ uint32_t s_keys[256 + 2 * 1024];
+    const KeyWin keys = stage_keys<256, 1024>(keys_g, n, s_keys);
+    const uint32_t i32 = blockIdx.x * 256u + threadIdx.x;
+    if (i32 >= n) return;
+    uint4 tp;
+    Aabb box;
+    karras_node_leaf(keys, svals, tris, n, i32, topo, parent, nodes, tri_s, tp, box);
 }
 
 // Stand-alone leaf-triangle pass (rt_stage_trace on caller nodes).
@@ -500,19 +531,36 @@ __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoO
     node[3] = a1 != RT_SENT ? b1 : RT_SENT;
 }
 
-// One block = kRefitT consecutive sorted leaves [B0, B1), one thread per leaf.
-__global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4* __restrict__ topo,
-                                                         const uint32_t* __restrict__ parent,
-                                                         void* __restrict__ nodes,
-                                                         float* __restrict__ prebuf, float* __restrict__ sufbuf,
-                                                         float* __restrict__ totals,
-                                                         uint32_t* __restrict__ cross, uint32_t* cross_ctr,
-                                                         uint32_t cross_cap, uint4* __restrict__ wnodes) {
-    constexpr int T = kRefitT, NW = T / 64;
-    __shared__ Aabb s_box[2 * T];      // [0,T) leaves, [T,2T) internal nodes of the block
+// K4 + K6 local + K7w local, fused.  One block = kRefitT consecutive sorted
+// leaves [B0, B1) and the internal nodes with the same indices, one thread
+// per leaf/node:
+//   1. Karras topology of internal node i and leaf i (karras_node_leaf; the
+//      topology words stay in LDS for step 4);
+//   2. block prefix/suffix scans of the leaf boxes for the crossing nodes
+//      (K6t: k_refit_cross) and the crossing list;
+//   3. the box of every LOCAL internal node (range inside the block) as a
+//      range union over its leaves: a sparse table over the block's leaf
+//      boxes, built level by level in LDS, and box[l, r] = T_k[l] U
+//      T_k[r - 2^k + 1] (k = floor(log2(r - l + 1))).  min/max are exact and
+//      order-free, so this is bit-identical to the bottom-up union of
+//      children -- without the serial climb (the old K6 spent ~6 us per
+//      block in its atomic-arrival loop) and without re-reading the
+//      topology and parent arrays K4 used to write for it;
+//   4. coalesced stores of the local internal nodes and their K7w records.
+__global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restrict__ keys_g,
+                                                        const uint32_t* __restrict__ svals,
+                                                        const float* __restrict__ tris, uint32_t n,
+                                                        uint4* __restrict__ topo, uint32_t* __restrict__ parent,
+                                                        void* __restrict__ nodes, float4* __restrict__ tri_s,
+                                                        float* __restrict__ prebuf, float* __restrict__ sufbuf,
+                                                        float* __restrict__ totals, uint32_t* __restrict__ cross,
+                                                        uint32_t* cross_ctr, uint32_t cross_cap,
+                                                        uint4* __restrict__ wnodes) {
+    constexpr int T = kRefitT, NW = T / 64, KW = 1024;
+    static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
+    __shared__ Aabb s_tab[T];          // key window first (uint32), then one sparse-table level
+    __shared__ Aabb s_box[2 * T];      // [0,T) leaves, [T,2T) local internal nodes
     __shared__ uint4 s_topo[T];
-    __shared__ uint32_t s_par[2 * T];
-    __shared__ uint32_t s_cnt[T];
     __shared__ Aabb s_wpre[NW], s_wsuf[NW];
     __shared__ uint32_t s_ncross, s_cbase;
 
@@ -522,41 +570,34 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
     const uint32_t B1 = (n - B0) < (uint32_t)T ? n : B0 + (uint32_t)T;
     const uint32_t k = B0 + tid;
     const bool valid = k < B1;
-    uint32_t cslot = RT_SENT;
+    const bool has_int = k + 1 < n;
     if (tid == 0) s_ncross = 0u;
     RT_STAMP(0);
-
-    Aabb box = aabb_empty();
+    // ---- 1. topology + leaf
     uint4 tp = make_uint4(0, 0, 0, 0);
-    if (valid) {
-        const float4* np = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)(L0 + k) * 32);
-        const float4 A = np[0], B = np[1];
-        box.lo[0] = A.x; box.lo[1] = A.y; box.lo[2] = A.z;
-        box.hi[0] = A.w; box.hi[1] = B.x; box.hi[2] = B.y;
-        s_box[tid] = box;
-        s_par[tid] = parent[L0 + k];
-        if (k + 1 < n) {  // internal node k exists
-            tp = topo[k];
-            s_topo[tid] = tp;
-            s_par[T + tid] = parent[k];
-        }
+    Aabb box = aabb_empty();
+    {
+        const KeyWin keys = stage_keys<T, KW>(keys_g, n, reinterpret_cast<uint32_t*>(s_tab));
+        RT_STAMP(1);
+        if (valid) karras_node_leaf(keys, svals, tris, n, k, topo, parent, nodes, tri_s, tp, box);
     }
-    s_cnt[tid] = 0u;
-    RT_STAMP(1);
-    // ---- block prefix / suffix scans of leaf AABBs (exact min/max)
+    s_box[tid] = box;
+    s_topo[tid] = tp;
+    RT_STAMP(2);
+    // ---- 2. block prefix / suffix scans of leaf AABBs (exact min/max)
     Aabb pre = box, suf = box;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) { shfl_up_aabb(pre, o); shfl_down_aabb(suf, o); }
     if (lane == 63) s_wpre[wv] = pre;
     if (lane == 0) s_wsuf[wv] = suf;
-    __syncthreads();
+    __syncthreads();  // also: s_box leaves, s_topo complete; the key window is dead
     for (uint32_t q = 0; q < wv; ++q) aabb_union(pre, s_wpre[q]);
     for (uint32_t q = wv + 1; q < NW; ++q) aabb_union(suf, s_wsuf[q]);
+    uint32_t cslot = RT_SENT;
     if (valid) {
         // crossing ends (DESIGN.md "refit"): the topmost node starting at leaf
         // k is internal k iff its range starts at k; the topmost node ending at
         // k is internal k iff its range ends at k; the root ends at n-1.
-        const bool has_int = k + 1 < n;
         const bool need_suf = has_int && tp.z == k && tp.w >= B1;
         const bool need_pre = (has_int && tp.w == k && tp.z < B0) || (k == n - 1 && B0 > 0);
         if (need_suf) store_aabb(sufbuf, k, suf);
@@ -565,48 +606,47 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
         if (has_int && (tp.z < B0 || tp.w >= B1)) cslot = atomicAdd(&s_ncross, 1u);  // LDS
     }
     __syncthreads();
-    RT_STAMP(2);
+    RT_STAMP(3);
     // one aggregated reservation per block on one of kCrossShards counters
-    // (a single global counter hit by every wave serialises at ~90 ops/us)
-    // (issued here, consumed after the climb: the atomic's latency overlaps it)
+    // (a single global counter hit by every wave serialises at ~90 ops/us);
+    // issued here, consumed after the sweep, so its latency overlaps it
     uint32_t cbase = 0;
     if (tid == 0 && s_ncross)
         cbase = (blockIdx.x % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[blockIdx.x % kCrossShards], s_ncross);
-    // ---- bottom-up climb inside the block, LDS only.  LDS instructions of a
-    // wave execute in order, so its s_box write lands before its own arrival
-    // add; the second arriver reads the sibling's box after its add returns.
-    // The asm statements only stop the compiler moving LDS accesses across
-    // the add (no global fence: node stores happen after the climb, coalesced).
-    if (valid && n > 1) {
-        uint32_t node = L0 + k;
-        uint32_t slot = tid;
-        for (uint32_t depth = 0; depth < (uint32_t)T; ++depth) {  // local depth < T
-            const uint32_t p = s_par[slot];
-            if (p == RT_SENT || p < B0 || p >= B1) break;
-            const uint4 pt = s_topo[p - B0];
-            if (pt.z < B0 || pt.w >= B1) break;  // p crosses the block: K6t's job
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            const uint32_t old = __hip_atomic_fetch_add(&s_cnt[p - B0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            asm volatile("" ::: "memory");
-            if (old == 0u) break;  // first arrival: the sibling finishes p
-            const uint32_t left = pt.x;
-            const uint32_t g = left >= L0 ? left - L0 : left;
-            const uint32_t right = (pt.w == g + 1) ? L0 + g + 1 : g + 1;
-            const uint32_t sib = (left == node) ? right : left;
-            const uint32_t sslot = sib >= L0 ? (sib - L0 - B0) : (T + sib - B0);
-            aabb_union(box, s_box[sslot]);
-            slot = T + (p - B0);
-            s_box[slot] = box;
-            node = p;
+    // ---- 3. sparse-table sweep: level kk holds T_kk[j] = U leaves [j, j + 2^kk)
+    const bool local = valid && has_int && tp.z >= B0 && tp.w < B1;
+    uint32_t need = 0, qa = 0, qb = 0;
+    if (local) {
+        const uint32_t len = tp.w - tp.z + 1;  // >= 2
+        need = 31u - (uint32_t)__clz((int)len);
+        qa = tp.z - B0;
+        qb = tp.w - B0 + 1 - (1u << need);
+    }
+    const uint32_t cnt = B1 - B0;
+    for (uint32_t kk = 1; (1u << kk) <= cnt; ++kk) {
+        const uint32_t h = 1u << (kk - 1);
+        const bool in = tid + 2 * h <= cnt;  // window [tid, tid + 2^kk) inside the block
+        Aabb v;
+        if (in) {
+            v = kk == 1 ? s_box[tid] : s_tab[tid];
+            aabb_union(v, kk == 1 ? s_box[tid + h] : s_tab[tid + h]);
+        }
+        __syncthreads();
+        if (in) s_tab[tid] = v;
+        __syncthreads();
+        if (need == kk) {
+            Aabb b = s_tab[qa];
+            aabb_union(b, s_tab[qb]);
+            s_box[T + tid] = b;
         }
     }
     if (tid == 0) s_cbase = cbase;
     __syncthreads();
-    RT_STAMP(3);
+    RT_STAMP(4);
     if (cslot != RT_SENT) cross[s_cbase + cslot] = k;
-    // ---- coalesced store of this block's local internal nodes [B0, B1), and
-    // their K7w wide records (every box they need is in LDS)
-    if (valid && k + 1 < n && tp.z >= B0 && tp.w < B1) {
+    // ---- 4. coalesced store of this block's local internal nodes and their
+    // K7w wide records (every box they need is in LDS)
+    if (local) {
         const Aabb bx = s_box[T + tid];
         store_node(nodes, k, bx, tp.x, tp.y);
         uint32_t node[4];
@@ -617,7 +657,7 @@ __global__ __launch_bounds__(kRefitT) void k_refit_local(uint32_t n, const uint4
             slot[i] = node[i] == RT_SENT ? T + tid : node[i] >= L0 ? node[i] - L0 - B0 : T + node[i] - B0;
         store_wide(wnodes, k, bx, node, [&](int i) { return s_box[slot[i]]; }, L0);
     }
-    RT_STAMP(4);
+    RT_STAMP(5);
 }
 
 __global__ __launch_bounds__(256) void k_sparse_level(const float* __restrict__ src, float* __restrict__ dst, uint32_t m, uint32_t half) {
@@ -762,36 +802,39 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.cross, (uint64_t)cross_cap(b.m_blocks) * kCrossShards * 4);
     RT_ALLOC(b.counts, (uint64_t)4 * b.ntiles * 256 * 4);
     RT_ALLOC(b.partials, (uint64_t)bounds_grid((uint32_t)N) * 24);
-    RT_ALLOC(b.ticket, 256);
     RT_ALLOC(b.params, sizeof(BuildParams));
     RT_ALLOC(b.zero, (uint64_t)b.nzero * 4);
 #undef RT_ALLOC
-    if ((e = hipMemset(b.ticket, 0, 256)) != hipSuccess) { free_build(b); return e; }
     if ((e = hipMemset(b.zero, 0, (uint64_t)b.nzero * 4)) != hipSuccess) { free_build(b); return e; }
     return hipSuccess;
 }
 
 void free_build(BuildBufs& b) {
     void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.tri_s, b.parent, b.topo, b.wnodes,
-                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.partials, b.ticket, b.params, b.zero};
+                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.partials, b.params, b.zero};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = BuildBufs{};
 }
 
-hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, uint32_t* ticket,
-                              BuildParams* params, hipStream_t s) {
-    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, tris, n, partials, ticket, params,
-                       (uint32_t*)nullptr, 0u);
+hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, BuildParams* params, hipStream_t s) {
+    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, tris, n, partials, (uint32_t*)nullptr, 0u);
+    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, partials, bounds_grid(n), params);
+    return hipGetLastError();
+}
+
+static hipError_t launch_morton_impl(const float* tris, uint32_t n, BuildParams* params, const float* partials,
+                                     uint32_t nb, uint32_t* keys, uint32_t* vals, uint32_t* ghist, uint32_t* counts0,
+                                     hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_morton, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials, nb, keys,
+                       vals, ghist, counts0);
     return hipGetLastError();
 }
 
 hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,
                          uint32_t* vals, uint32_t* ghist, uint32_t* counts0, hipStream_t s) {
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_morton, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, keys, vals, ghist,
-                       counts0);
-    return hipGetLastError();
+    return launch_morton_impl(tris, n, const_cast<BuildParams*>(params), nullptr, 0, keys, vals, ghist, counts0, s);
 }
 
 hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, float4* tri_s, hipStream_t s) {
@@ -808,10 +851,9 @@ hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const floa
     return hipGetLastError();
 }
 
-static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
+// K6t + K7w for the nodes whose range crosses a refit block (after k_topo_refit).
+static hipError_t launch_cross(const BuildBufs& b, uint32_t n, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
-    hipLaunchKernelGGL(k_refit_local, dim3(m), dim3(kRefitT), 0, s, n, b.topo, b.parent, b.nodes, b.prebuf, b.sufbuf,
-                       b.table, b.cross, b.zero + kZCrossCtr, cross_cap(m), b.wnodes);
     if (m <= 1) return hipGetLastError();
     if (m <= (uint32_t)kLdsTreeMaxBlocks) {
         uint32_t P = 1;
@@ -841,29 +883,37 @@ static hipError_t launch_refit(const BuildBufs& b, uint32_t n, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev) {
+hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages) {
     hipError_t e;
-    auto rec = [&](int i) -> hipError_t { return ev ? hipEventRecord(ev->e[i], s) : hipSuccess; };
+    auto rec = [&](int i) -> hipError_t {
+        return (ev && (stages || i == 0 || i == 6)) ? hipEventRecord(ev->e[i], s) : hipSuccess;
+    };
     if ((e = rec(0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.ticket, b.params,
-                       b.zero, kZEnd);
+    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.zero, kZEnd);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = rec(1)) != hipSuccess) return e;
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
-    if ((e = launch_morton(b.tris, n, b.params, b.keys[0], b.vals[0], b.zero + kZHist, counts[0], s)) != hipSuccess)
+    if (!n) hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
+    if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
+                                b.zero + kZHist, counts[0], s)) != hipSuccess)
         return e;
     if ((e = rec(2)) != hipSuccess) return e;
     uint32_t* K[2] = {b.keys[0], b.keys[1]};
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
     if ((e = launch_sort(K, V, n, b.zero + kZHist, counts, s)) != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;
-    if ((e = launch_karras(b.keys[0], b.vals[0], b.tris, n, b.topo, b.parent, b.nodes, b.tri_s, s)) != hipSuccess)
-        return e;
+    if (n) {
+        const uint32_t m = cdiv(n, kRefitT);
+        hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
+                           b.parent, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
+                           cross_cap(m), b.wnodes);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if ((e = rec(4)) != hipSuccess) return e;
-    if (n && (e = launch_refit(b, n, s)) != hipSuccess) return e;
+    if (n && (e = launch_cross(b, n, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
-    if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K6 (records written with the boxes)
+    if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K4/K6 (records written with the boxes)
     return hipSuccess;
 }
 

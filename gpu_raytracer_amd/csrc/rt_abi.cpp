@@ -76,10 +76,15 @@ rt_status ensure_stream(rt_scene* s) {
     if (st) return st;
     if (!s->stream) {
         HIPR(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-        for (auto& e : s->ev.e) HIPR(hipEventCreate(&e));
+        // timing-only events: no system-scope fence (L2 writeback + invalidate)
+        // at each record, which would add ~4.7 us per event to the GPU
+        // timeline between the kernels being timed.  Every host read of
+        // results goes through a stream synchronize or a blocking copy.
+        const unsigned fl = rt::g_trace_config.event_fence ? hipEventDefault : hipEventDisableSystemFence;
+        for (auto& e : s->ev.e) HIPR(hipEventCreateWithFlags(&e, fl));
         s->ev.valid = true;
-        HIPR(hipEventCreate(&s->r0));
-        HIPR(hipEventCreate(&s->r1));
+        HIPR(hipEventCreateWithFlags(&s->r0, fl));
+        HIPR(hipEventCreateWithFlags(&s->r1, fl));
         HIPR(hipMalloc((void**)&s->d_work, 4096));  // kPoolCounters x 128 B
     }
     return RT_OK;
@@ -143,6 +148,8 @@ rt_status rt_config_set(const char* key, int64_t value) {
     else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
+    else if (k == "build.stage_events" && (value == 0 || value == 1)) rt::g_trace_config.stage_events = (uint32_t)value;
+    else if (k == "timing.event_fence" && (value == 0 || value == 1)) rt::g_trace_config.event_fence = (uint32_t)value;
     else if (k == "path.wavefront" && (value == 0 || value == 1)) rt::g_trace_config.path_wave = (uint32_t)value;
     else if (k == "path.wg" && (value == 64 || value == 256)) rt::g_trace_config.path_wg = (uint32_t)value;
     else if (k == "path.sort" && value >= 0 && value <= 4) rt::g_trace_config.path_sort = (uint32_t)value;
@@ -303,11 +310,13 @@ rt_status rt_bvh_build(rt_scene* s, double* ms_out) {
     if (!s) return fail(RT_EINVAL, "null scene");
     rt_status st = upload(s);
     if (st) return st;
-    hipError_t e = rt::launch_build(s->bufs, s->n, s->stream, &s->ev);
+    const bool stages = rt::g_trace_config.stage_events != 0;
+    hipError_t e = rt::launch_build(s->bufs, s->n, s->stream, &s->ev, stages);
     if (e != hipSuccess) return hip_fail(e, "launch_build");
     HIPR(hipStreamSynchronize(s->stream));
-    float t[6];
-    for (int i = 0; i < 6; ++i) HIPR(hipEventElapsedTime(&t[i], s->ev.e[i], s->ev.e[i + 1]));
+    float t[6] = {0, 0, 0, 0, 0, 0};
+    if (stages)
+        for (int i = 0; i < 6; ++i) HIPR(hipEventElapsedTime(&t[i], s->ev.e[i], s->ev.e[i + 1]));
     s->times.bounds = t[0];
     s->times.morton = t[1];
     s->times.sort = t[2];
@@ -731,14 +740,12 @@ rt_status rt_stage_bounds(int device, const float* tris, uint32_t n, float bound
     if ((n && !tris) || !bounds9) return fail(RT_EINVAL, "null argument");
     rt_status st = ensure_device(device);
     if (st) return st;
-    DevBuf dt, dp, dk, dpar;
+    DevBuf dt, dp, dpar;
     HIPR(dt.alloc((size_t)n * 36));
     HIPR(dp.alloc((size_t)rt::bounds_grid(n) * 24));
-    HIPR(dk.alloc(256));
     HIPR(dpar.alloc(sizeof(rt::BuildParams)));
-    HIPR(hipMemset(dk.p, 0, 256));
     if (n) HIPR(hipMemcpy(dt.p, tris, (size_t)n * 36, hipMemcpyHostToDevice));
-    HIPR(rt::launch_bounds_only(dt.as<float>(), n, dp.as<float>(), dk.as<uint32_t>(), dpar.as<rt::BuildParams>(), 0));
+    HIPR(rt::launch_bounds_only(dt.as<float>(), n, dp.as<float>(), dpar.as<rt::BuildParams>(), 0));
     HIPR(hipDeviceSynchronize());
     HIPR(hipMemcpy(bounds9, dpar.p, 36, hipMemcpyDeviceToHost));
     return RT_OK;

@@ -27,7 +27,6 @@ struct BuildBufs {
     float* table = nullptr;         // sparse table over refit-block totals, levels x M x 6
     uint32_t* cross = nullptr;      // crossing internal nodes (list)
     float* partials = nullptr;      // K0 per-block partial bounds
-    uint32_t* ticket = nullptr;     // K0 last-block ticket (self-resetting)
     BuildParams* params = nullptr;  // lo/hi/inv
     uint32_t* zero = nullptr;       // per-build zeroed control words, see zero_layout()
     uint32_t nzero = 0;
@@ -51,12 +50,12 @@ void free_build(BuildBufs& b);
 struct BuildEvents { hipEvent_t e[7]; bool valid = false; };
 
 // K0..K7w on `stream` for the n tris already in b.tris.  Sorted keys/vals end
-// in keys[0]/vals[0].  Records e[0..6] around the stages when ev != nullptr.
-hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev);
+// in keys[0]/vals[0].  With ev: e[0] and e[6] around the build, and e[1..5]
+// between the stages when `stages`.
+hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev, bool stages);
 
 // Stage launchers for parity entry points (buffers sized by the caller).
-hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, uint32_t* ticket,
-                              BuildParams* params, hipStream_t s);
+hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, BuildParams* params, hipStream_t s);
 hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,
                          uint32_t* vals, uint32_t* ghist, uint32_t* counts0, hipStream_t s);
 hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s);
@@ -84,6 +83,8 @@ struct TraceConfig {
     uint32_t path_wg = 64;      // path megakernel: threads per block (64 = 8x8 quadrant, 256 = 16x16 tile)
     uint32_t path_sort = 0;     // wavefront: top key bytes the ray queue is sorted by (0 = unsorted, default)
     uint32_t path_batch = 0;    // wavefront: paths per batch (0 = 4M)
+    uint32_t stage_events = 0;  // build: record the per-stage events (rt_bvh_build_times); else total only
+    uint32_t event_fence = 0;   // timing events with the system-scope fence (scenes created afterwards)
 };
 extern TraceConfig g_trace_config;
 

@@ -82,8 +82,11 @@ rt_status rt_camera_look_at(const double eye[3], const double at[3], const doubl
 /* ---- BVH build (SURVEY.md §8(b) rt_bvh_build; device mask replaced by the
  * scene's device -- one process per GPU).  Uploads the soup once (H2D is not
  * part of ms_out), then runs K0..K6 on the scene's stream.  ms_out: device
- * time of the build. */
+ * time of the build (hipEvents around it). */
 rt_status rt_bvh_build(rt_scene* s, double* ms_out);
+/* times of the last build: `total` always; the per-stage fields only when
+ * the build ran with rt_config_set("build.stage_events", 1) (0 otherwise --
+ * the extra events cost GPU time, so timed builds run without them) */
 rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out);
 /* Read back the device BVH (any pointer may be NULL): nodes[2n-1],
  * sorted keys/vals[n], parent[2n-1], bounds[9] = lo[3], hi[3], inv[3]. */
@@ -209,8 +212,11 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * (default); "path.sort" 0..4 = top key bytes each queue is radix-sorted by
  * for coherence (ray kind, direction octant, Morton code of the origin; 0 =
  * unsorted, the default; sorting reads each queue length back to the host);
- * "path.batch" paths per wavefront batch (0 = 4M).  Results are
- * bit-identical for every setting. */
+ * "path.batch" paths per wavefront batch (0 = 4M).  "build.stage_events"
+ * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
+ * 0/1: timing events of scenes created afterwards record with the
+ * system-scope fence (default 0: no L2 writeback at each record).  Results
+ * are bit-identical for every setting. */
 rt_status rt_config_set(const char* key, int64_t value);
 
 const char* rt_last_error(void);

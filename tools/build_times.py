@@ -1,0 +1,30 @@
+"""Median build-stage times (hipEvents) of rt_bvh_build on the soup.
+usage: RT_LIB=<lib.so> python tools/build_times.py [n] [reps]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import gpu_raytracer_amd as R  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+R.config_set("timing.event_fence", int(os.environ.get("RT_EVENT_FENCE", "0")))
+s = R.Scene.generate_soup(n, 1)
+rows, tot = [], []
+R.config_set("build.stage_events", 1)
+for i in range(reps + 3):
+    s.build()
+    t = s.build_times()
+    if i >= 3:
+        rows.append([t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total])
+R.config_set("build.stage_events", 0)
+for i in range(reps + 3):
+    ms = s.build()
+    if i >= 3:
+        tot.append(ms)
+m = np.median(np.array(rows), 0) * 1e3
+lib = os.path.basename(os.environ.get("RT_LIB", "librtamd.so")) + (" fence" if os.environ.get("RT_EVENT_FENCE") == "1" else "")
+print(f"{lib:<24s} n={n} us: bounds {m[0]:6.1f} morton {m[1]:6.1f} sort {m[2]:6.1f} topo {m[3]:6.1f} "
+      f"refit {m[4]:6.1f} wide {m[5]:5.1f} total(stage events) {m[6]:6.1f}  total {np.median(tot) * 1e3:6.1f}")

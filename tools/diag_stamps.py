@@ -40,7 +40,8 @@ s = R.Scene.generate_soup(n, 1)
 for _ in range(3):
     s.build()
 M = (n + 511) // 512
-report("k_refit_local", stamps(M)[:, :5], ["leaf/topo/parent loads", "scans+flags+sync", "climb+sync", "node stores"], 5)
+report("k_topo_refit", stamps(M)[:, :6], ["key window+sync", "topology+leaf (thread 0)", "scans+flags+sync",
+                                          "sparse-table sweep+sync", "node+K7w stores"], 6)
 keys = np.random.default_rng(0).integers(0, 2**30, n, dtype=np.uint64).astype(np.uint32)
 for _ in range(2):
     R.stage_sort(keys, np.arange(n, dtype=np.uint32))
