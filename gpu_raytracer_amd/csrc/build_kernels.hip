@@ -292,68 +292,139 @@ __device__ __forceinline__ KeyWin stage_keys(const uint32_t* __restrict__ keys_g
     return KeyWin{keys_g, s_keys, wlo, whi};
 }
 
+// Karras topology word of internal node i from its direction d, dmin and the
+// range length l, plus the two parent pointers and the
+// §9.6 closed-form escape link.  lsplit: the split offset s.
+__device__ __forceinline__ uint4 karras_finish(const KeyWin& keys, int64_t N, int64_t i, int d, int64_t l, int64_t s,
+                                               uint4* __restrict__ topo, uint32_t* __restrict__ parent) {
+    const uint32_t L0 = (uint32_t)N - 1;
+    const int64_t j = i + l * d;
+    const int64_t g = i + s * d + (d < 0 ? d : 0);
+    const int64_t mn = d > 0 ? i : j, mx = d > 0 ? j : i;
+    const uint32_t left = (mn == g) ? (uint32_t)(L0 + g) : (uint32_t)g;
+    const uint32_t right = (mx == g + 1) ? (uint32_t)(L0 + g + 1) : (uint32_t)(g + 1);
+    // §9.6 closed form: esc(node with range end r) = r == n-1 ? SENT
+    //   : (r+1 <= n-2 && dir(r+1) == +1) ? internal r+1 : leaf r+1
+    uint32_t esc;
+    if (mx == N - 1) esc = RT_SENT;
+    else if (mx + 1 <= N - 2 && kdir(keys, N, mx + 1) > 0) esc = (uint32_t)(mx + 1);
+    else esc = (uint32_t)(L0 + mx + 1);
+    const uint4 tp = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
+    topo[i] = tp;
+    parent[left] = (uint32_t)i;
+    parent[right] = (uint32_t)i;
+    return tp;
+}
+
 // Thread i: internal node i (i < n-1) and leaf i (i < n).  Writes topo[i],
 // the two parent pointers, leaf node L0+i and tri_s[i]; returns the
-// topology word (zero when node i does not exist) and the leaf box.
-__device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const uint32_t* __restrict__ svals,
-                                                 const float* __restrict__ tris, uint32_t n, uint32_t i32,
+// topology word (zero when node i does not exist) and the leaf box.  With
+// allow_defer, a node whose exponential search would leave the staged key
+// window (a range longer than the window margin: the top ~log2(n/KW) levels,
+// about one node per block) is not searched here -- `deferred` is set and
+// its wave searches it cooperatively (karras_wave_search): the serial
+// search would be ~40 dependent global loads and hold the whole block.
+// Leaf i's triangle, gathered through the sorted index (issued early by the
+// callers so its latency overlaps the key staging and the searches).
+struct LeafTri { float v[9]; uint32_t prim; };
+__device__ __forceinline__ LeafTri gather_leaf(uint32_t prim, const float* __restrict__ tris) {
+    LeafTri t;
+    t.prim = prim;
+    const float* src = tris + (uint64_t)t.prim * 9;
+#pragma unroll
+    for (int c = 0; c < 9; ++c) t.v[c] = src[c];
+    return t;
+}
+
+__device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafTri& lt, uint32_t n, uint32_t i32,
                                                  uint4* __restrict__ topo, uint32_t* __restrict__ parent,
                                                  void* __restrict__ nodes, float4* __restrict__ tri_s, uint4& tp_out,
-                                                 Aabb& box) {
+                                                 Aabb& box, bool allow_defer, bool& deferred) {
     const int64_t i = i32, N = n;
     const uint32_t L0 = n - 1;
-    // leaf i's triangle: issue the gather first, consume it last
-    const uint32_t prim = svals[i32];
-    float tv[9];
-    const float* src = tris + (uint64_t)prim * 9;
-#ifdef RT_EXP_K4_NOGATHER
-#pragma unroll
-    for (int c = 0; c < 9; ++c) tv[c] = (float)(prim + c);
-#else
-#pragma unroll
-    for (int c = 0; c < 9; ++c) tv[c] = src[c];
-#endif
     if (i32 == 0) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
     uint32_t lesc;
     tp_out = make_uint4(0, 0, 0, 0);
+    deferred = false;
     if (i < N - 1) {
         const uint32_t ki = keys[i];
         const int d = (kdelta(keys, N, i, ki, i + 1) - kdelta(keys, N, i, ki, i - 1)) > 0 ? 1 : -1;
         const int dmin = kdelta(keys, N, i, ki, i - d);
         int64_t lmax = 2;
-        while (kdelta(keys, N, i, ki, i + lmax * d) > dmin) lmax <<= 1;
-        int64_t l = 0;
-        for (int64_t t = lmax >> 1; t >= 1; t >>= 1)
-            if (kdelta(keys, N, i, ki, i + (l + t) * d) > dmin) l += t;
-        const int64_t j = i + l * d;
-        const int dnode = kdelta(keys, N, i, ki, j);
-        int64_t s = 0, t = l;
-        do {
-            t = (t + 1) >> 1;
-            if (kdelta(keys, N, i, ki, i + (s + t) * d) > dnode) s += t;
-        } while (t > 1);
-        const int64_t g = i + s * d + (d < 0 ? d : 0);
-        const int64_t mn = d > 0 ? i : j, mx = d > 0 ? j : i;
-        const uint32_t left = (mn == g) ? (uint32_t)(L0 + g) : (uint32_t)g;
-        const uint32_t right = (mx == g + 1) ? (uint32_t)(L0 + g + 1) : (uint32_t)(g + 1);
-        // §9.6 closed form: esc(node with range end r) = r == n-1 ? SENT
-        //   : (r+1 <= n-2 && dir(r+1) == +1) ? internal r+1 : leaf r+1
-        uint32_t esc;
-        if (mx == N - 1) esc = RT_SENT;
-        else if (mx + 1 <= N - 2 && kdir(keys, N, mx + 1) > 0) esc = (uint32_t)(mx + 1);
-        else esc = (uint32_t)(L0 + mx + 1);
-        tp_out = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
-        topo[i] = tp_out;
-        parent[left] = i32;
-        parent[right] = i32;
+        for (;;) {
+            const int64_t q = i + lmax * d;
+            if (allow_defer && q >= 0 && q < N && (q < keys.lo || q >= keys.hi)) { deferred = true; break; }
+            if (!(kdelta(keys, N, i, ki, q) > dmin)) break;
+            lmax <<= 1;
+        }
+        if (!deferred) {
+            int64_t l = 0;
+            for (int64_t t = lmax >> 1; t >= 1; t >>= 1)
+                if (kdelta(keys, N, i, ki, i + (l + t) * d) > dmin) l += t;
+            const int dnode = kdelta(keys, N, i, ki, i + l * d);
+            int64_t s = 0, t = l;
+            do {
+                t = (t + 1) >> 1;
+                if (kdelta(keys, N, i, ki, i + (s + t) * d) > dnode) s += t;
+            } while (t > 1);
+            tp_out = karras_finish(keys, N, i, d, l, s, topo, parent);
+        } else {
+            // the crossing flags only need which end of the range i is
+            tp_out = make_uint4(0, 0, d > 0 ? i32 : 0u, d > 0 ? RT_SENT - 1 : i32);
+        }
         // leaf i's range ends at i: same closed form with r = i
         lesc = (i + 1 <= N - 2 && kdir(keys, N, i + 1) > 0) ? (uint32_t)(i + 1) : (uint32_t)(L0 + i + 1);
     } else {
         lesc = RT_SENT;  // leaf n-1
     }
-    tri_bounds(tv, box.lo, box.hi);
-    store_node(nodes, L0 + i32, box, prim, lesc);
-    store_leaf_tri(tri_s, i32, tv, prim);
+    tri_bounds(lt.v, box.lo, box.hi);
+    store_node(nodes, L0 + i32, box, lt.prim, lesc);
+    store_leaf_tri(tri_s, i32, lt.v, lt.prim);
+}
+
+// Largest t in [0, R) with delta(i, i + t d) > thr, all 64 lanes probing at
+// once (63-ary search; the predicate is monotone in t and true at t = 0).
+__device__ __forceinline__ int64_t wave_max_true(const KeyWin& keys, int64_t N, int64_t i, uint32_t ki, int d, int thr,
+                                                 int64_t R) {
+    const uint32_t lane = threadIdx.x & 63;
+    int64_t base = 0, span = R;  // answer in [base, base + span)
+    while (span > 1) {
+        const int64_t step = (span + 62) / 63;
+        const int64_t t = base + (int64_t)(lane + 1) * step;
+        const bool p = lane < 63 && t < base + span && kdelta(keys, N, i, ki, i + t * d) > thr;
+        const uint32_t c = (uint32_t)__popcll(__ballot(p));  // monotone: lanes [0, c) true
+        const int64_t nb = base + (int64_t)c * step;
+        const int64_t end = base + span;
+        base = nb;
+        span = (nb + step < end ? nb + step : end) - nb;
+    }
+    return base;
+}
+
+// The wave's deferred nodes, one at a time, every lane probing: exponential
+// search in one round (lanes p = 1..31 test 2^p), then the range and split
+// searches 63-ary.  Same monotone predicates and answers as the serial code.
+__device__ __forceinline__ void karras_wave_search(const KeyWin& keys, uint32_t n, uint32_t i32, bool deferred,
+                                                   uint4* __restrict__ topo, uint32_t* __restrict__ parent,
+                                                   uint4& tp) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t dm = __ballot(deferred);
+    const int64_t N = n;
+    while (dm) {
+        const uint32_t src = (uint32_t)__ffsll((long long)dm) - 1;
+        dm &= dm - 1;
+        const int64_t i = (int64_t)(uint32_t)__shfl((int)i32, (int)src, 64);
+        const uint32_t ki = keys[i];
+        const int d = (kdelta(keys, N, i, ki, i + 1) - kdelta(keys, N, i, ki, i - 1)) > 0 ? 1 : -1;
+        const int dmin = kdelta(keys, N, i, ki, i - d);
+        const bool pe = lane >= 1 && lane <= 31 && kdelta(keys, N, i, ki, i + ((int64_t)1 << lane) * d) > dmin;
+        const uint32_t pstar = 1u + (uint32_t)__popcll(__ballot(pe));
+        const int64_t lmax = (int64_t)1 << pstar;
+        const int64_t l = wave_max_true(keys, N, i, ki, d, dmin, lmax);
+        const int dnode = kdelta(keys, N, i, ki, i + l * d);
+        const int64_t s = wave_max_true(keys, N, i, ki, d, dnode, l);
+        if (lane == src) tp = karras_finish(keys, N, i, d, l, s, topo, parent);
+    }
 }
 
 // K4 alone (rt_stage_topology).
@@ -362,12 +433,15 @@ __global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restric
                                                        uint4* __restrict__ topo, uint32_t* __restrict__ parent,
                                                        void* __restrict__ nodes, float4* __restrict__ tri_s) {
     __shared__ uint32_t s_keys[256 + 2 * 1024];
-    const KeyWin keys = stage_keys<256, 1024>(keys_g, n, s_keys);
     const uint32_t i32 = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t prim = i32 < n ? svals[i32] : 0u;
+    const KeyWin keys = stage_keys<256, 1024>(keys_g, n, s_keys);
     if (i32 >= n) return;
+    const LeafTri lt = gather_leaf(prim, tris);
     uint4 tp;
     Aabb box;
-    karras_node_leaf(keys, svals, tris, n, i32, topo, parent, nodes, tri_s, tp, box);
+    bool deferred;
+    karras_node_leaf(keys, lt, n, i32, topo, parent, nodes, tri_s, tp, box, false, deferred);
 }
 
 // Stand-alone leaf-triangle pass (rt_stage_trace on caller nodes).
@@ -558,9 +632,8 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         uint4* __restrict__ wnodes) {
     constexpr int T = kRefitT, NW = T / 64, KW = 1024;
     static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
-    __shared__ Aabb s_tab[T];          // key window first (uint32), then one sparse-table level
-    __shared__ Aabb s_box[2 * T];      // [0,T) leaves, [T,2T) local internal nodes
-    __shared__ uint4 s_topo[T];
+    __shared__ Aabb s_tab[T];          // key window first (uint32), then the odd sparse-table levels
+    __shared__ Aabb s_box[2 * T];      // [0,T) leaves; [T,2T) the even levels, then local internal nodes
     __shared__ Aabb s_wpre[NW], s_wsuf[NW];
     __shared__ uint32_t s_ncross, s_cbase;
 
@@ -577,12 +650,18 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
     uint4 tp = make_uint4(0, 0, 0, 0);
     Aabb box = aabb_empty();
     {
+        // the gather is issued after the key staging: before it, the staging's
+        // wait (vmcnt is in order) would also wait for the random gather
+        const uint32_t prim = valid ? svals[k] : 0u;  // coalesced, with the window loads
         const KeyWin keys = stage_keys<T, KW>(keys_g, n, reinterpret_cast<uint32_t*>(s_tab));
         RT_STAMP(1);
-        if (valid) karras_node_leaf(keys, svals, tris, n, k, topo, parent, nodes, tri_s, tp, box);
+        LeafTri lt;
+        if (valid) lt = gather_leaf(prim, tris);
+        bool deferred = false;
+        if (valid) karras_node_leaf(keys, lt, n, k, topo, parent, nodes, tri_s, tp, box, true, deferred);
+        karras_wave_search(keys, n, k, deferred, topo, parent, tp);
     }
     s_box[tid] = box;
-    s_topo[tid] = tp;
     RT_STAMP(2);
     // ---- 2. block prefix / suffix scans of leaf AABBs (exact min/max)
     Aabb pre = box, suf = box;
@@ -590,7 +669,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
     for (int o = 1; o < 64; o <<= 1) { shfl_up_aabb(pre, o); shfl_down_aabb(suf, o); }
     if (lane == 63) s_wpre[wv] = pre;
     if (lane == 0) s_wsuf[wv] = suf;
-    __syncthreads();  // also: s_box leaves, s_topo complete; the key window is dead
+    __syncthreads();  // also: s_box leaves complete; the key window is dead
     for (uint32_t q = 0; q < wv; ++q) aabb_union(pre, s_wpre[q]);
     for (uint32_t q = wv + 1; q < NW; ++q) aabb_union(suf, s_wsuf[q]);
     uint32_t cslot = RT_SENT;
@@ -613,7 +692,9 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
     uint32_t cbase = 0;
     if (tid == 0 && s_ncross)
         cbase = (blockIdx.x % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[blockIdx.x % kCrossShards], s_ncross);
-    // ---- 3. sparse-table sweep: level kk holds T_kk[j] = U leaves [j, j + 2^kk)
+    // ---- 3. sparse-table sweep: level kk holds T_kk[j] = U leaves [j, j + 2^kk),
+    // odd levels in s_tab, even ones in s_box[T, 2T) (ping-pong: one barrier
+    // per level); a node's box waits in registers until the sweep is over
     const bool local = valid && has_int && tp.z >= B0 && tp.w < B1;
     uint32_t need = 0, qa = 0, qb = 0;
     if (local) {
@@ -623,23 +704,24 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         qb = tp.w - B0 + 1 - (1u << need);
     }
     const uint32_t cnt = B1 - B0;
+    Aabb nbox = aabb_empty();
     for (uint32_t kk = 1; (1u << kk) <= cnt; ++kk) {
         const uint32_t h = 1u << (kk - 1);
-        const bool in = tid + 2 * h <= cnt;  // window [tid, tid + 2^kk) inside the block
-        Aabb v;
-        if (in) {
-            v = kk == 1 ? s_box[tid] : s_tab[tid];
-            aabb_union(v, kk == 1 ? s_box[tid + h] : s_tab[tid + h]);
+        const Aabb* src = kk == 1 ? s_box : (kk & 1) ? s_box + T : s_tab;
+        Aabb* dst = (kk & 1) ? s_tab : s_box + T;
+        if (tid + 2 * h <= cnt) {  // window [tid, tid + 2^kk) inside the block
+            Aabb v = src[tid];
+            aabb_union(v, src[tid + h]);
+            dst[tid] = v;
         }
-        __syncthreads();
-        if (in) s_tab[tid] = v;
         __syncthreads();
         if (need == kk) {
-            Aabb b = s_tab[qa];
-            aabb_union(b, s_tab[qb]);
-            s_box[T + tid] = b;
+            nbox = dst[qa];
+            aabb_union(nbox, dst[qb]);
         }
     }
+    __syncthreads();  // the even-level buffer becomes the internal-node boxes
+    if (local) s_box[T + tid] = nbox;
     if (tid == 0) s_cbase = cbase;
     __syncthreads();
     RT_STAMP(4);
@@ -650,7 +732,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         const Aabb bx = s_box[T + tid];
         store_node(nodes, k, bx, tp.x, tp.y);
         uint32_t node[4];
-        wide_entries(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; }, node);
+        wide_entries(tp, L0, [&](uint32_t i) { return topo[i]; }, node);  // this block's words, L2-hot
         uint32_t slot[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
