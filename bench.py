@@ -240,6 +240,28 @@ def main():
     build_ms, trace_ms, gather_ms = (float(x) for x in per.mean(axis=0))
     trace_ms_min = float(per[:, 1].min())
 
+    # "rank 0 builds and then broadcasts" measured next to the
+    # replicated build (untimed by the step contract; 1 warm-up + 3 timed)
+    bvh_exchange = None
+    if world > 1 and args.dist_backend == "nccl":
+        try:
+            bms = []
+            for i in range(4):
+                barrier()
+                tb0 = time.perf_counter()
+                nbytes = D.broadcast_bvh(scene, dev)
+                torch.cuda.synchronize(dev)
+                barrier()
+                if i:
+                    bms.append((time.perf_counter() - tb0) * 1e3)
+            bt = torch.tensor([float(np.median(bms))], dtype=torch.float64, device=dev)
+            dist.all_reduce(bt, op=dist.ReduceOp.MAX)
+            bvh_exchange = {"replicated_build_ms": round(build_ms, 4), "broadcast_ms": round(float(bt.item()), 4),
+                            "broadcast_bytes": int(nbytes),
+                            "used": "replicated build (every rank builds; no BVH traffic)"}
+        except Exception as exc:  # a measurement only: never fail the bench line over it
+            bvh_exchange = {"error": f"{type(exc).__name__}: {exc}"[:200]}
+
     # work counters of this rank's trace launch (deterministic; untimed)
     cnt = scene.render_tiles_counters(cam, w, h, spp, rank, world) if world > 1 else scene.render_counters(cam, w, h, spp)
     rank_rays = D.rays_of_rank(w, h, spp, rank, world)
@@ -286,6 +308,7 @@ def main():
             "trace_ms": round(trace_ms, 4),
             "trace_ms_min": round(trace_ms_min, 4),
             "gather_ms": round(gather_ms, 4),
+            "bvh_exchange": bvh_exchange,
             "frame_mrays_per_s": round(rays / (wall / args.steps) / 1e6, 2),
             "build_stages_ms_last": {"bounds": round(stimes.bounds, 4), "morton": round(stimes.morton, 4),
                                      "sort": round(stimes.sort, 4), "topology": round(stimes.topology, 4),

@@ -38,6 +38,7 @@ EXPORTED = [
     "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_render", "rt_render_counters", "rt_render_work", "rt_render_device",
     "rt_render_shadow", "rt_render_shadow_device", "rt_render_shadow_work",
     "rt_render_path", "rt_render_path_device", "rt_render_path_work",
+    "rt_bvh_prepare", "rt_bvh_device_sections", "rt_bvh_mark_built",
     "rt_render_tiles_counters", "rt_tiles_for_rank",
     "rt_render_tiles_device", "rt_unpack_tiles_device", "rt_scene_stream", "rt_scene_sync",
     "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_trace",
@@ -108,6 +109,9 @@ def lib() -> C.CDLL:
         "rt_render_path": [P, cam, P, C.c_float, u32, u32, u32, u32, P, P, C.POINTER(dbl)],
         "rt_render_path_device": [P, cam, P, C.c_float, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_path_work": [P, cam, P, C.c_float, u32, u32, u32, u32, P],
+        "rt_bvh_prepare": [P],
+        "rt_bvh_device_sections": [P, u32, P, P, P],
+        "rt_bvh_mark_built": [P],
         "rt_render_device": [P, cam, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_tiles_counters": [P, cam, u32, u32, u32, u32, u32, P],
         "rt_render_tiles_device": [P, cam, u32, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],

@@ -147,6 +147,7 @@ rt_status rt_config_set(const char* key, int64_t value) {
     if (k == "trace.variant" && value >= 0 && value <= 2) rt::g_trace_config.variant = (uint32_t)value;
     else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
+    else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) rt::g_trace_config.wg_tiles = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) rt::g_trace_config.stage_events = (uint32_t)value;
     else if (k == "timing.event_fence" && (value == 0 || value == 1)) rt::g_trace_config.event_fence = (uint32_t)value;
@@ -469,6 +470,35 @@ rt_status rt_bvh_load(rt_scene* s, const char* path) {
         s->built = false;
         return fail(RT_EIO, std::string(path) + ": trailing bytes in BVH cache");
     }
+    s->times = rt_build_times{};
+    s->built = true;
+    return RT_OK;
+}
+
+// Device-resident BVH exchange (SURVEY.md §8(e) "rank 0 builds and then
+// broadcasts"): the same sections as the RTBVH1 file, as device pointers.
+rt_status rt_bvh_prepare(rt_scene* s) {
+    if (!s) return fail(RT_EINVAL, "null scene");
+    return upload(s);
+}
+
+rt_status rt_bvh_device_sections(rt_scene* s, uint32_t max, void** ptrs, uint64_t* bytes, uint32_t* count_out) {
+    if (!s || !count_out || (max && (!ptrs || !bytes))) return fail(RT_EINVAL, "null argument");
+    if (!s->uploaded) return fail(RT_EINVAL, "scene not prepared (rt_bvh_prepare or rt_bvh_build)");
+    const std::vector<BvhSection> secs = bvh_sections(s);
+    *count_out = (uint32_t)secs.size();
+    for (uint32_t i = 0; i < max && i < secs.size(); ++i) {
+        ptrs[i] = secs[i].dev;
+        bytes[i] = secs[i].bytes;
+    }
+    return RT_OK;
+}
+
+rt_status rt_bvh_mark_built(rt_scene* s) {
+    if (!s) return fail(RT_EINVAL, "null scene");
+    if (!s->uploaded) return fail(RT_EINVAL, "scene not prepared (rt_bvh_prepare)");
+    HIPR(hipSetDevice(s->device));
+    HIPR(hipDeviceSynchronize());  // the caller's writes (any stream) land before the first render
     s->times = rt_build_times{};
     s->built = true;
     return RT_OK;

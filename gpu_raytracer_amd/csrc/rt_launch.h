@@ -78,6 +78,7 @@ struct TraceConfig {
     uint32_t variant = 0;       // 0 wide per-pixel (default), 1 wide pool with refill, 2 binary per-pixel
     uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
     uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
+    uint32_t wg_tiles = 64;     // same, for one rank's tiles of a multi-GPU frame (nranks > 1)
     uint32_t stack_cap = 14;    // wide stack entries used, <= kWideStack (tests force the overflow path)
     uint32_t path_wave = 1;     // path mode: 0 megakernel, 1 wavefront (default: faster on soup-1M and Sponza)
     uint32_t path_wg = 64;      // path megakernel: threads per block (64 = 8x8 quadrant, 256 = 16x16 tile)

@@ -1147,7 +1147,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     // wide (4-ary) traversal unless asked for the binary one: variant 2, no
     // K7w records (stage entry points), n < 2, or binary work counters
     const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2 && !binary_counts;
-    const bool small = g_trace_config.wg == 64;
+    const bool small = (nranks > 1 ? g_trace_config.wg_tiles : g_trace_config.wg) == 64;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
     hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
                        cam, w, h, spp, rank, nranks, tilesX, H, R, counters)

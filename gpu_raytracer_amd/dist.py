@@ -39,6 +39,34 @@ def rays_of_rank(w: int, h: int, spp: int, rank: int, nranks: int) -> int:
     return n * spp
 
 
+class _DeviceBytes:
+    """A library-owned device buffer seen by torch without a copy
+    (__cuda_array_interface__; the HIP device pointer on ROCm)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 2}
+
+
+def bvh_tensors(scene, device) -> list:
+    """The scene's device BVH sections (rt_bvh_device_sections) as uint8
+    tensors aliasing the library's buffers."""
+    return [torch.as_tensor(_DeviceBytes(p, n), device=device) for p, n in scene.device_sections() if n]
+
+
+def broadcast_bvh(scene, device, src: int = 0) -> int:
+    """SURVEY.md §8(e)'s alternative to the replicated build: rank `src` has
+    built; every other rank has called scene.prepare().  Broadcasts the BVH
+    sections in place (RCCL over xGMI with the 'nccl' backend) and marks the
+    receivers built.  Returns the bytes moved per receiver."""
+    ts = bvh_tensors(scene, device)
+    for t in ts:
+        dist.broadcast(t, src=src)
+    if dist.get_rank() != src:
+        torch.cuda.synchronize(device)
+        scene.mark_built()
+    return sum(t.numel() for t in ts)
+
+
 def gather_slabs(slab: torch.Tensor, rank: int, world: int, gather_list=None, out: torch.Tensor | None = None):
     """Gather every rank's slab (same shape) to rank 0.  On rank 0 returns the
     concatenation [rank][slab] (written into `out` when given)."""

@@ -218,6 +218,22 @@ class Scene:
         call("rt_render_path_work", self._h, C.byref(cam), _p(L), float(sky), int(max_depth), w, h, spp, _p(c))
         return c
 
+    def prepare(self):
+        """Upload + allocate without building (a receiver of a broadcast BVH)."""
+        call("rt_bvh_prepare", self._h)
+
+    def device_sections(self):
+        """[(device pointer, bytes)] of the BVH buffers (RTBVH1 sections)."""
+        cnt = C.c_uint32()
+        call("rt_bvh_device_sections", self._h, 0, None, None, C.byref(cnt))
+        ptrs = (C.c_void_p * cnt.value)()
+        sizes = (C.c_uint64 * cnt.value)()
+        call("rt_bvh_device_sections", self._h, cnt.value, ptrs, sizes, C.byref(cnt))
+        return [(int(ptrs[i] or 0), int(sizes[i])) for i in range(cnt.value)]
+
+    def mark_built(self):
+        call("rt_bvh_mark_built", self._h)
+
     def render_counters(self, cam: rt_camera, w: int, h: int, spp: int = 1) -> np.ndarray:
         """§9.7 binary-traversal counters (the oracle's): nodes fetched, tris tested."""
         c = np.zeros(2, np.uint64)

@@ -88,6 +88,17 @@ rt_status rt_bvh_build(rt_scene* s, double* ms_out);
  * the build ran with rt_config_set("build.stage_events", 1) (0 otherwise --
  * the extra events cost GPU time, so timed builds run without them) */
 rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out);
+/* Device-resident BVH exchange ("rank 0 builds and then
+ * broadcasts", the alternative to every rank building its replica):
+ * rt_bvh_prepare uploads the soup and allocates the BVH buffers without
+ * building; rt_bvh_device_sections lists the device buffers that make up a
+ * built BVH (the RTBVH1 sections: params, sorted keys, sorted vals, nodes,
+ * parent, tri_s, wide records) -- a receiver fills them (e.g. an RCCL
+ * broadcast from a rank that built) and calls rt_bvh_mark_built.  count_out
+ * = number of sections (call with max = 0 to size the arrays). */
+rt_status rt_bvh_prepare(rt_scene* s);
+rt_status rt_bvh_device_sections(rt_scene* s, uint32_t max, void** ptrs, uint64_t* bytes, uint32_t* count_out);
+rt_status rt_bvh_mark_built(rt_scene* s);
 /* Read back the device BVH (any pointer may be NULL): nodes[2n-1],
  * sorted keys/vals[n], parent[2n-1], bounds[9] = lo[3], hi[3], inv[3]. */
 rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* sorted_keys,
@@ -207,7 +218,8 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * grid (0 = resident capacity); "trace.stack_cap" (1..14) wide-traversal
  * stack entries -- rays that need more are re-traced by the binary
  * traversal; "trace.wg" 64/256 threads per block (8x8 quadrant / 16x16
- * tile).  Path mode: "path.wavefront" 0 = megakernel ("path.wg" 64/256
+ * tile), default 256; "trace.wg_tiles" the same for one rank's tiles of a
+ * multi-GPU frame (rt_render_tiles_device), default 64.  Path mode: "path.wavefront" 0 = megakernel ("path.wg" 64/256
  * threads per block), 1 = wavefront schedule with per-depth ray queues
  * (default); "path.sort" 0..4 = top key bytes each queue is radix-sorted by
  * for coherence (ray kind, direction octant, Morton code of the origin; 0 =
