@@ -83,6 +83,16 @@ def lib():
     return _lib
 
 
+def default_threads() -> int:
+    """Host threads for the oracle's traces: the CPUs this process may use,
+    at most 16 (the GPU box's CPU share; os.cpu_count() shows the machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
 def _p(a: np.ndarray):
     assert a.flags["C_CONTIGUOUS"]
     return a.ctypes.data_as(C.c_void_p)
@@ -178,7 +188,7 @@ def trace(nodes, tris, cam: Camera, w, h, spp=1, row0=0, row_step=1, nthreads=No
     cnt = np.zeros(2, np.uint64)
     nd = np.ascontiguousarray(nodes) if len(nodes) else np.zeros(1, NODE_DTYPE)
     tr = tris if n else np.zeros((1, 9), np.float32)
-    nthreads = nthreads or (os.cpu_count() or 1)
+    nthreads = nthreads or default_threads()
     lib().orc_trace(_p(nd), n, _p(tr), C.byref(cam), w, h, spp, row0, row_step, _p(hits), _p(cnt), int(nthreads))
     return hits[: w * h * spp], cnt
 
@@ -195,7 +205,7 @@ def render_shadow(nodes, tris, cam: Camera, w, h, spp, light, ambient, nthreads=
     nd = np.ascontiguousarray(nodes) if len(nodes) else np.zeros(1, NODE_DTYPE)
     tr = tris if n else np.zeros((1, 9), np.float32)
     L = np.ascontiguousarray(light, np.float32).reshape(3)
-    nthreads = nthreads or (os.cpu_count() or 1)
+    nthreads = nthreads or default_threads()
     lib().orc_render_shadow(_p(nd), n, _p(tr), C.byref(cam), w, h, spp, _p(L), float(ambient), _p(hits), _p(rgba),
                             _p(cnt), int(nthreads))
     return hits[: w * h * spp], rgba[: w * h * 4], cnt
@@ -211,7 +221,7 @@ def render_path(nodes, tris, cam: Camera, w, h, spp, light, sky, max_depth, nthr
     nd = np.ascontiguousarray(nodes) if len(nodes) else np.zeros(1, NODE_DTYPE)
     tr = tris if n else np.zeros((1, 9), np.float32)
     L = np.ascontiguousarray(light, np.float32).reshape(3)
-    nthreads = nthreads or (os.cpu_count() or 1)
+    nthreads = nthreads or default_threads()
     lib().orc_render_path(_p(nd), n, _p(tr), C.byref(cam), w, h, spp, _p(L), float(sky), int(max_depth), _p(hits),
                           _p(rgba), _p(cnt), int(nthreads))
     return hits[: w * h * spp], rgba[: w * h * 4], cnt
