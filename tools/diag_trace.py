@@ -32,7 +32,10 @@ for _ in range(3):
 print("render ms", ms)
 nbq = ((w + 15) // 16) * ((h + 15) // 16)
 cbuf = np.zeros(nbq * 16, np.uint64)
-s.render_counters(cam, w, h, 1)
+if len(sys.argv) > 2 and sys.argv[2] == "wide":
+    s.render_work(cam, w, h, 1)  # the running (wide) kernel's own record counts
+else:
+    s.render_counters(cam, w, h, 1)  # binary traversal node counts
 assert L.rt_debug_stamps(2, cbuf.ctypes.data, cbuf.nbytes) == 0
 cst = cbuf.reshape(nbq * 4, 4).astype(np.int64)
 mx = cst[:, 3] & 0xFFFFFFFF
