@@ -221,6 +221,19 @@ def main():
     barrier()
     wall = time.perf_counter() - t0
     per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, gather (ms)
+    # the same frame with row-major tile dispatch (untimed by the step contract):
+    # the timed steps dispatch tiles longest-first from the previous frame's
+    # per-tile wave times (trace.tile_order 1, DESIGN.md "Tile order")
+    R.config_set("trace.tile_order", 0)
+    rm = []
+    for _ in range(6):
+        if world == 1:
+            rm.append(scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True))
+        else:
+            rm.append(scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
+                                                timed=True))
+    R.config_set("trace.tile_order", 1)
+    trace_ms_row_major = float(np.median(rm[1:]))
     # per-stage breakdown from one extra, untimed build with the stage events
     # on (each adds a little to the GPU timeline, so the timed steps run without)
     R.config_set("build.stage_events", 1)
@@ -307,6 +320,9 @@ def main():
             "build_ms": round(build_ms, 4),
             "trace_ms": round(trace_ms, 4),
             "trace_ms_min": round(trace_ms_min, 4),
+            "tile_order": "longest-first from the previous frame's per-tile wave times (32 KB cost map per frame "
+                          "shape; the first frame runs row-major)",
+            "trace_ms_row_major_rank0": round(trace_ms_row_major, 4),
             "gather_ms": round(gather_ms, 4),
             "bvh_exchange": bvh_exchange,
             "frame_mrays_per_s": round(rays / (wall / args.steps) / 1e6, 2),

@@ -39,6 +39,10 @@ struct rt_scene {
     size_t rgba_cap = 0;
     unsigned long long* d_ctr = nullptr;
     uint32_t* d_work = nullptr;  // pool-trace unit counters
+    void* d_order = nullptr;     // tile-order state: [order][cost A][cost B] per tile slot
+    size_t order_cap = 0;
+    rt::TileSched sched;
+    uint32_t sched_key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the cost map
     rt::PathBufs path;           // wavefront path-mode state (grown on demand)
     hipEvent_t r0 = nullptr, r1 = nullptr;
 };
@@ -117,6 +121,33 @@ rt_status grow(void** p, size_t* cap, size_t need) {
     return RT_OK;
 }
 
+// Tile-order state for a frame of this shape (DESIGN.md "Tile order"): the
+// cost map of the previous frame with the same w, h, spp, rank, nranks
+// drives this frame's dispatch order (nullptr: row-major, no map).
+rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks) {
+    const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
+    const uint32_t key[5] = {w, h, spp, rank, nranks};
+    const bool same = std::memcmp(key, s->sched_key, sizeof(key)) == 0;
+    const size_t need = 3ull * nb * 4;
+    if (!same || s->order_cap < need) {
+        if (grow(&s->d_order, &s->order_cap, need)) return nullptr;
+        uint32_t* b = static_cast<uint32_t*>(s->d_order);
+        s->sched.order = b;
+        s->sched.cost_prev = b + nb;
+        s->sched.cost_cur = b + 2 * nb;
+        s->sched.have_prev = false;
+        std::memcpy(s->sched_key, key, sizeof(key));
+    }
+    return &s->sched;
+}
+
+// after a launch that used sched_for: this frame's map becomes the previous one
+void sched_done(rt_scene* s) {
+    if (!rt::g_trace_config.tile_order) return;
+    std::swap(s->sched.cost_prev, s->sched.cost_cur);
+    s->sched.have_prev = true;
+}
+
 rt::CamF camf(const rt_camera* c) {
     rt::CamF f;
     std::memcpy(&f, c, sizeof(f));
@@ -148,6 +179,7 @@ rt_status rt_config_set(const char* key, int64_t value) {
     else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
     else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) rt::g_trace_config.wg_tiles = (uint32_t)value;
+    else if (k == "trace.tile_order" && (value == 0 || value == 1)) rt::g_trace_config.tile_order = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) rt::g_trace_config.stage_events = (uint32_t)value;
     else if (k == "timing.event_fence" && (value == 0 || value == 1)) rt::g_trace_config.event_fence = (uint32_t)value;
@@ -250,6 +282,7 @@ void rt_scene_free(rt_scene* s) {
         if (s->d_rgba) (void)hipFree(s->d_rgba);
         if (s->d_ctr) (void)hipFree(s->d_ctr);
         if (s->d_work) (void)hipFree(s->d_work);
+        if (s->d_order) (void)hipFree(s->d_order);
         for (auto& e : s->ev.e) (void)hipEventDestroy(e);
         (void)hipEventDestroy(s->r0);
         (void)hipEventDestroy(s->r1);
@@ -518,8 +551,9 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     HIPR(hipEventRecord(s->r0, s->stream));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
                                     false, hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, false, s->d_work,
-                                    s->stream);
+                                    sched_for(s, w, h, spp, 0, 1), s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
+    sched_done(s);
     HIPR(hipEventRecord(s->r1, s->stream));
     HIPR(hipStreamSynchronize(s->stream));
     float ms = 0;
@@ -685,7 +719,8 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
     HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
-                                    nranks, packed, nullptr, nullptr, s->d_ctr, binary, s->d_work, s->stream);
+                                    nranks, packed, nullptr, nullptr, s->d_ctr, binary, s->d_work, nullptr,
+                                    s->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(s->stream));
     HIPR(hipMemcpy(counters_out, s->d_ctr, 16, hipMemcpyDeviceToHost));
@@ -717,8 +752,10 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
-                                    false, d_hits, d_rgba, nullptr, false, s->d_work, hs);
+                                    false, d_hits, d_rgba, nullptr, false, s->d_work,
+                                    sched_for(s, w, h, spp, 0, 1), hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
+    sched_done(s);
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
         HIPR(hipEventSynchronize(s->r1));
@@ -743,8 +780,10 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
     if (ms_out) HIPR(hipEventRecord(s->r0, hs));
     hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
-                                    nranks, true, d_packed_hits, d_packed_rgba, nullptr, false, s->d_work, hs);
+                                    nranks, true, d_packed_hits, d_packed_rgba, nullptr, false, s->d_work,
+                                    sched_for(s, w, h, spp, rank, nranks), hs);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
+    sched_done(s);
     if (ms_out) {
         HIPR(hipEventRecord(s->r1, hs));
         HIPR(hipEventSynchronize(s->r1));
@@ -892,7 +931,7 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
     HIPR(dw.alloc(4096));
     HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
     HIPR(rt::launch_trace(dn.p, nullptr, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
-                          counters ? dc.as<unsigned long long>() : nullptr, true, dw.as<uint32_t>(), 0));
+                          counters ? dc.as<unsigned long long>() : nullptr, true, dw.as<uint32_t>(), nullptr, 0));
     HIPR(hipDeviceSynchronize());
     if (hits) HIPR(hipMemcpy(hits, dh.p, nh * 16, hipMemcpyDeviceToHost));
     if (rgba) HIPR(hipMemcpy(rgba, dr.p, (size_t)w * h * 4, hipMemcpyDeviceToHost));
@@ -971,6 +1010,11 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path) {
 #ifdef RT_STAMPS
 // diagnostic build only: copy the per-block phase stamps (8 x u64 per block)
 // of the build kernels (which = 0) or the sort kernels (which = 1)
+rt_status rt_debug_tile_order(const uint32_t* d_order) {
+    rt::g_trace_config.order_override = d_order;
+    return RT_OK;
+}
+
 rt_status rt_debug_stamps(int which, void* out, size_t bytes) {
     HIPR(hipDeviceSynchronize());
     HIPR(which == 2 ? rt::read_stamps_trace(out, bytes) : which ? rt::read_stamps_sort(out, bytes) : rt::read_stamps_build(out, bytes));

@@ -86,9 +86,21 @@ struct TraceConfig {
     uint32_t path_batch = 0;    // wavefront: paths per batch (0 = 4M)
     uint32_t stage_events = 0;  // build: record the per-stage events (rt_bvh_build_times); else total only
     uint32_t event_fence = 0;   // timing events with the system-scope fence (scenes created afterwards)
+    uint32_t tile_order = 1;    // 1: longest-first from the previous same-size frame's wave times; 0: row-major
+    const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
+};
+
+// Per-launch tile scheduling state (owned by the scene, one per frame shape).
+struct TileSched {
+    uint32_t* order = nullptr;      // [nb] dispatch index -> tile slot
+    uint32_t* cost_prev = nullptr;  // [nb] previous frame's per-tile wave time
+    uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
+    bool have_prev = false;
 };
 extern TraceConfig g_trace_config;
 
+// sched: the scene's tile-order state for this frame shape (nullptr:
+// row-major order, no cost map).
 // wnodes: the K7w wide records (nullptr: binary traversal only).  With
 // binary_counts the kernel is the binary one, so `counters` are the §9.7
 // node/triangle counts the oracle reports; otherwise they count the running
@@ -96,7 +108,7 @@ extern TraceConfig g_trace_config;
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tri_s, uint32_t n, const CamF& cam,
                         uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
                         void* hits, void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
-                        hipStream_t s);
+                        TileSched* sched, hipStream_t s);
 // Shadow mode: primary hits into `hits`, Lambert + shadow-ray
 // shaded image into `rgba`; tris = the scene's AoS triangles (normals).
 hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,

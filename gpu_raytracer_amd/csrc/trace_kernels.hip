@@ -392,7 +392,9 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                unsigned long long* __restrict__ counters,
-                                               const float* __restrict__ tris = nullptr, Light lt = Light{}) {
+                                               const float* __restrict__ tris = nullptr, Light lt = Light{},
+                                               const uint32_t* __restrict__ order = nullptr,
+                                               uint32_t* __restrict__ cost_out = nullptr) {
     __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     // tile slot from the block id: consecutive tiles go to different XCDs
@@ -403,7 +405,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
     // slot and LDS at once instead of waiting for the tile's slowest wave.
     constexpr uint32_t WPB = NT / 64;
     const uint32_t gw = blockIdx.x * WPB + (threadIdx.x >> 6);  // global wave id
-    const uint32_t slot = gw >> 2;
+    const uint32_t slot = order ? order[gw >> 2] : gw >> 2;  // dispatch order -> tile slot
     const uint32_t t = rank + slot * nranks;
     const uint32_t tx = t % tilesX, ty = t / tilesX;
     const uint32_t l = threadIdx.x & 63, w = gw & 3;
@@ -411,6 +413,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
     uint32_t cn = 0, ct = 0;
+    const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #ifdef RT_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -509,6 +512,10 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             atomicAdd(&counters[0], a);
             atomicAdd(&counters[1], bsum);
         }
+    }
+    if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
+        atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
     }
 }
 
@@ -1091,6 +1098,73 @@ __global__ void k_minmax(uint32_t count, const float* __restrict__ a, const floa
 }
 
 
+// ---------------------------------------------------------------- tile order
+// DESIGN.md "Tile order".  A frame's time is set by its longest waves (~1 us
+// per dependent record fetch, up to ~200 fetches for rays grazing the soup):
+// dispatched in row-major order they start late and the GPU idles behind
+// them.  Each wave of k_trace records its duration into cost[slot]
+// (atomicMax over the tile's waves); the next frame of the same size
+// dispatches its tiles longest-first from that map.  The order only decides
+// which block renders which tile, never a pixel's result.
+//
+// Counting sort, costliest first, on a log-scale key: 8 buckets per octave
+// of the duration (10-ns clock ticks).  Order within a bucket is free.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t d) {
+    if (d < 8) return d;
+    const uint32_t e = 31u - (uint32_t)__clz((int)d);  // d in [2^e, 2^(e+1)), e >= 3
+    return min(255u, (e - 2) * 8 + ((d >> (e - 3)) & 7u));
+}
+
+constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per rank (4K frames)
+
+__global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict__ cost, uint32_t nb,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_sum[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (tid < 256) s_hist[tid] = 0u;
+    __syncthreads();
+    // each cost is read once: both passes see the same buckets, so `order`
+    // is a permutation even if the map were being rewritten meanwhile
+    uint8_t bk[kOrderPerThread];
+#pragma unroll
+    for (uint32_t j = 0; j < kOrderPerThread; ++j) {
+        const uint32_t i = tid + j * 1024;
+        bk[j] = i < nb ? (uint8_t)(255u - cost_bucket(cost[i])) : 0;
+        if (i < nb) atomicAdd(&s_hist[bk[j]], 1u);
+    }
+    __syncthreads();
+    if (tid < 256) {  // exclusive scan of 256 buckets: 4 waves of 64
+        const uint32_t v = s_hist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_sum[wv] = x;
+    }
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
+        const uint32_t v = s_hist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        s_hist[tid] = pre + x - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < kOrderPerThread; ++j) {
+        const uint32_t i = tid + j * 1024;
+        if (i < nb) order[atomicAdd(&s_hist[bk[j]], 1u)] = i;
+    }
+}
+
 // ================================================================ launchers
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
     const uint32_t nt = ((w + 15) / 16) * ((h + 15) / 16);
@@ -1102,7 +1176,8 @@ TraceConfig g_trace_config;
 
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tris, uint32_t n, const CamF& c,
                         uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits,
-                        void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work, hipStream_t s) {
+                        void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
+                        TileSched* sched, hipStream_t s) {
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
     if (!nb) return hipSuccess;
     Cam cam;
@@ -1148,9 +1223,22 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     // K7w records (stage entry points), n < 2, or binary work counters
     const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2 && !binary_counts;
     const bool small = (nranks > 1 ? g_trace_config.wg_tiles : g_trace_config.wg) == 64;
+    // costliest tiles first from the previous frame's map (DESIGN.md "Tile order")
+    const uint32_t* order = nullptr;
+    uint32_t* cost_out = nullptr;
+    if (sched && g_trace_config.tile_order && nb <= 1024 * kOrderPerThread) {
+        if (sched->have_prev) {
+            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order);
+            order = sched->order;
+        }
+        hipError_t me = hipMemsetAsync(sched->cost_cur, 0, (size_t)nb * 4, s);
+        if (me != hipSuccess) return me;
+        cost_out = sched->cost_cur;
+    }
+    if (g_trace_config.order_override) order = g_trace_config.order_override;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
     hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
-                       cam, w, h, spp, rank, nranks, tilesX, H, R, counters)
+                       cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, cost_out)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \

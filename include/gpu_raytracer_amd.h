@@ -219,7 +219,10 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * stack entries -- rays that need more are re-traced by the binary
  * traversal; "trace.wg" 64/256 threads per block (8x8 quadrant / 16x16
  * tile), default 256; "trace.wg_tiles" the same for one rank's tiles of a
- * multi-GPU frame (rt_render_tiles_device), default 64.  Path mode: "path.wavefront" 0 = megakernel ("path.wg" 64/256
+ * multi-GPU frame (rt_render_tiles_device), default 64; "trace.tile_order"
+ * 1 = dispatch a frame's tiles longest-first from the previous frame of the
+ * same shape's per-tile wave times (a 32 KB cost map per scene; the first
+ * frame of a shape runs row-major), 0 = row-major always.  Path mode: "path.wavefront" 0 = megakernel ("path.wg" 64/256
  * threads per block), 1 = wavefront schedule with per-depth ray queues
  * (default); "path.sort" 0..4 = top key bytes each queue is radix-sorted by
  * for coherence (ray kind, direction octant, Morton code of the origin; 0 =

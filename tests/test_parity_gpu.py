@@ -301,3 +301,39 @@ def test_tiled_render_matches_full(R, oracle):
             R.unpack_tiles_device(slabs.data_ptr(), tmax, w, h, P, img.data_ptr())
             torch.cuda.synchronize()
             assert np.array_equal(img.cpu().numpy().view(np.uint8), full), P
+
+
+def test_tile_order_successive_frames(R, oracle):
+    """Longest-first tile dispatch from the previous frame's cost map (the
+    default): the 1st frame runs row-major, later frames reordered -- every
+    frame bit-identical to the oracle, full image and per-rank tiles alike,
+    and a frame of another shape starts a fresh map."""
+    import torch
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    tris = soup(oracle, 60000, 12)
+    exp = oracle.build(tris)
+    R.config_set("trace.tile_order", 1)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for (w, h, spp) in [(256, 144, 1), (256, 144, 1), (200, 120, 2), (256, 144, 1), (256, 144, 1)]:
+            cam = _cam(R, SOUP_VIEW, w, h)
+            ocam = oracle.camera_look_at(SOUP_VIEW.eye, SOUP_VIEW.at, SOUP_VIEW.up, SOUP_VIEW.vfov, w, h)
+            eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
+            er = oracle.shade(eh, w, h, spp)
+            hits, rgba, _ = s.render(cam, w, h, spp)
+            assert np.array_equal(rgba, er)
+            assert np.array_equal(hits["prim"], eh["prim"])
+            assert np.array_equal(bits(hits["t"]), bits(eh["t"]))
+        w, h, spp, P = 256, 144, 1, 3
+        cam = _cam(R, SOUP_VIEW, w, h)
+        _, full, _ = s.render(cam, w, h, spp, hits=False)
+        tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
+        for _ in range(3):  # per-rank maps: frames 2 and 3 reordered
+            slabs = torch.zeros((P, tmax * 256), dtype=torch.int32, device="cuda")
+            for r in range(P):
+                s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr())
+            s.sync()
+            img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+            R.unpack_tiles_device(slabs.data_ptr(), tmax, w, h, P, img.data_ptr())
+            torch.cuda.synchronize()
+            assert np.array_equal(img.cpu().numpy().view(np.uint8), full)

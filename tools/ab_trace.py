@@ -20,17 +20,22 @@ hits = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
 sel = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "2"]
 variants = []
 for v in sel:
+    order = 1
+    if "o" in v and not v.startswith("pool"):  # e.g. 0o0: row-major tile order (default 1: cost-map order)
+        v, order = v.split("o")[0], int(v.split("o")[1])
+    base = {"trace.tile_order": order}
+    tag = "longest-first" if order else "row-major"
     if v == "0":
-        variants.append(("wide (default)", {"trace.variant": 0, "trace.wg": 256}))
+        variants.append((f"wide ({tag})", {**base, "trace.variant": 0, "trace.wg": 256}))
     elif v == "0s":
-        variants.append(("wide, 64-thread blocks", {"trace.variant": 0, "trace.wg": 64}))
+        variants.append((f"wide, 64-thread blocks ({tag})", {**base, "trace.variant": 0, "trace.wg": 64}))
     elif v == "2s":
-        variants.append(("binary, 64-thread blocks", {"trace.variant": 2, "trace.wg": 64}))
+        variants.append((f"binary, 64-thread blocks ({tag})", {**base, "trace.variant": 2, "trace.wg": 64}))
     elif v == "2":
-        variants.append(("binary (deferred leaf test)", {"trace.variant": 2, "trace.wg": 256}))
+        variants.append((f"binary ({tag})", {**base, "trace.variant": 2, "trace.wg": 256}))
     elif v.startswith("pool"):  # pool[-bB]: wide with per-lane refill, B blocks (0 = resident capacity)
         b = int(v.split("-b")[1]) if "-b" in v else 0
-        variants.append((v, {"trace.variant": 1, "trace.blocks": b}))
+        variants.append((v, {**base, "trace.variant": 1, "trace.blocks": b}))
 cnts = {}
 for name, cfg in variants:
     for k, v in cfg.items():
@@ -51,6 +56,9 @@ for r in range(rounds):
         if ref is None:
             ref = out.copy()
         assert np.array_equal(out, ref), name
+R.config_set("trace.tile_order", 1)
+R.config_set("trace.variant", 0)
+R.config_set("trace.wg", 256)
 for name, _ in variants:
     t = np.array(times[name])
     print(f"{name:<36s} median {np.median(t):8.3f} ms  min {t.min():8.3f}  -> {w*h*spp/np.median(t)/1e3:8.1f} Mrays/s")
