@@ -340,8 +340,11 @@ def main():
                                          if kernel_bytes else None),
                          "note": "algorithmic bytes (SURVEY.md §8(d): 32/node + 36/tri + 16/ray over the §9.7 "
                                  "binary traversal's counters); kernel_bytes = what the wide kernel requests "
-                                 "(64/record + 48/tri record + 20/ray); the scene is Infinity-Cache resident, "
-                                 "so algorithmic GB/s can exceed DRAM traffic"},
+                                 "(64/record + 48/tri record + 20/ray). frac can exceed 1: the §8(d) model "
+                                 "charges every binary node visit 32 B as if from HBM, while the kernel fetches "
+                                 "~4x fewer (wide) records from the Infinity-Cache-resident structures; 'traffic' "
+                                 "is the PMC-measured HBM bytes per launch. The kernel is bound by dependent-fetch "
+                                 "latency and VALU issue (DESIGN.md), not HBM bandwidth"},
             "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM},

@@ -20,13 +20,15 @@ s = R.Scene.generate_soup(n, 1)
 s.build()
 cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
-configs = [("wide 256", {"trace.variant": 0, "trace.wg": 256, "trace.wg_tiles": 256}),
-           ("wide 64", {"trace.variant": 0, "trace.wg": 64, "trace.wg_tiles": 64})]
+configs = [("row-major 256", {"trace.variant": 0, "trace.wg": 256, "trace.wg_tiles": 256, "trace.tile_order": 0}),
+           ("row-major 64", {"trace.variant": 0, "trace.wg": 64, "trace.wg_tiles": 64, "trace.tile_order": 0}),
+           ("ordered 256", {"trace.variant": 0, "trace.wg": 256, "trace.wg_tiles": 256, "trace.tile_order": 1}),
+           ("ordered 64", {"trace.variant": 0, "trace.wg": 64, "trace.wg_tiles": 64, "trace.tile_order": 1})]
 for name, cfg in configs:
     for k, v in cfg.items():
         R.config_set(k, v)
     full = np.median([s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), timed=True) for _ in range(6)][1:])
-    line = f"{name:<9s} full {full:.3f} ms |"
+    line = f"{name:<14s} full {full:.3f} ms |"
     for P in (2, 4, 8):
         t = []
         for r in range(P):
@@ -39,3 +41,4 @@ for name, cfg in configs:
 R.config_set("trace.variant", 0)
 R.config_set("trace.wg", 256)
 R.config_set("trace.wg_tiles", 64)
+R.config_set("trace.tile_order", 1)
