@@ -171,17 +171,18 @@ __device__ __forceinline__ bool slab_hit(const float* lo, const float* hi, const
 // truncation rounds down and the skip test stays conservative).  Slot `cap`
 // is the spare that takes the writes of children that are not pushed.
 struct WRay {
-    float d[3], invd[3];
+    float d[3], invd[3], oslack[3];
     float tb, hu, hv, ctn;
     uint32_t hp, cur, pend, sp, steps;
     bool fin;  // 1/d finite on every axis: the wide traversal applies
 };
 
-__device__ __forceinline__ void wray_init(const float* d, WRay& R) {
+__device__ __forceinline__ void wray_init(const float* o, const float* d, WRay& R) {
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         R.d[c] = d[c];
         R.invd[c] = 1.0f / d[c];
+        R.oslack[c] = fmaf(fabsf(o[c] * R.invd[c]), 0x1p-20f, 0x1p-126f);  // record_test's |o/d| term
     }
     R.fin = isfinite(R.invd[0]) && isfinite(R.invd[1]) && isfinite(R.invd[2]);
     R.tb = __builtin_inff(); R.hu = 0.0f; R.hv = 0.0f; R.hp = RT_SENT;
@@ -207,11 +208,69 @@ __device__ __forceinline__ void wray_setup(const Cam& cam, uint32_t x, uint32_t 
                                            uint32_t s, WRay& R) {
     float d[3];
     ray_dir(cam, x, y, W, spp, s, d);
-    wray_init(d, R);
+    wray_init(cam.eye, d, R);
 }
 
 __device__ __forceinline__ uint32_t bin_of(uint32_t ref, uint32_t L0) {
     return (ref & kWideLeaf) ? L0 + (ref & ~kWideLeaf) : ref;
+}
+
+// Conservative slab test of a record's four quantized child boxes, in
+// about half the VALU of the §9.7 formula (this is the traversal's inner
+// loop, and the kernel is VALU-issue bound).  Child plane p = org + q*2^e, so
+// §9.7's (p - o)*invd is computed as fma(q, B, A) with the per-record
+// A = (org - o)*invd and B = 2^e*invd, and each axis's near/far plane is
+// picked once per record by the sign of invd (q_lo <= q_hi for every valid
+// child), replacing 6 sub + 6 mul + 6 min/max per child by 6 fma.
+//
+// Exactness.  The internal-node tests only prune; the traversal stays exact
+// as long as a child is entered whenever §9.7's test of the child's EXACT box
+// b would hit (see the wide_step comment).  The fma form differs from §9.7 on
+// b by rounding: from A (2 roundings, <= 2u|A|), the fma (u|t|, |t| <=
+// |A| + 255|B|), §9.7's own two roundings (2u|t|), and the gap between the
+// real plane org + q*2^e and its rounded value, which the build compared with
+// b (<= u(|org| + 256*2^e)|invd| <= u(|A| + |o*invd| + 256|B|)); u = 2^-24.
+// In total less than u(6|A| + |o*invd| + 1021|B|) + denormal terms, so
+// widening each axis's interval by
+//     delta = 2^-20 (|A| + 256|B| + |o*invd|) + 2^-126
+// (16x that, R.oslack holds the ray's |o*invd| term) makes tn_fast <= tn_97
+// and tf_fast >= tf_97: a child §9.7 enters is always entered, and the stack
+// entry distance tn_fast stays a lower bound of §9.7's.  A record whose
+// delta is not small (huge 1/d, infinities) is treated as wild: every valid
+// child counts as hit with entry distance 0.  Returns that wild flag.
+__device__ __forceinline__ bool record_test(const WRay& R, const float* o, const uint4& w0, const uint4& w1,
+                                            const uint4& w2, bool (&hit)[4], float (&tn)[4]) {
+    const float org[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
+    const uint32_t qlo[3] = {w1.x, w1.y, w1.z}, qhi[3] = {w1.w, w2.x, w2.y};
+    float An[3], Af[3], B[3];
+    uint32_t qn[3], qf[3];
+    float dmax = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float scl = __uint_as_float(((w0.w >> (8 * c)) & 0xFFu) << 23);  // 2^e
+        B[c] = scl * R.invd[c];
+        const float A = (org[c] - o[c]) * R.invd[c];
+        const float dl = fmaf(fabsf(A), 0x1p-20f, fmaf(fabsf(B[c]), 0x1p-12f, R.oslack[c]));
+        dmax = fmaxf(dmax, dl);
+        An[c] = A - dl;
+        Af[c] = A + dl;
+        const bool neg = R.invd[c] < 0.0f;
+        qn[c] = neg ? qhi[c] : qlo[c];
+        qf[c] = neg ? qlo[c] : qhi[c];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        float tnear[3], tfar[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            tnear[c] = fmaf((float)((qn[c] >> (8 * i)) & 0xFFu), B[c], An[c]);
+            tfar[c] = fmaf((float)((qf[c] >> (8 * i)) & 0xFFu), B[c], Af[c]);
+        }
+        tn[i] = fmaxf(fmaxf(fmaxf(tnear[0], tnear[1]), tnear[2]), 0.0f);
+        const float tf = fminf(fminf(fminf(tfar[0], tfar[1]), tfar[2]), R.tb);
+        hit[i] = tn[i] <= tf;
+    }
+    return !(dmax < 0x1p90f);  // also true for NaN
 }
 
 template <int NT>
@@ -263,26 +322,14 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     if (!node) return 0;
     if (R.ctn > R.tb) { R.cur = RT_SENT; return 0; }
     if (COUNT) ++cn;
-    const float org[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
-    float scl[3];
-#pragma unroll
-    for (int c = 0; c < 3; ++c) scl[c] = __uint_as_float(((w0.w >> (8 * c)) & 0xFFu) << 23);  // 2^e
     const uint32_t flags = w0.w >> 24;
-    const bool wild = flags & kWideWild;
-    const uint32_t qlo[3] = {w1.x, w1.y, w1.z}, qhi[3] = {w1.w, w2.x, w2.y};
     const uint32_t ref[4] = {w2.z, w2.w, w3.x, w3.y};
     bool hit[4];
     float tn[4];
+    const bool wild = record_test(R, o, w0, w1, w2, hit, tn);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float lo[3], hi[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            lo[c] = wide_plane(org[c], (qlo[c] >> (8 * i)) & 0xFFu, scl[c]);
-            hi[c] = wide_plane(org[c], (qhi[c] >> (8 * i)) & 0xFFu, scl[c]);
-        }
-        const bool h = slab_hit(lo, hi, o, R.invd, R.tb, tn[i]);
-        hit[i] = ((flags >> (4 + i)) & 1u) && (h || wild);
+        hit[i] = ((flags >> (4 + i)) & 1u) && (hit[i] || wild);
         if (wild) tn[i] = 0.0f;
     }
     bool earlier[4];
@@ -314,7 +361,7 @@ __device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const 
                                           const float* d, float tmax, bool any, uint32_t* sref, uint16_t* stn,
                                           float& tb, float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
     WRay R;
-    wray_init(d, R);
+    wray_init(o, d, R);
     R.tb = tmax;
     const bool wide = R.fin && wnodes && n >= 2;
     int st = wide ? 0 : 2;
@@ -435,7 +482,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             uint32_t hp = RT_SENT;
             if (WIDE) {
                 WRay R;
-                wray_init(d, R);
+                wray_init(cam.eye, d, R);
                 int st = R.fin ? 0 : 2;
                 const char* nd = reinterpret_cast<const char*>(nodes);
                 while (st == 0) st = wide_step<COUNT, NT>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,

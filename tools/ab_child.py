@@ -1,0 +1,60 @@
+"""One measurement process for tools/ab_libs.py (RT_LIB selects the library).
+Prints one JSON line: primary trace ms (longest-first and row-major), the
+max-rank tiled trace at P=8, shadow and path frames, 1M build ms, and CRCs of
+every output so the libraries can be checked for identical results."""
+import json
+import os
+import sys
+import zlib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import gpu_raytracer_amd as R  # noqa: E402
+from gpu_raytracer_amd.scenes import SOUP_VIEW as V  # noqa: E402
+
+modes = sys.argv[1].split(",") if len(sys.argv) > 1 else ["trace", "rowmajor", "p8", "shadow", "path", "build"]
+w, h, spp = 1920, 1080, 1
+s = R.Scene.generate_soup(1_000_000, 1)
+s.build()
+cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+hits = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
+out = {}
+
+
+def crc(*ts):
+    c = 0
+    for t in ts:
+        c = zlib.crc32(t.cpu().numpy().tobytes(), c)
+    return c
+
+
+def med(f, k):
+    return float(np.median([f() for _ in range(k)]))
+
+
+if "build" in modes:
+    out["build"] = med(lambda: s.build(), 10)
+if "trace" in modes:
+    R.config_set("trace.tile_order", 1)
+    out["trace"] = med(lambda: s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True), 12)
+    out["crc_trace"] = crc(img, hits)
+if "rowmajor" in modes:
+    R.config_set("trace.tile_order", 0)
+    out["rowmajor"] = med(lambda: s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), timed=True), 8)
+    R.config_set("trace.tile_order", 1)
+if "p8" in modes:
+    P, t = 8, []
+    for r in range(P):
+        slab = torch.zeros(max(R.tiles_for_rank(w, h, r, P), 1) * 256, dtype=torch.int32, device="cuda")
+        t.append(med(lambda: s.render_tiles_device(cam, w, h, spp, r, P, slab.data_ptr(), timed=True), 5))
+    out["p8"] = max(t)
+if "shadow" in modes:
+    out["shadow"] = med(lambda: s.render_shadow_device(cam, w, h, spp, (2.0, 3.0, -2.0), 0.2, d_rgba=img.data_ptr(), timed=True), 6)
+    out["crc_shadow"] = crc(img)
+if "path" in modes:
+    out["path"] = med(lambda: s.render_path_device(cam, w, h, spp, (2.0, 3.0, -2.0), 0.3, 2, d_rgba=img.data_ptr(), timed=True), 4)
+    out["crc_path"] = crc(img)
+print(json.dumps(out), flush=True)
