@@ -172,6 +172,9 @@ __device__ __forceinline__ uint32_t quant(float c, float lo, float inv) {
 // one block = one radix-sort tile: kSortThreads x kTrisPerThread = 4096 prims
 static_assert(kSortThreads * kTrisPerThread == kSortTile, "K1 block must be one sort tile");
 
+// MSB: the histograms are of the bucket digit key >> kMsbShift ([tile][1024]
+// counts + [1024] totals, for launch_sort_msb) instead of the four bytes.
+template <bool MSB>
 __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict__ tris, uint32_t n,
                                                          BuildParams* __restrict__ params,
                                                          const float* __restrict__ partials, uint32_t nb,
@@ -218,11 +221,20 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
 #pragma unroll
     for (uint32_t q = 0; q < kTrisPerThread; ++q)
         if (q < cnt) {
+            if (MSB) {
+                atomicAdd(&hist[k8[q] >> kMsbShift], 1u);  // 30-bit keys: < 1024
+            } else {
 #pragma unroll
-            for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((k8[q] >> (8 * d)) & 0xFFu)], 1u);
+                for (int d = 0; d < 4; ++d) atomicAdd(&hist[d * 256 + ((k8[q] >> (8 * d)) & 0xFFu)], 1u);
+            }
         }
     __syncthreads();
-    if (threadIdx.x < 256) counts0[(uint64_t)blockIdx.x * 256 + threadIdx.x] = hist[threadIdx.x];
+    if (MSB) {
+        for (uint32_t j = threadIdx.x; j < kMsbBuckets; j += kSortThreads)
+            counts0[(uint64_t)blockIdx.x * kMsbBuckets + j] = hist[j];
+    } else if (threadIdx.x < 256) {
+        counts0[(uint64_t)blockIdx.x * 256 + threadIdx.x] = hist[threadIdx.x];
+    }
     for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) {
         const uint32_t v = hist[j];
         if (v) atomicAdd(&ghist[j], v);
@@ -503,49 +515,55 @@ __device__ __forceinline__ void kids_of(const uint4& tp, uint32_t L0, uint32_t& 
 }
 
 // One axis of one record: grid step 2^e with 255 * 2^e >= extent, then for
-// each valid child the outward-rounded planes.  (lo - origin) * 2^-e is off
-// by at most one step after rounding, so one check with wide_plane -- the
-// trace kernel's own arithmetic -- makes plane(qlo) <= lo and plane(qhi) >=
-// hi exact.  false: not representable (non-finite values, exponent > 119,
-// or a plane the one correction step cannot fix) -- the record goes wild.
-// Fixed 4 slots, fully unrolled (no dynamic register indexing -> no scratch).
-__device__ bool quant_axis(float olo, float ohi, const float (&clo)[4], const float (&chi)[4], uint32_t valid,
-                           uint32_t& qlo_w, uint32_t& qhi_w, int& e_out) {
+// each valid child the outward-rounded planes.  false: not representable
+// (non-finite values, exponent > 119, or origin + 255 * 2^e rounding below
+// hi) -- the record goes wild.  Fixed 4 slots, fully unrolled (no dynamic
+// register indexing -> no scratch).
+//
+// Why one correction step and no clamps suffice (planes are checked with
+// wide_plane, the trace kernel's own arithmetic):
+//  * every slot's planes lie in [olo, ohi] (X's box is the exact union of its
+//    entries' boxes; unused slots carry X's box), so c = fl(x - olo) * 2^-e is
+//    in [0, fl(ohi - olo) * 2^-e] subset [0, 255] by the choice of e: floor
+//    and ceil need no clamp;
+//  * lo side: f = floor(c) gives a real plane olo + f 2^e <= lo + u|lo - olo|;
+//    if its rounding lands above lo, f - 1 is a full step 2^e >= ext/255 >>
+//    u|lo - olo| lower, so its real value is < lo and its rounding is <= lo
+//    (lo is a float).  f = 0 never needs the step (olo <= lo);
+//  * hi side, symmetric: ceil, and one step up when the plane rounds below
+//    hi.  The step would leave the byte only if origin + 255 * 2^e rounds
+//    below hi <= ohi, which the per-axis check `top` rejects (wild).
+// A NaN/inf anywhere makes the slot sum non-finite (so does an overflowing
+// sum of finite values: wild, which is only conservative).
+__device__ __forceinline__ bool quant_axis(float olo, float ohi, const float (&clo)[4], const float (&chi)[4],
+                                           uint32_t valid, uint32_t& qlo_w, uint32_t& qhi_w, int& e_out) {
     const float ext = ohi - olo;
-    bool fin = isfinite(olo) && isfinite(ohi) && isfinite(ext) && ext >= 0.0f;
-    float lo[4], hi[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // unused slots quantize the origin: always representable
-        const bool v = (valid >> i) & 1u;
-        lo[i] = v ? clo[i] : olo;
-        hi[i] = v ? chi[i] : olo;
-        fin = fin && isfinite(lo[i]) && isfinite(hi[i]);
-    }
-    if (!fin) return false;
+    // callers pass X's own box in unused slots (inside [olo, ohi]); their
+    // bytes are written as 0
+    const float(&lo)[4] = clo;
+    const float(&hi)[4] = chi;
+    const float chk = (((lo[0] + lo[1]) + (lo[2] + lo[3])) + ((hi[0] + hi[1]) + (hi[2] + hi[3]))) + ext;
+    if (!isfinite(chk) || !(ext >= 0.0f)) return false;
     const uint32_t be = (__float_as_uint(ext) >> 23) & 0xFF;  // ext normal: 2^(be-127) <= ext
     int e = (ext > 0.0f && be) ? (int)be - 134 : -126;
     e = e < -126 ? -126 : e;
     e += (ldexpf(255.0f, e) < ext) ? 1 : 0;
     if (e > 119) return false;
-    // one pass: a plane that still misses after the one-step correction
-    // (origin + 255 * 2^e rounding below hi: far-apart magnitudes) makes the
-    // record wild instead of retrying with a coarser grid
     const float sc = wide_scale(e);
+    const bool top = !(wide_plane(olo, 255u, sc) < ohi);
     uint32_t lw = 0, hw = 0;
-    bool ok = true;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        float fl = fminf(fmaxf(floorf(ldexpf(lo[i] - olo, -e)), 0.0f), 255.0f);
-        fl = (fl > 0.0f && wide_plane(olo, (uint32_t)fl, sc) > lo[i]) ? fl - 1.0f : fl;
-        float fh = fminf(fmaxf(ceilf(ldexpf(hi[i] - olo, -e)), 0.0f), 255.0f);
-        fh = (fh < 255.0f && wide_plane(olo, (uint32_t)fh, sc) < hi[i]) ? fh + 1.0f : fh;
-        ok = ok && !(wide_plane(olo, (uint32_t)fh, sc) < hi[i]) && !(wide_plane(olo, (uint32_t)fl, sc) > lo[i]);
-        const uint32_t v = (valid >> i) & 1u;
-        lw |= (v ? (uint32_t)fl : 0u) << (8 * i);
-        hw |= (v ? (uint32_t)fh : 0u) << (8 * i);
+        float fl = floorf(ldexpf(lo[i] - olo, -e));
+        fl = fmaf(fl, sc, olo) > lo[i] ? fl - 1.0f : fl;
+        float fh = ceilf(ldexpf(hi[i] - olo, -e));
+        fh = fmaf(fh, sc, olo) < hi[i] ? fh + 1.0f : fh;
+        const bool v = (valid >> i) & 1u;
+        lw = __builtin_amdgcn_cvt_pk_u8_f32(v ? fl : 0.0f, (uint32_t)i, lw);
+        hw = __builtin_amdgcn_cvt_pk_u8_f32(v ? fh : 0.0f, (uint32_t)i, hw);
     }
     qlo_w = lw; qhi_w = hw; e_out = e;
-    return ok;
+    return top;
 }
 
 // Quantize and store the wide record of internal node X from its box and the
@@ -632,6 +650,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         uint4* __restrict__ wnodes) {
     constexpr int T = kRefitT, NW = T / 64, KW = 1024;
     static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
+    static_assert(sizeof(uint4) <= sizeof(Aabb), "topology words must fit the table buffer");
     __shared__ Aabb s_tab[T];          // key window first (uint32), then the odd sparse-table levels
     __shared__ Aabb s_box[2 * T];      // [0,T) leaves; [T,2T) the even levels, then local internal nodes
     __shared__ Aabb s_wpre[NW], s_wsuf[NW];
@@ -720,8 +739,10 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
             aabb_union(nbox, dst[qb]);
         }
     }
-    __syncthreads();  // the even-level buffer becomes the internal-node boxes
+    __syncthreads();  // the even-level buffer becomes the internal-node boxes; s_tab the topology words
+    uint4* s_topo = reinterpret_cast<uint4*>(s_tab);
     if (local) s_box[T + tid] = nbox;
+    s_topo[tid] = tp;
     if (tid == 0) s_cbase = cbase;
     __syncthreads();
     RT_STAMP(4);
@@ -732,7 +753,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         const Aabb bx = s_box[T + tid];
         store_node(nodes, k, bx, tp.x, tp.y);
         uint32_t node[4];
-        wide_entries(tp, L0, [&](uint32_t i) { return topo[i]; }, node);  // this block's words, L2-hot
+        wide_entries(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; }, node);  // children of a local node are local
         uint32_t slot[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -883,6 +904,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.table, (uint64_t)b.levels * b.m_blocks * 24);
     RT_ALLOC(b.cross, (uint64_t)cross_cap(b.m_blocks) * kCrossShards * 4);
     RT_ALLOC(b.counts, (uint64_t)4 * b.ntiles * 256 * 4);
+    RT_ALLOC(b.bstart, (kMsbBuckets + 4) * 4);
     RT_ALLOC(b.partials, (uint64_t)bounds_grid((uint32_t)N) * 24);
     RT_ALLOC(b.params, sizeof(BuildParams));
     RT_ALLOC(b.zero, (uint64_t)b.nzero * 4);
@@ -893,7 +915,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
 
 void free_build(BuildBufs& b) {
     void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.tri_s, b.parent, b.topo, b.wnodes,
-                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.partials, b.params, b.zero};
+                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.bstart, b.partials, b.params, b.zero};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = BuildBufs{};
@@ -907,10 +929,14 @@ hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, Bu
 
 static hipError_t launch_morton_impl(const float* tris, uint32_t n, BuildParams* params, const float* partials,
                                      uint32_t nb, uint32_t* keys, uint32_t* vals, uint32_t* ghist, uint32_t* counts0,
-                                     hipStream_t s) {
+                                     hipStream_t s, bool msb = false) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_morton, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials, nb, keys,
-                       vals, ghist, counts0);
+    if (msb)
+        hipLaunchKernelGGL(k_morton<true>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials, nb,
+                           keys, vals, ghist, counts0);
+    else
+        hipLaunchKernelGGL(k_morton<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials,
+                           nb, keys, vals, ghist, counts0);
     return hipGetLastError();
 }
 
@@ -977,13 +1003,16 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
     if (!n) hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
+    const bool msb = n >= 2 && n <= kMsbMaxN && g_trace_config.sort_msb;
     if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
-                                b.zero + kZHist, counts[0], s)) != hipSuccess)
+                                b.zero + kZHist, counts[0], s, msb)) != hipSuccess)
         return e;
     if ((e = rec(2)) != hipSuccess) return e;
     uint32_t* K[2] = {b.keys[0], b.keys[1]};
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
-    if ((e = launch_sort(K, V, n, b.zero + kZHist, counts, s)) != hipSuccess) return e;
+    if (msb) e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, s);
+    else e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
+    if (e != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;
     if (n) {
         const uint32_t m = cdiv(n, kRefitT);

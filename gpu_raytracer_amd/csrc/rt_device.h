@@ -69,6 +69,11 @@ constexpr int kSortThreads = 512;
 constexpr int kSortItems = 8;
 constexpr int kSortTile = kSortThreads * kSortItems;   // 4096 keys / tile
 constexpr uint32_t kPrefixInKernelMaxTiles = 256;      // <= 1M keys: cross-tile prefix inside k_scatter
+// MSB bucket sort (sort_kernels.hip): bucket = key >> kMsbShift of the 30-bit
+// Morton keys, used by the build for 2 <= n <= kMsbMaxN (<= 512 tiles)
+constexpr uint32_t kMsbShift = 20;
+constexpr uint32_t kMsbBuckets = 1024;
+constexpr uint32_t kMsbMaxN = 512u * kSortTile;
 constexpr int kRefitT = 512;                           // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
 

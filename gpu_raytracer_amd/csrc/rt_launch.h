@@ -21,7 +21,8 @@ struct BuildBufs {
     uint32_t* parent = nullptr;     // 2n-1, unified index space
     uint4* topo = nullptr;          // n-1 x {left, esc, range_lo, range_hi}
     uint4* wnodes = nullptr;        // n-1 x 64 B wide (4-ary) trace records, K7w
-    uint32_t* counts = nullptr;     // 4 x [tile][256] radix-sort tile digit counts
+    uint32_t* counts = nullptr;     // 4 x [tile][256] radix-sort tile digit counts (MSB: [tile][1024])
+    uint32_t* bstart = nullptr;     // [1025] MSB bucket starts
     float* prebuf = nullptr;        // n x 6: block-prefix AABB at crossing ends
     float* sufbuf = nullptr;        // n x 6: block-suffix AABB at crossing ends
     float* table = nullptr;         // sparse table over refit-block totals, levels x M x 6
@@ -87,6 +88,7 @@ struct TraceConfig {
     uint32_t stage_events = 0;  // build: record the per-stage events (rt_bvh_build_times); else total only
     uint32_t event_fence = 0;   // timing events with the system-scope fence (scenes created afterwards)
     uint32_t tile_order = 1;    // 1: longest-first from the previous same-size frame's wave times; 0: row-major
+    uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbMaxN, 0 = 4-pass LSB always
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };
 
@@ -147,6 +149,11 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const f
 // top `digits` (1..4) bytes of 32-bit keys, stable; returns the buffer index
 // (0 or 1) holding the result.  counts: tiles(n)*256 words; ghist: [4][256]
 // totals of all four digits (launch_digit_hist).
+// MSB bucket sort of 30-bit keys (2 <= n <= kMsbMaxN): keys[0]/vals[0] ->
+// keys[0]/vals[0] via keys[1]/vals[1]; ghist = [1024] bucket totals and
+// counts = [tile][1024] bucket counts (both from k_morton<true>).
+hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
+                           uint32_t* bstart, hipStream_t s);
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
                            uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,

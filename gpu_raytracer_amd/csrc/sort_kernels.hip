@@ -260,6 +260,315 @@ __global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__
     }
 }
 
+// ================================================================ MSB bucket sort
+// The build's sort for 2 <= n <= kMsbMaxN 30-bit Morton keys: one global
+// scatter by the top 10 key bits, then every bucket sorted on its own in LDS
+// -- two scatter levels instead of four LSB passes.
+//   K1 (k_morton<true>)  per-tile counts of bucket d = key >> 20 and the
+//                        global bucket histogram (one LDS atomic per key);
+//   k_msb_scan           counts -> exclusive destinations offs[tile][d] =
+//                        bucket start + earlier tiles' counts; bucket starts;
+//   k_msb_scatter        one 4096-key tile per block: stable 10-bit ballot
+//                        ranking, LDS bucketing, runs -> keys[1]/vals[1];
+//   k_bucket_sort        one bucket per block: stable LSB sort of the bucket by
+//                        the low 20 key bits (2 x 10-bit passes) in LDS ->
+//                        keys[0]/vals[0]; a bucket over kBucketCap keys runs
+//                        the same passes chunk by chunk through global memory.
+// The first level is stable, so a bucket arrives in index order, and the
+// second is stable: the result is §9.4's unique (key, index) order, the LSB
+// sort's (tests/test_parity_gpu.py compares the two).
+constexpr int kBucketThreads = 256;
+constexpr int kBucketWaves = kBucketThreads / 64;
+constexpr uint32_t kBucketCap = kBucketThreads * kSortItems;  // keys per LDS sort
+
+// Stable rank of each item among the equal 10-bit digits of its wave, in
+// (item, lane) order, on top of the wave's running digit counters s_wc[w].
+__device__ __forceinline__ void rank10(const uint32_t (&dg)[kSortItems], const bool (&ok)[kSortItems],
+                                       uint32_t (*s_wc)[kMsbBuckets], uint32_t (&r)[kSortItems]) {
+    const uint32_t w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) {
+        const uint32_t d = dg[i];
+        uint64_t peers = __ballot(ok[i]);
+#pragma unroll
+        for (int b = 0; b < 10; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t bal = __ballot(ok[i] && bit);
+            peers &= bit ? bal : ~bal;
+        }
+        const uint32_t below = sort_count_below(peers);
+        const uint32_t cur = s_wc[w][d];
+        r[i] = cur + below;
+        if (ok[i] && below == 0) s_wc[w][d] = cur + (uint32_t)__popcll(peers);
+    }
+}
+
+// s_wc[w][d] -> exclusive prefix over the waves; s_cnt[d] = the digit's total.
+template <int NW, int NT>
+__device__ __forceinline__ void wave_prefix(uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt) {
+    for (uint32_t d = threadIdx.x; d < kMsbBuckets; d += NT) {
+        uint32_t acc = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = s_wc[w][d];
+            s_wc[w][d] = acc;
+            acc += c;
+        }
+        s_cnt[d] = acc;
+    }
+}
+
+// In-place exclusive scan of a[1024] in LDS by NT threads (a written before a
+// barrier); ends with a barrier.
+template <int NT>
+__device__ __forceinline__ void scan1024(uint32_t* a, uint32_t* s_sw /* [NT / 64] */) {
+    constexpr int PER = (int)kMsbBuckets / NT;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        v[j] = a[t * PER + j];
+        sum += v[j];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    if (l == 63) s_sw[w] = x;
+    __syncthreads();
+    uint32_t pre = x - sum;
+    for (uint32_t k = 0; k < w; ++k) pre += s_sw[k];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        a[t * PER + j] = pre;
+        pre += v[j];
+    }
+    __syncthreads();
+}
+
+// counts[t][d] (t < nt <= 512) -> exclusive destinations bucket start +
+// sum_{t' < t} counts[t'][d], in place; bstart[0..1024] = bucket starts.
+// 16 blocks x 1024 threads: block b owns buckets [64b, 64b + 64), a thread
+// one bucket and a chunk of <= 32 tiles.
+__global__ __launch_bounds__(1024) void k_msb_scan(uint32_t* __restrict__ offs, uint32_t nt,
+                                                   const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bstart) {
+    __shared__ uint32_t s_base[kMsbBuckets];
+    __shared__ uint32_t s_sw[16];
+    __shared__ uint32_t s_csum[16][64];
+    const uint32_t t = threadIdx.x;
+    const uint32_t g = ghist[t];
+    s_base[t] = g;
+    __syncthreads();
+    scan1024<1024>(s_base, s_sw);
+    if (blockIdx.x == 0) {
+        bstart[t] = s_base[t];
+        if (t == kMsbBuckets - 1) bstart[kMsbBuckets] = s_base[t] + g;
+    }
+    const uint32_t dl = t & 63, c = t >> 6, d = blockIdx.x * 64 + dl;
+    const uint32_t C = (nt + 15) / 16;
+    uint32_t v[32], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 32; ++j) {
+        const uint32_t tt = c * C + j;
+        v[j] = (j < C && tt < nt) ? offs[(uint64_t)tt * kMsbBuckets + d] : 0u;
+        sum += v[j];
+    }
+    s_csum[c][dl] = sum;
+    __syncthreads();
+    uint32_t run = s_base[d];
+    for (uint32_t k = 0; k < c; ++k) run += s_csum[k][dl];
+#pragma unroll
+    for (uint32_t j = 0; j < 32; ++j) {
+        const uint32_t tt = c * C + j;
+        if (j < C && tt < nt) {
+            offs[(uint64_t)tt * kMsbBuckets + d] = run;
+            run += v[j];
+        }
+    }
+}
+
+// First level: one 4096-key tile per block, bucket d = key >> 20.
+__global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __restrict__ kin,
+                                                              const uint32_t* __restrict__ vin,
+                                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                              uint32_t n, const uint32_t* __restrict__ offs) {
+    constexpr int W = kSortThreads / 64;
+    static_assert(W * kMsbBuckets == 2 * kSortTile, "counters and bucketed tile share one buffer");
+    __shared__ uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
+    __shared__ uint32_t s_start[kMsbBuckets], s_gofs[kMsbBuckets];
+    __shared__ uint32_t s_sw[W];
+    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_buf);
+    uint32_t* s_key = s_buf;
+    uint32_t* s_val = s_buf + kSortTile;
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const uint32_t tile = blockIdx.x, base = tile * (uint32_t)kSortTile;
+    for (uint32_t j = tid; j < 2 * kSortTile; j += kSortThreads) s_buf[j] = 0u;
+    for (uint32_t j = tid; j < kMsbBuckets; j += kSortThreads) s_gofs[j] = offs[(uint64_t)tile * kMsbBuckets + j];
+    uint32_t k[kSortItems], v[kSortItems], dg[kSortItems], r[kSortItems];
+    bool ok[kSortItems];
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) {
+        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
+        ok[i] = idx < n;
+        k[i] = ok[i] ? kin[idx] : 0u;
+        v[i] = ok[i] ? vin[idx] : 0u;
+        dg[i] = (k[i] >> kMsbShift) & (kMsbBuckets - 1);
+    }
+    __syncthreads();
+    rank10(dg, ok, s_wc, r);
+    __syncthreads();
+    wave_prefix<W, kSortThreads>(s_wc, s_start);
+    __syncthreads();
+    scan1024<kSortThreads>(s_start, s_sw);
+    uint32_t pos[kSortItems];
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) pos[i] = s_start[dg[i]] + s_wc[w][dg[i]] + r[i];
+    __syncthreads();  // the counters are dead: the buffer becomes the bucketed tile
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i)
+        if (ok[i]) {
+            s_key[pos[i]] = k[i];
+            s_val[pos[i]] = v[i];
+        }
+    __syncthreads();
+    const uint32_t trem = n - base;
+    const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
+#pragma unroll
+    for (int m = 0; m < kSortItems; ++m) {
+        const uint32_t p = tid + m * kSortThreads;
+        if (p < tcount) {
+            const uint32_t key = s_key[p];
+            const uint32_t d = (key >> kMsbShift) & (kMsbBuckets - 1);
+            const uint32_t o = s_gofs[d] + (p - s_start[d]);
+            kout[o] = key;
+            vout[o] = s_val[p];
+        }
+    }
+}
+
+// Ranks one chunk (<= kBucketCap items in registers, item j = w*512 + i*64 +
+// lane) by the 10-bit digit at `shift`: r[i] = the item's position among its
+// digit's items of the chunk (earlier waves first, then item order); s_cnt =
+// the chunk's digit counts.  Callers barrier before reusing s_wc.
+__device__ __forceinline__ void bucket_rank(const uint32_t (&k)[kSortItems], const bool (&ok)[kSortItems],
+                                            uint32_t shift, uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt,
+                                            uint32_t (&dg)[kSortItems], uint32_t (&r)[kSortItems]) {
+    for (uint32_t j = threadIdx.x; j < kBucketWaves * kMsbBuckets; j += kBucketThreads) (&s_wc[0][0])[j] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) dg[i] = (k[i] >> shift) & (kMsbBuckets - 1);
+    rank10(dg, ok, s_wc, r);
+    __syncthreads();
+    wave_prefix<kBucketWaves, kBucketThreads>(s_wc, s_cnt);
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < kSortItems; ++i) r[i] += s_wc[w][dg[i]];
+}
+
+// Second level: one bucket [bstart[b], bstart[b+1]) per block, sorted stably by
+// key bits 0..19 (the bucket shares bits 20..29).
+__global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __restrict__ kin, uint32_t* __restrict__ vin,
+                                                                uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                                const uint32_t* __restrict__ bstart) {
+    static_assert(kBucketWaves * kMsbBuckets == 2 * kBucketCap, "counters and sorted chunk share one buffer");
+    __shared__ uint32_t s_wc[kBucketWaves][kMsbBuckets];  // ranking counters; fast path: then the sorted chunk
+    __shared__ uint32_t s_cnt[kMsbBuckets], s_run[kMsbBuckets];
+    __shared__ uint32_t s_sw[kBucketWaves];
+    const uint32_t s = bstart[blockIdx.x], m = bstart[blockIdx.x + 1] - s;
+    if (m == 0) return;
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    uint32_t k[kSortItems], v[kSortItems], dg[kSortItems], r[kSortItems];
+    bool ok[kSortItems];
+    if (m <= kBucketCap) {
+        uint32_t* s_key = &s_wc[0][0];
+        uint32_t* s_val = s_key + kBucketCap;
+#pragma unroll
+        for (int i = 0; i < kSortItems; ++i) {
+            const uint32_t j = w * (64u * kSortItems) + i * 64u + l;
+            ok[i] = j < m;
+            k[i] = ok[i] ? kin[s + j] : 0u;
+            v[i] = ok[i] ? vin[s + j] : 0u;
+        }
+        for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+            bucket_rank(k, ok, shift, s_wc, s_cnt, dg, r);
+            scan1024<kBucketThreads>(s_cnt, s_sw);  // its barriers also end every counter read
+#pragma unroll
+            for (int i = 0; i < kSortItems; ++i)
+                if (ok[i]) {
+                    const uint32_t p = s_cnt[dg[i]] + r[i];
+                    s_key[p] = k[i];
+                    s_val[p] = v[i];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < kSortItems; ++i) {
+                const uint32_t j = w * (64u * kSortItems) + i * 64u + l;
+                if (ok[i]) {
+                    k[i] = s_key[j];
+                    v[i] = s_val[j];
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < kSortItems; ++i) {
+            const uint32_t j = w * (64u * kSortItems) + i * 64u + l;
+            if (ok[i]) {
+                kout[s + j] = k[i];
+                vout[s + j] = v[i];
+            }
+        }
+        return;
+    }
+    // A bucket beyond one LDS sort (clustered or degenerate scenes): the same
+    // two passes chunk by chunk through global memory -- kin -> kout (digit 0),
+    // kout -> kin (digit 1) -- then a copy kin -> kout.  The block owns
+    // [s, s + m) of all four arrays.
+    uint32_t *sk = kin, *sv = vin, *dk = kout, *dv = vout;
+    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+        for (uint32_t j = tid; j < kMsbBuckets; j += kBucketThreads) s_run[j] = 0u;
+        __syncthreads();
+        for (uint32_t j = tid; j < m; j += kBucketThreads) atomicAdd(&s_run[(sk[s + j] >> shift) & (kMsbBuckets - 1)], 1u);
+        __syncthreads();
+        scan1024<kBucketThreads>(s_run, s_sw);
+        for (uint32_t c0 = 0; c0 < m; c0 += kBucketCap) {
+#pragma unroll
+            for (int i = 0; i < kSortItems; ++i) {
+                const uint32_t j = c0 + w * (64u * kSortItems) + i * 64u + l;
+                ok[i] = j < m;
+                k[i] = ok[i] ? sk[s + j] : 0u;
+                v[i] = ok[i] ? sv[s + j] : 0u;
+            }
+            bucket_rank(k, ok, shift, s_wc, s_cnt, dg, r);
+#pragma unroll
+            for (int i = 0; i < kSortItems; ++i)
+                if (ok[i]) {
+                    const uint32_t o = s_run[dg[i]] + r[i];
+                    dk[s + o] = k[i];
+                    dv[s + o] = v[i];
+                }
+            __syncthreads();  // s_run and s_wc reads done
+            for (uint32_t d = tid; d < kMsbBuckets; d += kBucketThreads) s_run[d] += s_cnt[d];
+            __syncthreads();
+        }
+        __threadfence();  // this pass's stores before the next pass's loads (also drops stale L1 lines)
+        __syncthreads();
+        uint32_t* t0 = sk;
+        sk = dk;
+        dk = t0;
+        t0 = sv;
+        sv = dv;
+        dv = t0;
+    }
+    for (uint32_t j = tid; j < m; j += kBucketThreads) {  // the result is in kin/vin
+        kout[s + j] = kin[s + j];
+        vout[s + j] = vin[s + j];
+    }
+}
+
 // ================================================================ launchers
 static inline uint32_t sdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
@@ -302,6 +611,18 @@ hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const u
     scatter_pass<16>(keys[0], vals[0], keys[1], vals[1], n, ghist + 512, counts[2], s);
     hipLaunchKernelGGL(k_tile_hist<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[3]);
     scatter_pass<24>(keys[1], vals[1], keys[0], vals[0], n, ghist + 768, counts[3], s);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
+                           uint32_t* bstart, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    const uint32_t nt = sort_tiles(n);
+    if (n > kMsbMaxN) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart);
+    hipLaunchKernelGGL(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts);
+    hipLaunchKernelGGL(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
+                       bstart);
     return hipGetLastError();
 }
 

@@ -179,6 +179,42 @@ def test_build_degenerate_inputs(R, oracle):
     _compare_build(R, oracle, neg)
 
 
+def _compare_sorts(R, tris):
+    """The build with the MSB bucket sort (default for 2 <= n <= 2^21) and with
+    the 4-pass LSB sort (build.sort = 0) must give the same BVH."""
+    tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    outs = []
+    try:
+        for mode in (0, 1):
+            R.config_set("build.sort", mode)
+            with R.Scene.from_soup(tris) as s:
+                s.build()
+                outs.append(s.read_bvh())
+    finally:
+        R.config_set("build.sort", 1)
+    a, b = outs
+    assert np.array_equal(a["keys"], b["keys"])
+    assert np.array_equal(a["vals"], b["vals"])
+    assert np.array_equal(a["nodes"].view(np.uint32), b["nodes"].view(np.uint32))
+
+
+@pytest.mark.parametrize("n", [2, 3, 4097, 70000, 1000000, 2097152])
+def test_build_sort_paths_agree(R, oracle, n):
+    _compare_sorts(R, soup(oracle, n, 11))
+
+
+def test_build_sort_paths_agree_clustered(R, oracle):
+    """Buckets beyond one LDS sort (2048 keys): the chunked path."""
+    rng = np.random.default_rng(12)
+    c = (rng.random((30000, 9)) * 1e-3).astype(np.float32)
+    c[:5] += 1.0                                   # outliers: the cluster is one top-10-bit bucket
+    _compare_sorts(R, c)
+    _compare_sorts(R, np.tile(soup(oracle, 1, 3), (9000, 1)))   # all keys equal
+    mixed = soup(oracle, 60000, 13).copy()
+    mixed[:25000] = mixed[:25000] * 1e-4 + 0.5     # one dense cell inside a uniform soup
+    _compare_sorts(R, mixed)
+
+
 def test_build_repeat_and_rebuild(R, oracle):
     """Control words are re-armed between builds (zeroed per build)."""
     tris = soup(oracle, 70000, 2)
