@@ -290,6 +290,7 @@ __device__ __forceinline__ void rank10(const uint32_t (&dg)[kSortItems], const b
     for (int i = 0; i < kSortItems; ++i) {
         const uint32_t d = dg[i];
         uint64_t peers = __ballot(ok[i]);
+        if (!peers) continue;  // wave-uniform: no item of this group (a bucket's tail)
 #pragma unroll
         for (int b = 0; b < 10; ++b) {
             const bool bit = (d >> b) & 1u;
