@@ -15,6 +15,9 @@ import gpu_raytracer_amd as R  # noqa: E402
 from gpu_raytracer_amd.scenes import SOUP_VIEW as V  # noqa: E402
 
 modes = sys.argv[1].split(",") if len(sys.argv) > 1 else ["trace", "rowmajor", "p8", "shadow", "path", "build"]
+for kv in os.environ.get("RT_CONFIG", "").split(","):  # e.g. RT_CONFIG=trace.steal=1
+    if kv:
+        R.config_set(kv.split("=")[0], int(kv.split("=")[1]))
 w, h, spp = 1920, 1080, 1
 s = R.Scene.generate_soup(1_000_000, 1)
 s.build()

@@ -1,7 +1,8 @@
 """A/B of librtamd builds: alternating measurement processes (tools/ab_child.py,
 one library per process via RT_LIB), medians per library, and a check that
 every library produced identical outputs.
-usage: python tools/ab_libs.py ROUNDS MODES lib1.so lib2.so ..."""
+usage: python tools/ab_libs.py ROUNDS MODES lib1.so lib2.so ...
+A library argument may carry a config: lib.so@trace.steal=1 (RT_CONFIG)."""
 import json
 import os
 import subprocess
@@ -14,7 +15,8 @@ rounds, modes, libs = int(sys.argv[1]), sys.argv[2], sys.argv[3:]
 res = {lib: [] for lib in libs}
 for r in range(rounds):
     for lib in libs:
-        env = dict(os.environ, RT_LIB=os.path.abspath(lib))
+        path, _, cfg = lib.partition("@")
+        env = dict(os.environ, RT_LIB=os.path.abspath(path), RT_CONFIG=cfg)
         p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "ab_child.py"), modes], env=env,
                            capture_output=True, text=True, timeout=300)
         if p.returncode != 0:
