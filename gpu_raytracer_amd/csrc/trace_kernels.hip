@@ -284,7 +284,14 @@ __device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const ui
 // Returns 0 = more steps, 1 = done, 2 = finish with
 // trace_ray_from(bin_of(R.cur)) (stack overflow at record R.cur, or the step
 // guard of a malformed tree).
-template <bool COUNT, int NT, bool ANY = false>
+//
+// MTF: Moller-Trumbore before the leaf-box test -- fewer instructions per
+// step, more registers (84 vs 72 VGPRs: 5 waves per SIMD instead of 7).
+// Used where waves run latency-bound (a rank's tiles, shadow rays:
+// 4-6 % faster); the full-frame primary kernel, issue-bound at high
+// occupancy, and path mode (3 % slower with it) keep the box test first
+// (profiles/ab_mtfirst_r01.log).
+template <bool COUNT, int NT, bool ANY = false, bool MTF = false>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
                                          uint32_t& cn, uint32_t& ct, bool any = ANY) {
@@ -308,13 +315,33 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
         const float4* tp = tri_s + (uint64_t)(R.pend & ~kWideLeaf) * 3;
         const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
         const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
-        float lo[3], hi[3], tn;
-        tri_bounds(tv, lo, hi);
-        if (slab_hit(lo, hi, o, R.invd, R.tb, tn)) {
+        if (MTF) {
+            // §9.7 takes the triangle iff its exact leaf box passes the slab
+            // test and Moller-Trumbore hits closer, both against the same tb:
+            // MT first, the box test only for lanes with a closer MT hit (the
+            // wave skips it when it has none), on vertices loaded again
+            // (L1-hot) rather than kept live across MT.
             float t, u, v;
             if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) {
-                R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(T2.y);
-                if (any) { R.pend = RT_SENT; return 1; }  // any-hit: done
+                __asm__ volatile("" ::: "memory");  // reload below instead of keeping tv live
+                const float4 U0 = tp[0], U1 = tp[1], U2 = tp[2];
+                const float uv[9] = {U0.x, U0.y, U0.z, U0.w, U1.x, U1.y, U1.z, U1.w, U2.x};
+                float lo[3], hi[3], tn;
+                tri_bounds(uv, lo, hi);
+                if (slab_hit(lo, hi, o, R.invd, R.tb, tn)) {
+                    R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(U2.y);
+                    if (any) { R.pend = RT_SENT; return 1; }  // any-hit: done
+                }
+            }
+        } else {
+            float lo[3], hi[3], tn;
+            tri_bounds(tv, lo, hi);
+            if (slab_hit(lo, hi, o, R.invd, R.tb, tn)) {
+                float t, u, v;
+                if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) {
+                    R.tb = t; R.hu = u; R.hv = v; R.hp = __float_as_uint(T2.y);
+                    if (any) { R.pend = RT_SENT; return 1; }  // any-hit: done
+                }
             }
         }
         R.pend = RT_SENT;
@@ -355,7 +382,7 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
 // One ray from o along d over (0, tmax): the wide traversal when it applies
 // (finite 1/d, K7w records present), with the binary hand-off on overflow;
 // the binary traversal from the root otherwise.  any: the first hit ends it.
-template <bool COUNT, int NT>
+template <bool COUNT, int NT, bool MTF = false>
 __device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                           uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n, const float* o,
                                           const float* d, float tmax, bool any, uint32_t* sref, uint16_t* stn,
@@ -365,7 +392,7 @@ __device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const 
     R.tb = tmax;
     const bool wide = R.fin && wnodes && n >= 2;
     int st = wide ? 0 : 2;
-    while (st == 0) st = wide_step<COUNT, NT>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any);
+    while (st == 0) st = wide_step<COUNT, NT, false, MTF>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any);
     if (st == 2) {
         const uint32_t start = !wide ? (n ? 0u : RT_SENT) : (R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1));
         trace_ray_from<COUNT>(nodes, tri_s, n, o, R.d, start, R.tb, R.hu, R.hv, R.hp, cn, ct, any);
@@ -427,7 +454,7 @@ __device__ __forceinline__ float shadow_factor(const char* __restrict__ nodes, c
     surface(tris, prim, o, d, t, lt.p, f);
     float tb, hu, hv;
     uint32_t hp;
-    trace_gen<COUNT, NT>(nodes, wnodes, wcap, tri_s, n, f.S, f.D, 1.0f, true, sref, stn, tb, hu, hv, hp, cn, ct);
+    trace_gen<COUNT, NT, true>(nodes, wnodes, wcap, tri_s, n, f.S, f.D, 1.0f, true, sref, stn, tb, hu, hv, hp, cn, ct);
     const float lit = hp != RT_SENT ? 0.0f : fmaxf(f.cosl, 0.0f);
     return lt.ambient + (1.0f - lt.ambient) * lit;
 }
@@ -485,7 +512,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                 wray_init(cam.eye, d, R);
                 int st = R.fin ? 0 : 2;
                 const char* nd = reinterpret_cast<const char*>(nodes);
-                while (st == 0) st = wide_step<COUNT, NT>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
+                while (st == 0) st = wide_step<COUNT, NT, false, PACKED || SHADOW>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
                                                           s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct);
                 if (st == 2) {
                     if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
