@@ -10,7 +10,10 @@ W untimed warm-up steps, then K timed steps between barrier+synchronize on
 both sides; the max over ranks is reported by rank 0 as ONE JSON line.
 
   value      = W*H*spp / (mean over steps of max-rank trace time + gather time)
-               [Mrays/s, whole image, all ranks; SURVEY.md §8(e)]
+               [Mrays/s, whole image, all ranks; SURVEY.md §8(e)].  At N>1 the
+               trace, the RCCL gather and the unpack are queued back to back
+               on torch's stream and timed together with events on it
+               (gather time = that span minus the trace)
   build_mprims_per_s = N_tris / mean build time (per GPU; replicated)
   ms_per_step = wall time per frame incl. build, trace, gather and host syncs
 Device times come from hipEvents recorded on the stream each kernel runs on
@@ -188,23 +191,39 @@ def main():
     slabs_all = torch.zeros(world * max(tmax, 1) * 256, dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
     gather_list = None  # gather_slabs receives straight into slabs_all's per-rank rows
 
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
     def step():
         build_ms = scene.build()
         if world == 1:
             trace_ms = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
             return build_ms, trace_ms, 0.0
+        cur = torch.cuda.current_stream(dev)
+        if args.dist_backend == "nccl":
+            # trace -> RCCL gather -> unpack queued back to back on torch's
+            # stream (the collective waits on it; no host round trip between
+            # them), timed with events on that stream
+            ev[0].record(cur)
+            scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
+                                      stream=cur.cuda_stream)
+            ev[1].record(cur)
+            D.gather_slabs(slab, rank, world, gather_list, slabs_all)
+            if rank == 0:
+                R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
+                                      cur.cuda_stream)
+            ev[2].record(cur)
+            ev[2].synchronize()
+            trace_ms = ev[0].elapsed_time(ev[1])
+            return build_ms, trace_ms, ev[0].elapsed_time(ev[2]) - trace_ms
+        # gloo rehearsal: stage through host memory, host-timed
         trace_ms = scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
                                              timed=True)
         t0 = time.perf_counter()
-        if args.dist_backend == "nccl":
-            D.gather_slabs(slab, rank, world, gather_list, slabs_all)
-        else:  # rehearsal: stage through host memory
-            g = D.gather_slabs(slab.cpu(), rank, world)
-            if rank == 0:
-                slabs_all.copy_(g)
+        g = D.gather_slabs(slab.cpu(), rank, world)
         if rank == 0:
+            slabs_all.copy_(g)
             R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
-                                  torch.cuda.current_stream(dev).cuda_stream)
+                                  cur.cuda_stream)
         torch.cuda.synchronize(dev)
         return build_ms, trace_ms, (time.perf_counter() - t0) * 1e3
 
