@@ -606,13 +606,55 @@ __device__ __forceinline__ void store_wide(uint4* __restrict__ wnodes, uint32_t 
     o[3] = make_uint4(ref[2], ref[3], 0u, 0u);
 }
 
-// The record's entries: X's children, each internal child replaced by its
-// two children (4 slots, RT_SENT-padded); topo_of(i) gives internal node i's
-// topology word.
-template <typename TopoOf>
-__device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoOf topo_of, uint32_t (&node)[4]) {
+// The record's entries (4 slots, RT_SENT-padded); topo_of(i) gives internal
+// node i's topology word, box_of_node(i) its box.  collapse = 0: X's
+// children, each internal child replaced by its two children.
+//
+// collapse = 1 (default): greedy instead of fixed depth -- starting from
+// {left, right}, twice replace the internal entry with the largest box
+// surface (first in preorder on ties) by its two children.  Any such set is
+// a preorder cut of X's subtree (each entry a descendant, their subtrees
+// partitioning X's leaves, listed in preorder), which is all the trace's
+// exactness argument uses; the greedy cut fills the slots a leaf child
+// leaves empty in the fixed one and descends where the big boxes are.
+__device__ __forceinline__ float half_area(const Aabb& b) {
+    const float dx = b.hi[0] - b.lo[0], dy = b.hi[1] - b.lo[1], dz = b.hi[2] - b.lo[2];
+    return (dx * dy + dy * dz) + dz * dx;
+}
+
+template <typename TopoOf, typename BoxOfNode>
+__device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoOf topo_of, BoxOfNode box_of_node,
+                                             uint32_t collapse, uint32_t (&node)[4]) {
     uint32_t l, r;
     kids_of(tx, L0, l, r);
+    if (collapse == 1) {
+        node[0] = l; node[1] = r; node[2] = RT_SENT; node[3] = RT_SENT;
+#pragma unroll
+        for (int step = 0; step < 2; ++step) {
+            int best = -1;
+            float ba = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {  // slot 3 is still empty
+                if (node[i] < L0) {       // internal (RT_SENT and leaves are >= L0)
+                    const float a = half_area(box_of_node(node[i]));
+                    if (best < 0 || a > ba) { best = i; ba = a; }
+                }
+            }
+            if (best < 0) break;
+            uint32_t pick = node[0];
+#pragma unroll
+            for (int i = 1; i < 3; ++i) pick = best == i ? node[i] : pick;
+            uint32_t c0, c1;
+            kids_of(topo_of(pick), L0, c0, c1);
+            uint32_t nn[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                nn[i] = i < best ? node[i] : i == best ? c0 : i == best + 1 ? c1 : node[i - 1];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) node[i] = nn[i];
+        }
+        return;
+    }
     uint32_t a0 = l, a1 = RT_SENT, b0 = r, b1 = RT_SENT;
     if (l < L0) kids_of(topo_of(l), L0, a0, a1);
     if (r < L0) kids_of(topo_of(r), L0, b0, b1);
@@ -647,7 +689,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         float* __restrict__ prebuf, float* __restrict__ sufbuf,
                                                         float* __restrict__ totals, uint32_t* __restrict__ cross,
                                                         uint32_t* cross_ctr, uint32_t cross_cap,
-                                                        uint4* __restrict__ wnodes) {
+                                                        uint4* __restrict__ wnodes, uint32_t collapse) {
     constexpr int T = kRefitT, NW = T / 64, KW = 1024;
     static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
     static_assert(sizeof(uint4) <= sizeof(Aabb), "topology words must fit the table buffer");
@@ -753,7 +795,9 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         const Aabb bx = s_box[T + tid];
         store_node(nodes, k, bx, tp.x, tp.y);
         uint32_t node[4];
-        wide_entries(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; }, node);  // children of a local node are local
+        // every descendant of a local node is local: topology and boxes in LDS
+        wide_entries(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; },
+                     [&](uint32_t i) { return s_box[T + i - B0]; }, collapse, node);
         uint32_t slot[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -839,7 +883,7 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
 __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ topo, const uint32_t* __restrict__ cross,
                                                     const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
                                                     const void* __restrict__ nodes, uint32_t n,
-                                                    uint4* __restrict__ wnodes) {
+                                                    uint4* __restrict__ wnodes, uint32_t collapse) {
     uint32_t pre[kCrossShards + 1];
     pre[0] = 0;
 #pragma unroll
@@ -854,7 +898,8 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         if (X >= L0) continue;
         const uint4 tx = topo[X];
         uint32_t node[4];
-        wide_entries(tx, L0, [&](uint32_t i) { return topo[i]; }, node);
+        wide_entries(tx, L0, [&](uint32_t i) { return topo[i]; }, [&](uint32_t i) { return load_aabb_node(nodes, i); },
+                     collapse, node);
         const Aabb bx = load_aabb_node(nodes, X);
         store_wide(wnodes, X, bx, node, [&](int i) { return load_aabb_node(nodes, node[i] == RT_SENT ? X : node[i]); },
                    L0);
@@ -987,7 +1032,7 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, hipStream_t s) {
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     hipLaunchKernelGGL(k_wide_cross, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr, cross_cap(m),
-                       b.nodes, n, b.wnodes);
+                       b.nodes, n, b.wnodes, g_trace_config.wide_collapse);
     return hipGetLastError();
 }
 
@@ -1018,7 +1063,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
         const uint32_t m = cdiv(n, kRefitT);
         hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
                            b.parent, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.wnodes);
+                           cross_cap(m), b.wnodes, g_trace_config.wide_collapse);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if ((e = rec(4)) != hipSuccess) return e;

@@ -182,6 +182,7 @@ rt_status rt_config_set(const char* key, int64_t value) {
     else if (k == "trace.tile_order" && (value == 0 || value == 1)) rt::g_trace_config.tile_order = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
     else if (k == "build.sort" && (value == 0 || value == 1)) rt::g_trace_config.sort_msb = (uint32_t)value;
+    else if (k == "build.wide_collapse" && (value == 0 || value == 1)) rt::g_trace_config.wide_collapse = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) rt::g_trace_config.stage_events = (uint32_t)value;
     else if (k == "timing.event_fence" && (value == 0 || value == 1)) rt::g_trace_config.event_fence = (uint32_t)value;
     else if (k == "path.wavefront" && (value == 0 || value == 1)) rt::g_trace_config.path_wave = (uint32_t)value;

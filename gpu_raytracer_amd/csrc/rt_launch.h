@@ -88,6 +88,7 @@ struct TraceConfig {
     uint32_t stage_events = 0;  // build: record the per-stage events (rt_bvh_build_times); else total only
     uint32_t event_fence = 0;   // timing events with the system-scope fence (scenes created afterwards)
     uint32_t tile_order = 1;    // 1: longest-first from the previous same-size frame's wave times; 0: row-major
+    uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbMaxN, 0 = 4-pass LSB always
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };

@@ -1,6 +1,6 @@
-"""Diagnostic: rt_stage_bounds vs oracle over many n (prints mismatches)."""
+"""(tests/diag: uses the oracle as the checker.) Diagnostic: rt_stage_bounds vs oracle over many n (prints mismatches)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
 import gpu_raytracer_amd as R
 from oracle import oracle as O

@@ -41,13 +41,57 @@ def _decode_planes(rec):
     return lo.astype(np.float32), hi.astype(np.float32)
 
 
-def _check_wide(R, tris):
+def _half_area(lo, hi):
+    """csrc/build_kernels.hip half_area, same float32 operation order."""
+    d = (hi - lo).astype(np.float32)
+    return np.float32(np.float32(d[0] * d[1]) + np.float32(d[1] * d[2])) + np.float32(d[2] * d[0])
+
+
+def _entries(X, a, esc, lo_e, hi_e, L0, collapse):
+    """Restatement of wide_entries: the record's entries in preorder."""
+    def kids(c):
+        L = a[c]
+        return [L, esc[L]]  # escape of a left child = its right sibling
+    if collapse == 0:
+        out = []
+        for c in kids(X):
+            out += kids(c) if c < L0 else [c]
+        return out
+    ent = kids(X)
+    for _ in range(2):
+        best, ba = -1, None
+        for i, c in enumerate(ent):
+            if c < L0:
+                ar = _half_area(lo_e[c], hi_e[c])
+                if best < 0 or ar > ba:
+                    best, ba = i, ar
+        if best < 0:
+            break
+        ent = ent[:best] + kids(ent[best]) + ent[best + 1:]
+    return ent
+
+
+def _leaf_range(c, a, esc, L0, memo):
+    """[first, last] leaf of node c (leaves are in sorted order left to right)."""
+    if c >= L0:
+        return c - L0, c - L0
+    if c not in memo:
+        L = a[c]
+        memo[c] = (_leaf_range(L, a, esc, L0, memo)[0], _leaf_range(esc[L], a, esc, L0, memo)[1])
+    return memo[c]
+
+
+def _check_wide(R, tris, collapse=1):
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     n = len(tris)
-    with R.Scene.from_soup(tris) as s:
-        s.build()
-        nodes = s.read_bvh()["nodes"]
-        rec = s.read_wide()
+    R.config_set("build.wide_collapse", collapse)
+    try:
+        with R.Scene.from_soup(tris) as s:
+            s.build()
+            nodes = s.read_bvh()["nodes"]
+            rec = s.read_wide()
+    finally:
+        R.config_set("build.wide_collapse", 1)
     assert rec.shape == (n - 1, 16)
     L0 = n - 1
     a, esc = nodes["a"].astype(np.int64), nodes["esc"].astype(np.int64)
@@ -57,16 +101,16 @@ def _check_wide(R, tris):
     wild = ((meta >> 24) & 1).astype(bool)
     mask = (meta >> 28) & 0xF
     refs = rec[:, 10:14]
+    memo = {}
     for X in range(n - 1):
-        L = a[X]
-        Rr = esc[L]  # escape of a left child = its right sibling
-        kids = []
-        for c in (L, Rr):
-            if c < L0:
-                g0 = a[c]
-                kids += [g0, esc[g0]]
-            else:
-                kids.append(c)
+        kids = _entries(X, a, esc, lo_e, hi_e, L0, collapse)
+        # a preorder cut of X's subtree: consecutive leaf ranges covering X's
+        rng = [_leaf_range(c, a, esc, L0, memo) for c in kids]
+        xl, xh = _leaf_range(X, a, esc, L0, memo)
+        assert rng[0][0] == xl and rng[-1][1] == xh, X
+        assert all(rng[i][1] + 1 == rng[i + 1][0] for i in range(len(rng) - 1)), X
+        if collapse == 1:
+            assert len(kids) == min(4, xh - xl + 1), X
         assert mask[X] == (1 << len(kids)) - 1, X
         for i, c in enumerate(kids):
             want = c if c < L0 else (LEAF | (c - L0))
@@ -78,19 +122,23 @@ def _check_wide(R, tris):
     return rec
 
 
-def test_wide_records_small_and_degenerate(R, oracle):
-    _check_wide(R, oracle.soup(3000, 2).reshape(-1, 9))
+@pytest.mark.parametrize("collapse", [1, 0])
+def test_wide_records_small_and_degenerate(R, oracle, collapse):
+    """K7w records for both entry rules (build.wide_collapse 1 = greedy
+    largest-surface cut, the default; 0 = fixed two levels)."""
+    _check = lambda t: _check_wide(R, t, collapse)  # noqa: E731
+    _check(oracle.soup(3000, 2).reshape(-1, 9))
     rng = np.random.default_rng(3)
     flat = oracle.soup(2000, 4).reshape(-1, 9).copy()
     flat[:, 2::3] = 0.25                                      # zero extent in z
-    _check_wide(R, flat)
+    _check(flat)
     tiny = (rng.random((1500, 9)) * 1e-30).astype(np.float32)  # denormal-scale grids
-    _check_wide(R, tiny)
+    _check(tiny)
     huge = (rng.random((1500, 9)) * 3e37 - 1.5e37).astype(np.float32)
-    _check_wide(R, huge)
-    _check_wide(R, np.tile(oracle.soup(1, 3).reshape(-1, 9), (700, 1)))  # identical boxes
+    _check(huge)
+    _check(np.tile(oracle.soup(1, 3).reshape(-1, 9), (700, 1)))  # identical boxes
     two = oracle.soup(2, 9).reshape(-1, 9)
-    rec = _check_wide(R, two)
+    rec = _check(two)
     assert rec.shape[0] == 1
 
 
@@ -196,3 +244,4 @@ def test_wide_work_counters(R, oracle):
         wide = s.render_work(cam, w, h, 1)
     assert wide[0] * 2 < binary[0]
     assert wide[1] >= binary[1]
+

@@ -60,4 +60,7 @@ if "shadow" in modes:
 if "path" in modes:
     out["path"] = med(lambda: s.render_path_device(cam, w, h, spp, (2.0, 3.0, -2.0), 0.3, 2, d_rgba=img.data_ptr(), timed=True), 4)
     out["crc_path"] = crc(img)
+if "work" in modes:  # wide records and triangle records fetched by the primary frame
+    wk = s.render_work(cam, w, h, spp)
+    out["records"], out["tri_records"] = float(wk[0]), float(wk[1])
 print(json.dumps(out), flush=True)
