@@ -128,13 +128,17 @@ rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint
     const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     const uint32_t key[5] = {w, h, spp, rank, nranks};
     const bool same = std::memcmp(key, s->sched_key, sizeof(key)) == 0;
-    const size_t need = 3ull * nb * 4;
+    // [order][cost A][cost B] u32, [px A][px B] u16 x 256, [perm] u8 x 256 per tile slot
+    const size_t need = 3ull * nb * 4 + 2ull * nb * 512 + (size_t)nb * 256;
     if (!same || s->order_cap < need) {
         if (grow(&s->d_order, &s->order_cap, need)) return nullptr;
         uint32_t* b = static_cast<uint32_t*>(s->d_order);
         s->sched.order = b;
         s->sched.cost_prev = b + nb;
         s->sched.cost_cur = b + 2 * nb;
+        s->sched.px_prev = reinterpret_cast<uint16_t*>(b + 3 * nb);
+        s->sched.px_cur = s->sched.px_prev + (size_t)nb * 256;
+        s->sched.perm = reinterpret_cast<uint8_t*>(s->sched.px_cur + (size_t)nb * 256);
         s->sched.have_prev = false;
         std::memcpy(s->sched_key, key, sizeof(key));
     }
@@ -145,6 +149,7 @@ rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint
 void sched_done(rt_scene* s) {
     if (!rt::g_trace_config.tile_order) return;
     std::swap(s->sched.cost_prev, s->sched.cost_cur);
+    std::swap(s->sched.px_prev, s->sched.px_cur);
     s->sched.have_prev = true;
 }
 
@@ -180,6 +185,7 @@ rt_status rt_config_set(const char* key, int64_t value) {
     else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
     else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) rt::g_trace_config.wg_tiles = (uint32_t)value;
     else if (k == "trace.tile_order" && (value == 0 || value == 1)) rt::g_trace_config.tile_order = (uint32_t)value;
+    else if (k == "trace.px_sort" && value >= 0 && value <= 2) rt::g_trace_config.px_sort = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
     else if (k == "build.sort" && (value == 0 || value == 1)) rt::g_trace_config.sort_msb = (uint32_t)value;
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) rt::g_trace_config.wide_collapse = (uint32_t)value;

@@ -88,6 +88,8 @@ struct TraceConfig {
     uint32_t stage_events = 0;  // build: record the per-stage events (rt_bvh_build_times); else total only
     uint32_t event_fence = 0;   // timing events with the system-scope fence (scenes created afterwards)
     uint32_t tile_order = 1;    // 1: longest-first from the previous same-size frame's wave times; 0: row-major
+    uint32_t px_sort = 1;       // with tile_order: each tile's pixels to lanes costliest first (previous
+                                // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbMaxN, 0 = 4-pass LSB always
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
@@ -98,6 +100,9 @@ struct TileSched {
     uint32_t* order = nullptr;      // [nb] dispatch index -> tile slot
     uint32_t* cost_prev = nullptr;  // [nb] previous frame's per-tile wave time
     uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
+    uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
+    uint16_t* px_cur = nullptr;     // [nb][256] this frame's
+    uint8_t* perm = nullptr;        // [nb][256] lane -> local pixel, from px_prev
     bool have_prev = false;
 };
 extern TraceConfig g_trace_config;

@@ -468,7 +468,9 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                                unsigned long long* __restrict__ counters,
                                                const float* __restrict__ tris = nullptr, Light lt = Light{},
                                                const uint32_t* __restrict__ order = nullptr,
-                                               uint32_t* __restrict__ cost_out = nullptr) {
+                                               uint32_t* __restrict__ cost_out = nullptr,
+                                               const uint8_t* __restrict__ perm = nullptr,
+                                               uint16_t* __restrict__ px_cost = nullptr) {
     __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     // tile slot from the block id: consecutive tiles go to different XCDs
@@ -483,10 +485,19 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
     const uint32_t t = rank + slot * nranks;
     const uint32_t tx = t % tilesX, ty = t / tilesX;
     const uint32_t l = threadIdx.x & 63, w = gw & 3;
-    const uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
+    // pixel of this lane: the 8x8 quadrant w of the tile, or (trace.px_sort,
+    // from the 2nd frame of a shape on) the tile's pixels ordered costliest
+    // first by the previous frame's per-pixel step counts, so the tile's
+    // expensive rays share a wave instead of stretching all four
+    uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
+    if (perm) {
+        const uint32_t li = perm[(uint64_t)slot * 256 + w * 64 + l];
+        lx = li & 15;
+        ly = li >> 4;
+    }
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
-    uint32_t cn = 0, ct = 0;
+    uint32_t cn = 0, ct = 0, steps = 0;
     const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #ifdef RT_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
@@ -520,6 +531,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                           R.tb, R.hu, R.hv, R.hp, cn, ct);
                 }
                 tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
+                steps += R.steps + (st == 2 ? 64u : 0u);  // a binary finish: a nominal charge
             } else {
                 trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
             }
@@ -587,6 +599,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             atomicAdd(&counters[1], bsum);
         }
     }
+    if (px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
     if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
         atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
@@ -1239,6 +1252,38 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict_
     }
 }
 
+// trace.px_sort: per tile slot, its 256 pixels ordered costliest first by
+// the previous frame's per-pixel step counts (k_trace's px_cost), as local
+// pixel indices ly * 16 + lx -- a permutation whatever the costs (counting
+// sort; order within a bucket free).  k_trace lane j of wave w renders pixel
+// perm[slot][w * 64 + j].
+__global__ __launch_bounds__(256) void k_tile_perm(const uint16_t* __restrict__ px_cost, uint8_t* __restrict__ perm) {
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_sum[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t base = (uint64_t)blockIdx.x * 256;
+    s_hist[tid] = 0u;
+    __syncthreads();
+    const uint32_t bk = 255u - cost_bucket(px_cost[base + tid]);
+    atomicAdd(&s_hist[bk], 1u);
+    __syncthreads();
+    const uint32_t v = s_hist[tid];
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_sum[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
+    __syncthreads();
+    s_hist[tid] = pre + x - v;
+    __syncthreads();
+    perm[base + atomicAdd(&s_hist[bk], 1u)] = (uint8_t)tid;
+}
+
 // ================================================================ launchers
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
     const uint32_t nt = ((w + 15) / 16) * ((h + 15) / 16);
@@ -1310,9 +1355,24 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         cost_out = sched->cost_cur;
     }
     if (g_trace_config.order_override) order = g_trace_config.order_override;
+    const uint8_t* perm = nullptr;
+    uint16_t* px_cost = nullptr;
+    // full frames only by default: a frame is issue-bound and the sort cuts the
+    // instructions its costly tiles issue; one rank's share of a multi-GPU
+    // frame is bound by its slowest wave, which a wave of 64 costly rays
+    // (more lanes in both branches of every step) only lengthens
+    // (DESIGN.md "Pixel order")
+    if (cost_out && sched->px_cur && (g_trace_config.px_sort == 2 || (g_trace_config.px_sort == 1 && nranks == 1))) {
+        if (sched->have_prev) {
+            hipLaunchKernelGGL(k_tile_perm, dim3(nb), dim3(256), 0, s, sched->px_prev, sched->perm);
+            perm = sched->perm;
+        }
+        px_cost = sched->px_cur;
+    }
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
     hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
-                       cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, cost_out)
+                       cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, cost_out, \
+                       perm, px_cost)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \

@@ -339,19 +339,33 @@ def test_tiled_render_matches_full(R, oracle):
             assert np.array_equal(img.cpu().numpy().view(np.uint8), full), P
 
 
-def test_tile_order_successive_frames(R, oracle):
+@pytest.mark.parametrize("px_sort", [1, 0, 2])
+def test_tile_order_successive_frames(R, oracle, px_sort):
     """Longest-first tile dispatch from the previous frame's cost map (the
     default): the 1st frame runs row-major, later frames reordered -- every
     frame bit-identical to the oracle, full image and per-rank tiles alike,
-    and a frame of another shape starts a fresh map."""
-    import torch
-    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    and a frame of another shape starts a fresh map.  px_sort: each tile's
+    pixels dealt to lanes costliest first from the previous frame's per-pixel
+    steps (1 = full frames, the default; 2 = also per-rank tiles; 0 = off);
+    the 250x138 frames leave invalid pixels in the edge tiles' permutations."""
     tris = soup(oracle, 60000, 12)
     exp = oracle.build(tris)
     R.config_set("trace.tile_order", 1)
+    R.config_set("trace.px_sort", px_sort)
+    try:
+        _successive_frames(R, oracle, s_tris=tris, exp=exp)
+    finally:
+        R.config_set("trace.px_sort", 1)
+
+
+def _successive_frames(R, oracle, s_tris, exp):
+    import torch
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    tris = s_tris
     with R.Scene.from_soup(tris) as s:
         s.build()
-        for (w, h, spp) in [(256, 144, 1), (256, 144, 1), (200, 120, 2), (256, 144, 1), (256, 144, 1)]:
+        for (w, h, spp) in [(256, 144, 1), (256, 144, 1), (200, 120, 2), (256, 144, 1), (256, 144, 1),
+                            (250, 138, 1), (250, 138, 1), (250, 138, 1)]:
             cam = _cam(R, SOUP_VIEW, w, h)
             ocam = oracle.camera_look_at(SOUP_VIEW.eye, SOUP_VIEW.at, SOUP_VIEW.up, SOUP_VIEW.vfov, w, h)
             eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
@@ -360,7 +374,7 @@ def test_tile_order_successive_frames(R, oracle):
             assert np.array_equal(rgba, er)
             assert np.array_equal(hits["prim"], eh["prim"])
             assert np.array_equal(bits(hits["t"]), bits(eh["t"]))
-        w, h, spp, P = 256, 144, 1, 3
+        w, h, spp, P = 250, 138, 1, 3
         cam = _cam(R, SOUP_VIEW, w, h)
         _, full, _ = s.render(cam, w, h, spp, hits=False)
         tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
