@@ -128,8 +128,8 @@ rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint
     const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     const uint32_t key[5] = {w, h, spp, rank, nranks};
     const bool same = std::memcmp(key, s->sched_key, sizeof(key)) == 0;
-    // [order][cost A][cost B] u32, [px A][px B] u16 x 256, [perm] u8 x 256 per tile slot
-    const size_t need = 3ull * nb * 4 + 2ull * nb * 512 + (size_t)nb * 256;
+    // [order][cost A][cost B] u32, [px A][px B] u16 x 256 per tile slot
+    const size_t need = 3ull * nb * 4 + 2ull * nb * 512;
     if (!same || s->order_cap < need) {
         if (grow(&s->d_order, &s->order_cap, need)) return nullptr;
         uint32_t* b = static_cast<uint32_t*>(s->d_order);
@@ -138,7 +138,6 @@ rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint
         s->sched.cost_cur = b + 2 * nb;
         s->sched.px_prev = reinterpret_cast<uint16_t*>(b + 3 * nb);
         s->sched.px_cur = s->sched.px_prev + (size_t)nb * 256;
-        s->sched.perm = reinterpret_cast<uint8_t*>(s->sched.px_cur + (size_t)nb * 256);
         s->sched.have_prev = false;
         std::memcpy(s->sched_key, key, sizeof(key));
     }

@@ -102,7 +102,6 @@ struct TileSched {
     uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
     uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
     uint16_t* px_cur = nullptr;     // [nb][256] this frame's
-    uint8_t* perm = nullptr;        // [nb][256] lane -> local pixel, from px_prev
     bool have_prev = false;
 };
 extern TraceConfig g_trace_config;

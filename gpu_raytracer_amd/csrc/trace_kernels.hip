@@ -459,6 +459,53 @@ __device__ __forceinline__ float shadow_factor(const char* __restrict__ nodes, c
     return lt.ambient + (1.0f - lt.ambient) * lit;
 }
 
+// trace.px_sort: a 256-thread block deals its tile's 256 pixels to its four
+// waves costliest first by the previous frame's per-pixel step counts
+// (px_prev, written by k_trace), computed at block start (no extra launch).
+// Only the wave a pixel lands in matters, so a 16-bucket key (two per octave
+// of the step count) is enough; the ranking is atomic-free -- per wave one
+// ballot per bucket, then position = pixels in costlier buckets + same-bucket
+// pixels of earlier waves + the lane's rank in its own ballot -- so it is a
+// permutation whatever the costs.  Returns the local pixel (ly * 16 + lx) of
+// thread tid.  Called by all 256 threads.
+__device__ __forceinline__ uint32_t px_bucket(uint32_t c) {
+    if (c < 4) return 0u;
+    const uint32_t e = 31u - (uint32_t)__clz((int)c);  // c in [2^e, 2^(e+1)), e >= 2
+    return min(15u, 2u * (e - 2u) + ((c >> (e - 1u)) & 1u));
+}
+
+__device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict__ px_prev, uint32_t tid) {
+    __shared__ uint32_t s_cnt[4][16];  // [wave][bucket] pixel counts
+    __shared__ uint32_t s_pre[16];     // pixels in costlier buckets
+    __shared__ uint8_t s_perm[256];
+    const uint32_t lane = tid & 63, wv = tid >> 6;
+    const uint32_t b = 15u - px_bucket(px_prev[tid]);  // 0 = costliest
+    uint32_t rank = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) {
+        const uint64_t m = __ballot(b == k);
+        if (b == k) rank = lanes_below(m);
+        if (lane == k) s_cnt[wv][k] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 16 bucket totals in wave 0
+        const uint32_t tot = tid < 16 ? s_cnt[0][tid] + s_cnt[1][tid] + s_cnt[2][tid] + s_cnt[3][tid] : 0u;
+        uint32_t x = tot;
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (tid < 16) s_pre[tid] = x - tot;
+    }
+    __syncthreads();
+    uint32_t pos = s_pre[b] + rank;
+    for (uint32_t q = 0; q < wv; ++q) pos += s_cnt[q][b];
+    s_perm[pos] = (uint8_t)tid;
+    __syncthreads();
+    return s_perm[tid];
+}
+
 template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false>
 __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
@@ -469,7 +516,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                                const float* __restrict__ tris = nullptr, Light lt = Light{},
                                                const uint32_t* __restrict__ order = nullptr,
                                                uint32_t* __restrict__ cost_out = nullptr,
-                                               const uint8_t* __restrict__ perm = nullptr,
+                                               const uint16_t* __restrict__ px_prev = nullptr,
                                                uint16_t* __restrict__ px_cost = nullptr) {
     __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
@@ -486,12 +533,15 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
     const uint32_t tx = t % tilesX, ty = t / tilesX;
     const uint32_t l = threadIdx.x & 63, w = gw & 3;
     // pixel of this lane: the 8x8 quadrant w of the tile, or (trace.px_sort,
-    // from the 2nd frame of a shape on) the tile's pixels ordered costliest
-    // first by the previous frame's per-pixel step counts, so the tile's
-    // expensive rays share a wave instead of stretching all four
+    // 256-thread blocks, from the 2nd frame of a shape on) the tile's pixels
+    // dealt to waves costliest first by the previous frame's per-pixel step
+    // counts, so the tile's expensive rays share a wave instead of
+    // stretching all four.  Primary-ray full frames only: compiled out of the
+    // shadow, counting and 64-thread variants, whose registers it would cost.
+    constexpr bool PX = !SHADOW && !COUNT && NT == 256;
     uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
-    if (perm) {
-        const uint32_t li = perm[(uint64_t)slot * 256 + w * 64 + l];
+    if (PX && px_prev) {  // uniform: the whole block
+        const uint32_t li = tile_pixel_order(px_prev + (uint64_t)slot * 256, threadIdx.x);
         lx = li & 15;
         ly = li >> 4;
     }
@@ -531,7 +581,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                           R.tb, R.hu, R.hv, R.hp, cn, ct);
                 }
                 tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
-                steps += R.steps + (st == 2 ? 64u : 0u);  // a binary finish: a nominal charge
+                if (PX) steps += R.steps + (st == 2 ? 64u : 0u);  // a binary finish: a nominal charge
             } else {
                 trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
             }
@@ -599,7 +649,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             atomicAdd(&counters[1], bsum);
         }
     }
-    if (px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
+    if (PX && px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
     if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
         atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
@@ -1252,38 +1302,6 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict_
     }
 }
 
-// trace.px_sort: per tile slot, its 256 pixels ordered costliest first by
-// the previous frame's per-pixel step counts (k_trace's px_cost), as local
-// pixel indices ly * 16 + lx -- a permutation whatever the costs (counting
-// sort; order within a bucket free).  k_trace lane j of wave w renders pixel
-// perm[slot][w * 64 + j].
-__global__ __launch_bounds__(256) void k_tile_perm(const uint16_t* __restrict__ px_cost, uint8_t* __restrict__ perm) {
-    __shared__ uint32_t s_hist[256];
-    __shared__ uint32_t s_sum[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const uint64_t base = (uint64_t)blockIdx.x * 256;
-    s_hist[tid] = 0u;
-    __syncthreads();
-    const uint32_t bk = 255u - cost_bucket(px_cost[base + tid]);
-    atomicAdd(&s_hist[bk], 1u);
-    __syncthreads();
-    const uint32_t v = s_hist[tid];
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= (uint32_t)o) x += y;
-    }
-    if (lane == 63) s_sum[wv] = x;
-    __syncthreads();
-    uint32_t pre = 0;
-    for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
-    __syncthreads();
-    s_hist[tid] = pre + x - v;
-    __syncthreads();
-    perm[base + atomicAdd(&s_hist[bk], 1u)] = (uint8_t)tid;
-}
-
 // ================================================================ launchers
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
     const uint32_t nt = ((w + 15) / 16) * ((h + 15) / 16);
@@ -1355,24 +1373,23 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         cost_out = sched->cost_cur;
     }
     if (g_trace_config.order_override) order = g_trace_config.order_override;
-    const uint8_t* perm = nullptr;
+    const uint16_t* px_prev = nullptr;
     uint16_t* px_cost = nullptr;
     // full frames only by default: a frame is issue-bound and the sort cuts the
     // instructions its costly tiles issue; one rank's share of a multi-GPU
     // frame is bound by its slowest wave, which a wave of 64 costly rays
     // (more lanes in both branches of every step) only lengthens
-    // (DESIGN.md "Pixel order")
-    if (cost_out && sched->px_cur && (g_trace_config.px_sort == 2 || (g_trace_config.px_sort == 1 && nranks == 1))) {
-        if (sched->have_prev) {
-            hipLaunchKernelGGL(k_tile_perm, dim3(nb), dim3(256), 0, s, sched->px_prev, sched->perm);
-            perm = sched->perm;
-        }
+    // (DESIGN.md "Pixel order").  256-thread blocks only (the ranking is per
+    // block).
+    if (cost_out && !small && sched->px_cur &&
+        (g_trace_config.px_sort == 2 || (g_trace_config.px_sort == 1 && nranks == 1))) {
+        if (sched->have_prev) px_prev = sched->px_prev;
         px_cost = sched->px_cur;
     }
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
     hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
                        cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, cost_out, \
-                       perm, px_cost)
+                       px_prev, px_cost)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \
