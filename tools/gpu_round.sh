@@ -1,6 +1,6 @@
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_r01i.log 2>&1 || { tail -30 gpurun_out/t_r01i.log; exit 1; }
-tail -1 gpurun_out/t_r01i.log
-timeout -k 10 300 python -u bench.py > gpurun_out/bench_r01i.json 2> gpurun_out/bench_r01i.err || { tail -20 gpurun_out/bench_r01i.err; exit 1; }
-cat gpurun_out/bench_r01i.json | cut -c1-400
-bash tools/profile.sh r01i
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/t_r01j.log 2>&1 || { tail -30 gpurun_out/t_r01j.log; exit 1; }
+tail -1 gpurun_out/t_r01j.log
+timeout -k 10 300 python -u bench.py > gpurun_out/bench_r01j.json 2> gpurun_out/bench_r01j.err || { tail -20 gpurun_out/bench_r01j.err; exit 1; }
+cat gpurun_out/bench_r01j.json | cut -c1-400
+bash tools/profile.sh r01j
