@@ -266,6 +266,20 @@ __device__ __forceinline__ int kdelta(const KeyWin& keys, int64_t n, int64_t i, 
     return __clz((int)(ki ^ kj));
 }
 
+// 32-bit forms for the per-thread searches (n <= 2^30 at the ABI): an
+// index j = i + m*d is formed modulo 2^32, so a position before 0 wraps
+// above n and both out-of-range cases are the one test j >= n.
+__device__ __forceinline__ uint32_t kkey32(const KeyWin& keys, uint32_t j) {
+    const uint32_t r = j - (uint32_t)keys.lo;
+    return r < (uint32_t)(keys.hi - keys.lo) ? keys.s[r] : keys.g[j];
+}
+__device__ __forceinline__ int kdelta32(const KeyWin& keys, uint32_t n, uint32_t i, uint32_t ki, uint32_t j) {
+    if (j >= n) return -1;
+    const uint32_t kj = kkey32(keys, j);
+    if (ki == kj) return 32 + __clz((int)(i ^ j));
+    return __clz((int)(ki ^ kj));
+}
+
 __device__ __forceinline__ int kdir(const KeyWin& keys, int64_t n, int64_t i) {
     const uint32_t ki = keys[i];
     return (kdelta(keys, n, i, ki, i + 1) - kdelta(keys, n, i, ki, i - 1)) > 0 ? 1 : -1;
@@ -359,27 +373,33 @@ __device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafT
     tp_out = make_uint4(0, 0, 0, 0);
     deferred = false;
     if (i < N - 1) {
-        const uint32_t ki = keys[i];
-        const int d = (kdelta(keys, N, i, ki, i + 1) - kdelta(keys, N, i, ki, i - 1)) > 0 ? 1 : -1;
-        const int dmin = kdelta(keys, N, i, ki, i - d);
-        int64_t lmax = 2;
+        // §9.5 searches in 32-bit index arithmetic (kdelta32); m*d as
+        // (d > 0 ? m : -m) modulo 2^32
+        const uint32_t ki = kkey32(keys, i32);
+        const int d = (kdelta32(keys, n, i32, ki, i32 + 1) - kdelta32(keys, n, i32, ki, i32 - 1)) > 0 ? 1 : -1;
+        const uint32_t ud = (uint32_t)d;  // +1 or 0xFFFFFFFF
+        const int dmin = kdelta32(keys, n, i32, ki, i32 - ud);
+        uint32_t lmax = 2;
         for (;;) {
-            const int64_t q = i + lmax * d;
-            if (allow_defer && q >= 0 && q < N && (q < keys.lo || q >= keys.hi)) { deferred = true; break; }
-            if (!(kdelta(keys, N, i, ki, q) > dmin)) break;
+            const uint32_t q = i32 + lmax * ud;
+            if (allow_defer && q < n && (q - (uint32_t)keys.lo) >= (uint32_t)(keys.hi - keys.lo)) {
+                deferred = true;
+                break;
+            }
+            if (!(kdelta32(keys, n, i32, ki, q) > dmin)) break;
             lmax <<= 1;
         }
         if (!deferred) {
-            int64_t l = 0;
-            for (int64_t t = lmax >> 1; t >= 1; t >>= 1)
-                if (kdelta(keys, N, i, ki, i + (l + t) * d) > dmin) l += t;
-            const int dnode = kdelta(keys, N, i, ki, i + l * d);
-            int64_t s = 0, t = l;
+            uint32_t l = 0;
+            for (uint32_t t = lmax >> 1; t >= 1; t >>= 1)
+                if (kdelta32(keys, n, i32, ki, i32 + (l + t) * ud) > dmin) l += t;
+            const int dnode = kdelta32(keys, n, i32, ki, i32 + l * ud);
+            uint32_t s = 0, t = l;
             do {
                 t = (t + 1) >> 1;
-                if (kdelta(keys, N, i, ki, i + (s + t) * d) > dnode) s += t;
+                if (kdelta32(keys, n, i32, ki, i32 + (s + t) * ud) > dnode) s += t;
             } while (t > 1);
-            tp_out = karras_finish(keys, N, i, d, l, s, topo, parent);
+            tp_out = karras_finish(keys, N, i, d, (int64_t)l, (int64_t)s, topo, parent);
         } else {
             // the crossing flags only need which end of the range i is
             tp_out = make_uint4(0, 0, d > 0 ? i32 : 0u, d > 0 ? RT_SENT - 1 : i32);
