@@ -186,6 +186,26 @@ def test_variants_and_stack_overflow(R, oracle, variant, cap):
     _same(hits, rgba, eh, er)
 
 
+@pytest.mark.parametrize("collapse", [0, 1])
+@pytest.mark.parametrize("cap", [2, 14])
+def test_collapse_rules_render_identically(R, oracle, collapse, cap):
+    """Both K7w cut rules (build.wide_collapse) give the oracle's hits and
+    image, with and without forced stack overflows."""
+    from gpu_raytracer_amd.scenes import SOUP_VIEW as V
+    tris = oracle.soup(40000, 13).reshape(-1, 9)
+    w, h, spp = 120, 72, 1
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    ocam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    eh, er = _oracle_render(oracle, tris, ocam, w, h, spp)
+    R.config_set("build.wide_collapse", collapse)
+    try:
+        hits, rgba = _render_all(R, tris, cam, w, h, spp, 0, cap)
+    finally:
+        R.config_set("build.wide_collapse", 1)
+        R.config_set("trace.stack_cap", 14)
+    _same(hits, rgba, eh, er)
+
+
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_variants_presets(R, oracle, variant):
     from gpu_raytracer_amd import scenes as S
