@@ -139,6 +139,7 @@ rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint
         s->sched.px_prev = reinterpret_cast<uint16_t*>(b + 3 * nb);
         s->sched.px_cur = s->sched.px_prev + (size_t)nb * 256;
         s->sched.have_prev = false;
+        s->sched.fresh = true;
         std::memcpy(s->sched_key, key, sizeof(key));
     }
     return &s->sched;

@@ -103,6 +103,7 @@ struct TileSched {
     uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
     uint16_t* px_cur = nullptr;     // [nb][256] this frame's
     bool have_prev = false;
+    bool fresh = true;              // maps (re)allocated: clear both before the first launch
 };
 extern TraceConfig g_trace_config;
 

@@ -1254,7 +1254,9 @@ __device__ __forceinline__ uint32_t cost_bucket(uint32_t d) {
 
 constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per rank (4K frames)
 
-__global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict__ cost, uint32_t nb,
+// It also clears the map it consumed: after the host's swap that buffer is
+// the one the next frame writes, so no memset is needed per frame.
+__global__ __launch_bounds__(1024) void k_tile_order(uint32_t* __restrict__ cost, uint32_t nb,
                                                      uint32_t* __restrict__ order) {
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_sum[16];
@@ -1268,7 +1270,10 @@ __global__ __launch_bounds__(1024) void k_tile_order(const uint32_t* __restrict_
     for (uint32_t j = 0; j < kOrderPerThread; ++j) {
         const uint32_t i = tid + j * 1024;
         bk[j] = i < nb ? (uint8_t)(255u - cost_bucket(cost[i])) : 0;
-        if (i < nb) atomicAdd(&s_hist[bk[j]], 1u);
+        if (i < nb) {
+            atomicAdd(&s_hist[bk[j]], 1u);
+            cost[i] = 0u;
+        }
     }
     __syncthreads();
     if (tid < 256) {  // exclusive scan of 256 buckets: 4 waves of 64
@@ -1364,12 +1369,16 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     const uint32_t* order = nullptr;
     uint32_t* cost_out = nullptr;
     if (sched && g_trace_config.tile_order && nb <= 1024 * kOrderPerThread) {
+        if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
+            hipError_t me = hipMemsetAsync(sched->cost_prev, 0, (size_t)nb * 4, s);
+            if (me == hipSuccess) me = hipMemsetAsync(sched->cost_cur, 0, (size_t)nb * 4, s);
+            if (me != hipSuccess) return me;
+            sched->fresh = false;
+        }
         if (sched->have_prev) {
             hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order);
             order = sched->order;
         }
-        hipError_t me = hipMemsetAsync(sched->cost_cur, 0, (size_t)nb * 4, s);
-        if (me != hipSuccess) return me;
         cost_out = sched->cost_cur;
     }
     if (g_trace_config.order_override) order = g_trace_config.order_override;
