@@ -186,3 +186,46 @@ def test_bvh_cache_rejects_without_device_work(rt, tmp_path):
         with pytest.raises(rt.RtError) as e:
             s.load_bvh(str(q))
         assert e.value.status == -3
+
+
+# rt_config_set keys: accepted values, a rejected value each, and the default
+# restored afterwards (include/gpu_raytracer_amd.h; INTEGRATION.md "tuning").
+CONFIG_KEYS = {
+    "trace.variant": ([0, 1, 2], [3, -1], 0),
+    "trace.stack_cap": ([1, 14], [0, 15], 14),
+    "trace.wg": ([64, 256], [128], 256),
+    "trace.wg_tiles": ([64, 256], [32], 64),
+    "trace.tile_order": ([0, 1], [2], 1),
+    "trace.px_sort": ([0, 1, 2], [3], 1),
+    "trace.blocks": ([0, 4096], [-1], 0),
+    "build.sort": ([0, 1], [2], 1),
+    "build.wide_collapse": ([0, 1], [2, -1], 1),
+    "build.stage_events": ([0, 1], [2], 0),
+    "timing.event_fence": ([0, 1], [2], 0),
+    "path.wavefront": ([0, 1], [2], 1),
+    "path.wg": ([64, 256], [100], 64),
+    "path.sort": ([0, 4], [5], 0),
+    "path.batch": ([0, 1 << 20], [-1], 0),
+}
+
+
+@pytest.mark.parametrize("key", sorted(CONFIG_KEYS))
+def test_config_keys(rt, key):
+    """Every tuning knob takes its documented values and rejects others with
+    RT_EINVAL (no device needed: the knobs are host-side state)."""
+    good, bad, default = CONFIG_KEYS[key]
+    try:
+        for v in good:
+            rt.config_set(key, v)
+        for v in bad:
+            with pytest.raises(rt.RtError) as e:
+                rt.config_set(key, v)
+            assert e.value.status == -1
+    finally:
+        rt.config_set(key, default)
+
+
+def test_config_unknown_key(rt):
+    with pytest.raises(rt.RtError) as e:
+        rt.config_set("trace.no_such_knob", 1)
+    assert e.value.status == -1
