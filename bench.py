@@ -2,8 +2,10 @@
 """Headline benchmark: Mrays/s @1920x1080x1spp + BVH-build Mprims/s on the
 1M-triangle synthetic soup (BASELINE.json configs[2]), 1..N GPUs.
 
-One STEP = one frame of the hot path on inputs already resident in HBM:
-  rt_bvh_build (K0..K6, replicated on every rank) -> trace this rank's image
+One STEP = one frame of the hot path on inputs already resident in HBM, with
+the camera orbiting the scene 0.25 degrees per step (so no frame repeats the
+previous one):
+  rt_bvh_build (K0..K7w, replicated on every rank) -> trace this rank's image
   tiles (K8/K9; full image on one GPU) -> [N>1] RCCL gather of the packed
   tiles to rank 0 (torch.distributed 'nccl' == RCCL) + unpack kernel.
 W untimed warm-up steps, then K timed steps between barrier+synchronize on
@@ -14,27 +16,40 @@ both sides; the max over ranks is reported by rank 0 as ONE JSON line.
                trace, the RCCL gather and the unpack are queued back to back
                on torch's stream and timed together with events on it
                (gather time = that span minus the trace)
+  value_cold = the same frame with row-major tile dispatch (a first frame: no
+               previous frame's cost map); static_camera = the same camera
+               every frame (the map replays an identical frame: best case)
   build_mprims_per_s = N_tris / mean build time (per GPU; replicated)
   ms_per_step = wall time per frame incl. build, trace, gather and host syncs
 Device times come from hipEvents recorded on the stream each kernel runs on
-(the scene's stream inside librtamd).
+(the scene's stream inside librtamd, or torch's stream at N>1).
 
-roofline: the dominant kernel (trace) -- algorithmic bytes per launch =
-  32 B x nodes fetched + 36 B x tris tested + 16 B x rays (SURVEY.md §8(d):
-  the §9.7 binary traversal's deterministic counters, which the oracle
-  reproduces), over its mean event-timed duration, against 8.0 TB/s HBM.
-  The default kernel traverses the K7w wide (4-ary) records instead; the
-  bytes IT requests (64 B x records + 48 B x triangle records + 20 B x rays,
-  its own deterministic counters) are reported beside as kernel_bytes.
+Launch: `python bench.py --gpus N` spawns N rank processes itself (one per
+GPU, before any of them touches the GPU); under torch.distributed.run the
+ranks come from the environment.
+
+roofline: the trace launch (k_tile_order + k_trace) -- the bytes the kernel
+  requests (64 B per K7w record + 48 B per triangle record fetched, its own
+  deterministic counters, + 16 B hit + 4 B RGBA written per ray) over its
+  event-timed duration, against the 8.0 TB/s HBM peak; beside it the PMC
+  measured HBM bytes (hbm_frac) and VALU issue (issue_frac) of the same
+  kernel from the committed profile (profiles/pmc_summary.json); `bound` is
+  the largest of the three.  The SURVEY.md §8(d) binary-traversal byte model
+  is kept as algo_bytes_binary_model (it charges node visits the wide kernel
+  does not make, so its fraction is not a roofline of this kernel).
 cpu_baseline (rank 0, N=1 only): the CPU oracle (oracle/, a port of the same
-  contract -- the reference has no runnable code) builds the same 1M soup
-  single-threaded and traces the same full frame on up to 16 host threads.
+  contract -- the reference has no runnable code), built on this host with
+  -O3 -march=native, builds the same 1M soup single-threaded and traces the
+  same full frame on every CPU this process may use.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -46,6 +61,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
 BUILD_BYTES_PER_PRIM = 404  # SURVEY.md §8(d) canonical build byte model
 METRIC = "Mrays/s @1920×1080×1spp + BVH build Mprims/s, 1M-tri scene, 1/2/4/8 GPUs"
+ORBIT_DEG = 0.25  # camera motion per step
+# VALU issue peak: 256 CUs x 4 SIMDs, a wave64 VALU op issues over 2 cycles
+# (MI355X_MICROARCH.md "v_fma_f32 (wave64) 2 cyc (SIMD-32)")
+VALU_ISSUE_PER_CYCLE = 1024 * 0.5
 
 
 def parse():
@@ -55,19 +74,53 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=3, help="scenes.CONFIGS key (3 = soup-1M headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_trace.json"))
+    ap.add_argument("--no-extra", action="store_true", help="skip the other configs / secondary modes")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     ap.add_argument("--dump", default="", help="write the rank-0 image as PPM")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for the benchmark; gloo only to rehearse N>1 on one GPU")
     return ap.parse_args()
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N rank processes (one per
+    GPU) with the torch.distributed env, before anything here touches a GPU;
+    rank 0 prints the JSON line.  Returns the worst exit status."""
+    port = str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, abs(p.wait()))
+    return rc
+
+
+def orbit_view(view, step):
+    """The view's eye rotated about the vertical axis through `at` by
+    ORBIT_DEG per step (host double math, like rt_camera_look_at)."""
+    a = math.radians(ORBIT_DEG * step)
+    ex, ey, ez = (e - c for e, c in zip(view.eye, view.at))
+    rx, rz = ex * math.cos(a) + ez * math.sin(a), -ex * math.sin(a) + ez * math.cos(a)
+    return (view.at[0] + rx, view.at[1] + ey, view.at[2] + rz)
+
+
 def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters):
-    """Oracle build (1 thread) + full-frame trace (threads); returns dict."""
+    """Oracle (-march=native build) build on 1 thread + full-frame trace on
+    `threads` threads; returns dict."""
     from oracle import oracle as O  # cpu_baseline leg only
-    if not os.path.exists(O._LIB_PATH):
-        O.build_oracle()
+    O.use_native_build()
     t0 = time.perf_counter()
     b = O.build(tris)
     t_build = time.perf_counter() - t0
@@ -86,15 +139,31 @@ def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters):
     rays = w * h * spp
     return {
         "value": rays / t_trace / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-        "sample": f"full frame {w}x{h}x{spp} traced on {threads} threads ({t_trace:.2f} s); "
-                  f"full {len(tris)}-tri BVH built on 1 thread ({t_build:.2f} s)",
+        "threads_used": threads, "cores_available": len(os.sched_getaffinity(0)),
+        "cpus_in_machine": os.cpu_count(),
+        "sample": f"full frame {w}x{h}x{spp} (static camera) traced on {threads} threads ({t_trace:.2f} s); "
+                  f"full {len(tris)}-tri BVH built on 1 thread ({t_build:.2f} s); oracle built -O3 -march=native "
+                  f"-ffp-contract=off on this host",
         "build_mprims_per_s": len(tris) / t_build / 1e6, "build_threads": 1,
         "cpu_model": model,
         "counters_match_gpu": bool(int(cnt[0]) == int(gpu_counters[0]) and int(cnt[1]) == int(gpu_counters[1])),
     }
 
 
-def secondary_rays(R, S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev, primary_ms):
+def load_pmc(path, cfg_name, world):
+    """PMC summary of the trace kernel (tools/pmc_summary.py output) for this
+    config and GPU count, or None."""
+    try:
+        pj = json.load(open(path))
+    except Exception:
+        return None
+    for e in pj.get("entries", []):
+        if e.get("config") == cfg_name and e.get("n_gpus", 1) == world:
+            return e
+    return None
+
+
+def secondary_rays(S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev, primary_ms):
     """SURVEY.md §8(f) row 3, shadow mode: the same frame with one
     any-hit shadow ray per primary hit.  Untimed by the step contract; its own
     warm-up and timed launches (hipEvents), median reported."""
@@ -121,12 +190,9 @@ PATH_DEPTH = 2   # bounces after the primary segment
 PATH_SKY = 0.3
 
 
-def path_tracing(R, S, scene, cfg, cam, w, h, spp, img, args, torch, dev):
+def path_tracing(S, scene, cfg, cam, w, h, spp, img, args, torch, dev):
     """SURVEY.md §8(f) row 3, path mode: diffuse paths of up to
-    1 + PATH_DEPTH segments with a shadow ray at every hit, same frame.
-    Untimed by the step contract; its own warm-up and timed launches
-    (hipEvents), median reported; the ray count comes from the kernel's own
-    counters (deterministic: the same paths every launch)."""
+    1 + PATH_DEPTH segments with a shadow ray at every hit, same frame."""
     light = S.LIGHTS[cfg.scene]
     ms = []
     for i in range(args.warmup + max(args.steps, 3)):
@@ -144,15 +210,61 @@ def path_tracing(R, S, scene, cfg, cam, w, h, spp, img, args, torch, dev):
             "node_records": int(work[0]), "tri_records": int(work[1])}
 
 
+def make_scene(R, S, cfg):
+    if cfg.scene == "soup":
+        return R.Scene.generate_soup(cfg.n, 1)
+    return R.Scene.from_soup(S.tris_for(cfg.scene))
+
+
+def other_config(R, S, key, torch, dev, steps=8, warmup=2):
+    """One N=1 line for another BASELINE config (untimed by the step
+    contract): build + full-frame trace, static camera, with its row-major
+    (cold) time and the kernel's own byte rate."""
+    cfg = S.CONFIGS[key]
+    view = S.VIEWS[cfg.scene]
+    w, h, spp = cfg.w, cfg.h, cfg.spp
+    scene = make_scene(R, S, cfg)
+    scene.set_device(dev.index or 0)
+    cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    img = torch.zeros(w * h, dtype=torch.int32, device=dev)
+    hits = torch.empty(w * h * spp * 4, dtype=torch.float32, device=dev)
+    b, t = [], []
+    for i in range(warmup + steps):
+        bm = scene.build()
+        tm = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+        if i >= warmup:
+            b.append(bm)
+            t.append(tm)
+    R.config_set("trace.tile_order", 0)
+    cold = float(np.median([scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(),
+                                                timed=True) for _ in range(4)]))
+    R.config_set("trace.tile_order", 1)
+    wk = scene.render_work(cam, w, h, spp)
+    rays = w * h * spp
+    kb = 64.0 * float(wk[0]) + 48.0 * float(wk[1]) + 16.0 * rays + 4.0 * w * h
+    tr, bd = float(np.mean(t)), float(np.mean(b))
+    scene.close()
+    return {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{key - 1}])", "n_tris": cfg.n,
+            "n_gpus": 1, "value": round(rays / (tr * 1e-3) / 1e6, 2), "unit": "Mrays/s",
+            "value_cold": round(rays / (cold * 1e-3) / 1e6, 2), "trace_ms": round(tr, 4),
+            "trace_ms_row_major": round(cold, 4), "build_ms": round(bd, 4),
+            "build_mprims_per_s": round(cfg.n / (bd * 1e-3) / 1e6, 2),
+            "build_roofline_frac": round(BUILD_BYTES_PER_PRIM * cfg.n / (bd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "kernel_bytes_per_launch": kb,
+            "kernel_frac": round(kb / (tr * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "scene_variant": "splitmix64 soup (SURVEY.md §9.9)" if cfg.scene == "soup"
+            else "procedural substitute (SURVEY.md §9.9; no asset files offline)"}
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if args.gpus > 1 and world == 1:
-            raise SystemExit("for --gpus N>1 launch with torch.distributed.run --nproc-per-node N")
-        world = max(world, 1)
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
 
     import torch
     import torch.distributed as dist
@@ -173,13 +285,12 @@ def main():
     view = S.VIEWS[cfg.scene]
     w, h, spp = cfg.w, cfg.h, cfg.spp
     rays = w * h * spp
-    if cfg.scene == "soup":
-        scene = R.Scene.generate_soup(cfg.n, 1)
-    else:
-        scene = R.Scene.from_soup(S.tris_for(cfg.scene))
+    scene = make_scene(R, S, cfg)
     n_tris = scene.num_tris
     scene.set_device(local)
-    cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    cam_static = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    cams = [R.camera_look_at(orbit_view(view, i), view.at, view.up, view.vfov, w, h)
+            for i in range(args.warmup + args.steps)]
 
     tmax = D.slab_tiles(w, h, world)
     dev = torch.device("cuda", local)
@@ -189,15 +300,12 @@ def main():
     # every rank writes its hit records too (16 B/ray, part of the byte model); only RGBA is gathered
     slab_hits = torch.empty(max(tmax, 1) * 256 * spp * 4, dtype=torch.float32, device=dev) if world > 1 else None
     slabs_all = torch.zeros(world * max(tmax, 1) * 256, dtype=torch.int32, device=dev) if (world > 1 and rank == 0) else None
-    gather_list = None  # gather_slabs receives straight into slabs_all's per-rank rows
-
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
-    def step():
-        build_ms = scene.build()
+    def frame(cam):
+        """trace (+ gather + unpack) of one frame; returns (trace_ms, gather_ms)."""
         if world == 1:
-            trace_ms = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
-            return build_ms, trace_ms, 0.0
+            return scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True), 0.0
         cur = torch.cuda.current_stream(dev)
         if args.dist_backend == "nccl":
             # trace -> RCCL gather -> unpack queued back to back on torch's
@@ -207,14 +315,14 @@ def main():
             scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
                                       stream=cur.cuda_stream)
             ev[1].record(cur)
-            D.gather_slabs(slab, rank, world, gather_list, slabs_all)
+            D.gather_slabs(slab, rank, world, None, slabs_all)
             if rank == 0:
                 R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
                                       cur.cuda_stream)
             ev[2].record(cur)
             ev[2].synchronize()
             trace_ms = ev[0].elapsed_time(ev[1])
-            return build_ms, trace_ms, ev[0].elapsed_time(ev[2]) - trace_ms
+            return trace_ms, ev[0].elapsed_time(ev[2]) - trace_ms
         # gloo rehearsal: stage through host memory, host-timed
         trace_ms = scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
                                              timed=True)
@@ -223,54 +331,73 @@ def main():
         if rank == 0:
             slabs_all.copy_(g)
             R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
-                                  cur.cuda_stream)
+                                  torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
-        return build_ms, trace_ms, (time.perf_counter() - t0) * 1e3
+        return trace_ms, (time.perf_counter() - t0) * 1e3
+
+    def step(i):
+        build_ms = scene.build()
+        return (build_ms,) + frame(cams[i])
 
     def barrier():
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
 
-    for _ in range(args.warmup):
-        step()
+    for i in range(args.warmup):
+        step(i)
     barrier()
     t0 = time.perf_counter()
-    rec = [step() for _ in range(args.steps)]
+    rec = [step(args.warmup + i) for i in range(args.steps)]
     barrier()
     wall = time.perf_counter() - t0
     per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, gather (ms)
-    # the same frame with row-major tile dispatch (untimed by the step contract):
-    # the timed steps dispatch tiles longest-first from the previous frame's
-    # per-tile wave times (trace.tile_order 1, DESIGN.md "Tile order")
+    rank_trace_ms = float(per[:, 1].mean())
+
+    # ---- beside the timed steps (untimed by the step contract)
+    # the same moving sequence with row-major dispatch = every frame cold
     R.config_set("trace.tile_order", 0)
-    rm = []
-    for _ in range(6):
-        if world == 1:
-            rm.append(scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True))
-        else:
-            rm.append(scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
-                                                timed=True))
+    cold = [frame(cams[args.warmup + i])[0] for i in range(args.steps)]
     R.config_set("trace.tile_order", 1)
-    trace_ms_row_major = float(np.median(rm[1:]))
-    # per-stage breakdown from one extra, untimed build with the stage events
-    # on (each adds a little to the GPU timeline, so the timed steps run without)
+    # static camera: the map replays an identical frame (best case)
+    static = [frame(cam_static)[0] for _ in range(args.steps + 1)][1:]
+    # per-stage breakdown from one extra build with the stage events on
     R.config_set("build.stage_events", 1)
     stage_total_ms = scene.build()
     stimes = scene.build_times()
     R.config_set("build.stage_events", 0)
 
+    # work counters of this rank's timed frames (deterministic; untimed)
+    kernel_bytes = 0.0
+    algo_bytes = 0.0
+    rank_rays = D.rays_of_rank(w, h, spp, rank, world)
+    rank_px = rank_rays // spp
+    cnt0 = None
+    for i in range(args.steps):
+        c = cams[args.warmup + i]
+        if world > 1:
+            wk, bc = scene.render_tiles_work(c, w, h, spp, rank, world), scene.render_tiles_counters(c, w, h, spp, rank, world)
+        else:
+            wk, bc = scene.render_work(c, w, h, spp), scene.render_counters(c, w, h, spp)
+        kernel_bytes += 64.0 * float(wk[0]) + 48.0 * float(wk[1]) + 16.0 * rank_rays + 4.0 * rank_px
+        algo_bytes += 32.0 * float(bc[0]) + 36.0 * float(bc[1]) + 16.0 * rank_rays
+    cnt_static = (scene.render_tiles_counters(cam_static, w, h, spp, rank, world) if world > 1
+                  else scene.render_counters(cam_static, w, h, spp))
+    kernel_bytes /= args.steps
+    algo_bytes /= args.steps
+
     # max over ranks (per step), then mean over steps
+    extra = np.array([float(np.mean(cold)), float(np.median(static))], dtype=np.float64)
     if world > 1:
         rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
         t = torch.tensor(per, dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         per = t.cpu().numpy()
-        wt = torch.tensor([wall], dtype=torch.float64, device=rdev)
-        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
-        wall = float(wt.item())
+        t = torch.tensor(np.append(extra, wall), dtype=torch.float64, device=rdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        extra, wall = t.cpu().numpy()[:2], float(t[2].item())
     build_ms, trace_ms, gather_ms = (float(x) for x in per.mean(axis=0))
-    trace_ms_min = float(per[:, 1].min())
+    cold_ms, static_ms = (float(x) for x in extra)
 
     # "rank 0 builds and then broadcasts" measured next to the
     # replicated build (untimed by the step contract; 1 warm-up + 3 timed)
@@ -294,28 +421,21 @@ def main():
         except Exception as exc:  # a measurement only: never fail the bench line over it
             bvh_exchange = {"error": f"{type(exc).__name__}: {exc}"[:200]}
 
-    # work counters of this rank's trace launch (deterministic; untimed)
-    cnt = scene.render_tiles_counters(cam, w, h, spp, rank, world) if world > 1 else scene.render_counters(cam, w, h, spp)
-    rank_rays = D.rays_of_rank(w, h, spp, rank, world)
-    algo_bytes = 32.0 * float(cnt[0]) + 36.0 * float(cnt[1]) + 16.0 * rank_rays
-    rank_trace_ms = float(np.array(rec)[:, 1].mean())
-    achieved = algo_bytes / (rank_trace_ms * 1e-3) / 1e9
-    kernel_bytes = None
-    if world == 1:
-        wk = scene.render_work(cam, w, h, spp)
-        kernel_bytes = 64.0 * float(wk[0]) + 48.0 * float(wk[1]) + 20.0 * rank_rays
-    traffic = None
-    if os.path.exists(args.traffic_json):
-        try:
-            tj = json.load(open(args.traffic_json))
-            if tj.get("config") == cfg.name and tj.get("n_gpus", 1) == world:
-                traffic = tj.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-
     out = None
     if rank == 0:
         value = rays / ((trace_ms + gather_ms) * 1e-3) / 1e6
+        achieved = kernel_bytes / (rank_trace_ms * 1e-3) / 1e9
+        frac = achieved / HBM_PEAK_GBS
+        pmc = load_pmc(args.pmc_json, cfg.name, world)
+        hbm_frac = issue_frac = traffic = None
+        if pmc:
+            traffic = pmc.get("hbm_bytes_per_launch")
+            if traffic:
+                hbm_frac = traffic / (rank_trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+            if pmc.get("valu_insts_per_launch") and pmc.get("cycles_per_launch"):
+                issue_frac = pmc["valu_insts_per_launch"] / (VALU_ISSUE_PER_CYCLE * pmc["cycles_per_launch"])
+        cands = {"memory_requests": frac, "hbm": hbm_frac, "valu_issue": issue_frac}
+        bound = max((k for k in cands if cands[k] is not None), key=lambda k: cands[k])
         build_gbs = BUILD_BYTES_PER_PRIM * n_tris / (build_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
@@ -329,60 +449,85 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: random-triangle soup, splitmix64 seed 1, r=1/cbrt(N) (SURVEY.md §9.9)"
-                    if cfg.scene == "soup" else f"synthetic: procedural {cfg.name} (SURVEY.md §9.9)",
+            "data": ("synthetic: random-triangle soup, splitmix64 seed 1, r=1/cbrt(N) (SURVEY.md §9.9)"
+                     if cfg.scene == "soup" else f"synthetic: procedural {cfg.name} (SURVEY.md §9.9)")
+                    + f"; camera orbiting {ORBIT_DEG} deg per step (every frame differs)",
             "config": {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{args.config - 1}])",
                        "n_tris": n_tris, "width": w, "height": h, "spp": spp,
+                       "camera": f"soup view orbiting {ORBIT_DEG} deg/step about the vertical axis through look-at",
                        "parallelism": f"image tiles 16x16 round-robin over {world} GPU(s), BVH replicated"
                                       + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else ", gloo gather (rehearsal)") if world > 1 else "")},
             "build_mprims_per_s": round(n_tris / (build_ms * 1e-3) / 1e6, 2),
             "build_ms": round(build_ms, 4),
             "trace_ms": round(trace_ms, 4),
-            "trace_ms_min": round(trace_ms_min, 4),
-            "tile_order": "longest-first from the previous frame's per-tile wave times (32 KB cost map per frame "
-                          "shape; the first frame runs row-major)",
-            "trace_ms_row_major_rank0": round(trace_ms_row_major, 4),
             "gather_ms": round(gather_ms, 4),
+            "value_cold": round(rays / ((cold_ms + gather_ms) * 1e-3) / 1e6, 2),
+            "value_static_camera_best_case": round(rays / ((static_ms + gather_ms) * 1e-3) / 1e6, 2),
+            "tile_order": {"timed": "longest-first from the previous frame's per-tile wave times (the camera moved "
+                                    f"{ORBIT_DEG} deg since)",
+                           "trace_ms_moving_ordered": round(trace_ms, 4),
+                           "trace_ms_moving_row_major": round(cold_ms, 4),
+                           "trace_ms_static_ordered": round(static_ms, 4),
+                           "gain_moving": round(cold_ms / trace_ms, 4)},
             "bvh_exchange": bvh_exchange,
             "frame_mrays_per_s": round(rays / (wall / args.steps) / 1e6, 2),
             "build_stages_ms_last": {"bounds": round(stimes.bounds, 4), "morton": round(stimes.morton, 4),
                                      "sort": round(stimes.sort, 4), "topology": round(stimes.topology, 4),
                                      "refit": round(stimes.refit, 4), "wide": round(stimes.wide, 4),
                                      "total_with_stage_events": round(stage_total_ms, 4)},
-            "trace_counters_rank0": {"nodes_fetched": int(cnt[0]), "tris_tested": int(cnt[1]), "rays": rank_rays},
-            "roofline": {"bound": "hbm", "kernel": "k_trace<wide>", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
-                         "algo_bytes_per_launch": algo_bytes,
-                         "kernel_bytes_per_launch": kernel_bytes,
-                         "kernel_frac": (round(kernel_bytes / (rank_trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-                                         if kernel_bytes else None),
-                         "note": "algorithmic bytes (SURVEY.md §8(d): 32/node + 36/tri + 16/ray over the §9.7 "
-                                 "binary traversal's counters); kernel_bytes = what the wide kernel requests "
-                                 "(64/record + 48/tri record + 20/ray). frac can exceed 1: the §8(d) model "
-                                 "charges every binary node visit 32 B as if from HBM, while the kernel fetches "
-                                 "~4x fewer (wide) records from the Infinity-Cache-resident structures; 'traffic' "
-                                 "is the PMC-measured HBM bytes per launch. The kernel is bound by dependent-fetch "
-                                 "latency and VALU issue (DESIGN.md), not HBM bandwidth"},
+            "trace_counters_rank0_static": {"nodes_fetched": int(cnt_static[0]), "tris_tested": int(cnt_static[1]),
+                                            "rays": rank_rays},
+            "roofline": {"bound": bound, "kernel": "trace launch: k_tile_order + k_trace<wide>",
+                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(frac, 4), "traffic": traffic,
+                         "bytes_per_launch": kernel_bytes,
+                         "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
+                         "issue_frac": round(issue_frac, 4) if issue_frac is not None else None,
+                         "pmc_source": (os.path.relpath(args.pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]")
+                         if pmc else None,
+                         "algo_bytes_binary_model": algo_bytes,
+                         "note": "bytes the wide kernel requests per launch (64 B per K7w record + 48 B per "
+                                 "triangle record, its own counters, + 16 B hit + 4 B RGBA per ray) over the "
+                                 "event-timed launch; traffic = PMC HBM bytes per launch (2*FETCH_SIZE + "
+                                 "WRITE_SIZE, gfx950 correction); issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 "
+                                 "x cycles); algo_bytes_binary_model = SURVEY.md §8(d) 32/node + 36/tri + 16/ray "
+                                 "over the §9.7 binary traversal (not what this kernel fetches)"},
             "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
-                               "bytes_per_prim": BUILD_BYTES_PER_PRIM},
+                               "bytes_per_prim": BUILD_BYTES_PER_PRIM,
+                               "note": "SURVEY.md §8(d) 404 B/prim over the event-timed build (launch gaps "
+                                       "included; the rocprof kernel sum is in profiles/)"},
             "cpu_baseline": None,
         }
-        host_img = img.cpu().numpy().view(np.uint8)   # the primary frame, before the secondary modes reuse img
-        if world == 1:
-            out["secondary"] = secondary_rays(R, S, scene, cfg, cam, w, h, spp, img, hits, args, torch, dev,
-                                              float(np.median(per[:, 1])))
-            out["path"] = path_tracing(R, S, scene, cfg, cam, w, h, spp, img, args, torch, dev)
-        if world == 1 and not args.no_cpu_baseline:
-            threads = max(1, min(args.cpu_threads, len(os.sched_getaffinity(0))))
-            out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt)
+        # the static frame: same CRC for every N (bit-exact tiles)
+        frame(cam_static)
+        torch.cuda.synchronize(dev)
+        host_img = img.cpu().numpy().view(np.uint8)
         import zlib
-        out["image_crc32"] = zlib.crc32(host_img.tobytes()) & 0xFFFFFFFF  # same for every N (bit-exact tiles)
+        out["image_crc32"] = zlib.crc32(host_img.tobytes()) & 0xFFFFFFFF
         if args.dump:
             R.dump_ppm(host_img, w, h, args.dump)
-        print(json.dumps(out), flush=True)
+        if world == 1 and not args.no_extra:
+            out["secondary"] = secondary_rays(S, scene, cfg, cam_static, w, h, spp, img, hits, args, torch, dev,
+                                              static_ms)
+            out["path"] = path_tracing(S, scene, cfg, cam_static, w, h, spp, img, args, torch, dev)
+        if world == 1 and not args.no_cpu_baseline:
+            threads = args.cpu_threads or len(os.sched_getaffinity(0))
+            out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt_static)
+    elif world > 1 and rank != 0:
+        frame(cam_static)  # rank 0's CRC frame needs every rank's tiles
     scene.close()
+    if rank == 0 and world == 1 and not args.no_extra:
+        out["other_configs"] = {}
+        for key in (2, 4, 5):
+            if key == args.config:
+                continue
+            try:
+                out["other_configs"][f"config{key}"] = other_config(R, S, key, torch, dev)
+            except Exception as exc:  # a side measurement: never lose the headline line over it
+                out["other_configs"][f"config{key}"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -27,6 +27,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RT_LIB") or os.path.join(PKG_DIR, "lib", "librtamd.so")
 
 RT_OK, RT_EINVAL, RT_ENOMEM, RT_EIO, RT_EDEVICE, RT_ECOMM = 0, -1, -2, -3, -4, -5
+RT_BACKEND_CPU, RT_BACKEND_HIP = 0, 1
 SENTINEL = 0xFFFFFFFF
 _STATUS_NAMES = {0: "RT_OK", -1: "RT_EINVAL", -2: "RT_ENOMEM", -3: "RT_EIO", -4: "RT_EDEVICE", -5: "RT_ECOMM"}
 
@@ -38,10 +39,10 @@ EXPORTED = [
     "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_render", "rt_render_counters", "rt_render_work", "rt_render_device",
     "rt_render_shadow", "rt_render_shadow_device", "rt_render_shadow_work",
     "rt_render_path", "rt_render_path_device", "rt_render_path_work",
-    "rt_bvh_prepare", "rt_bvh_device_sections", "rt_bvh_mark_built",
-    "rt_render_tiles_counters", "rt_tiles_for_rank",
+    "rt_bvh_prepare", "rt_bvh_device_sections", "rt_bvh_mark_built", "rt_bvh_replicas",
+    "rt_render_tiles_counters", "rt_render_tiles_work", "rt_tiles_for_rank",
     "rt_render_tiles_device", "rt_unpack_tiles_device", "rt_scene_stream", "rt_scene_sync",
-    "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_trace",
+    "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_refit", "rt_stage_trace",
     "rt_stage_intersect", "rt_stage_minmax", "rt_framebuffer_dump_ppm", "rt_hits_dump",
     "rt_config_set", "rt_last_error", "rt_device_count", "rt_version",
 ]
@@ -96,11 +97,12 @@ def lib() -> C.CDLL:
         "rt_scene_get_tris": [P, P],
         "rt_scene_set_device": [P, i32],
         "rt_camera_look_at": [P, P, P, dbl, u32, u32, cam],
-        "rt_bvh_build": [P, C.POINTER(dbl)],
+        "rt_bvh_build": [P, i32, u32, C.POINTER(dbl)],
+        "rt_bvh_replicas": [P, u32, P, C.POINTER(u32)],
         "rt_bvh_build_times": [P, C.POINTER(rt_build_times)],
         "rt_bvh_read": [P, P, P, P, P, P],
         "rt_bvh_read_wide": [P, P],
-        "rt_render": [P, cam, u32, u32, u32, P, P, C.POINTER(dbl)],
+        "rt_render": [P, cam, u32, u32, u32, u32, P, P, C.POINTER(dbl)],
         "rt_render_counters": [P, cam, u32, u32, u32, P],
         "rt_render_work": [P, cam, u32, u32, u32, P],
         "rt_render_shadow": [P, cam, P, C.c_float, u32, u32, u32, P, P, C.POINTER(dbl)],
@@ -114,6 +116,7 @@ def lib() -> C.CDLL:
         "rt_bvh_mark_built": [P],
         "rt_render_device": [P, cam, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_tiles_counters": [P, cam, u32, u32, u32, u32, u32, P],
+        "rt_render_tiles_work": [P, cam, u32, u32, u32, u32, u32, P],
         "rt_render_tiles_device": [P, cam, u32, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_unpack_tiles_device": [P, u32, u32, u32, u32, P, i32, P],
         "rt_scene_stream": [P, PP],
@@ -122,6 +125,7 @@ def lib() -> C.CDLL:
         "rt_stage_morton": [i32, P, u32, P, P, P, P],
         "rt_stage_sort": [i32, P, P, u32],
         "rt_stage_topology": [i32, P, u32, P, P, P],
+        "rt_stage_refit": [i32, P, P, P, u32, P],
         "rt_stage_trace": [i32, P, u32, P, cam, u32, u32, u32, P, P, P],
         "rt_stage_intersect": [i32, u32, P, P, P, P, P, P],
         "rt_stage_minmax": [i32, u32, P, P, P],

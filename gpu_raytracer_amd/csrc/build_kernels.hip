@@ -26,6 +26,8 @@
 #include "rt_device.h"
 #include "rt_launch.h"
 
+#include <mutex>
+
 #include <algorithm>
 
 namespace rt {
@@ -1025,21 +1027,31 @@ hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const floa
 }
 
 // K6t + K7w for the nodes whose range crosses a refit block (after k_topo_refit).
-static hipError_t launch_cross(const BuildBufs& b, uint32_t n, hipStream_t s) {
+// k_refit_cross<true>'s dynamic LDS above 64 KB needs the attribute once per
+// device (a process may drive several devices from several threads).
+static hipError_t ensure_cross_attr() {
+    static std::once_flag once[kMaxDevices];
+    static hipError_t err[kMaxDevices];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    std::call_once(once[dev], [dev] {
+        err[dev] = hipFuncSetAttribute((const void*)k_refit_cross<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       2 * kLdsTreeMaxBlocks * (int)sizeof(Aabb));
+    });
+    return err[dev];
+}
+
+static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     if (m <= 1) return hipGetLastError();
     if (m <= (uint32_t)kLdsTreeMaxBlocks) {
         uint32_t P = 1;
         while (P < m) P <<= 1;
         const size_t lds = 2ull * P * sizeof(Aabb);
-        static bool attr_set = false;
-        if (!attr_set) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_refit_cross<true>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               2 * kLdsTreeMaxBlocks * (int)sizeof(Aabb));
-            if (e != hipSuccess) return e;
-            attr_set = true;
-        }
+        const hipError_t e = ensure_cross_attr();
+        if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_refit_cross<true>, dim3(64), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
@@ -1052,11 +1064,31 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, hipStream_t s) {
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     hipLaunchKernelGGL(k_wide_cross, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr, cross_cap(m),
-                       b.nodes, n, b.wnodes, g_trace_config.wide_collapse);
+                       b.nodes, n, b.wnodes, wide_collapse);
     return hipGetLastError();
 }
 
+// K4 + K5 + K6-local + K7w-local (k_topo_refit) over sorted keys/vals in
+// keys[0]/vals[0]; expects the crossing-list counters zeroed (K0 does it).
+static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, hipStream_t s) {
+    if (!n) return hipSuccess;
+    const uint32_t m = cdiv(n, kRefitT);
+    hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo, b.parent,
+                       b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr, cross_cap(m),
+                       b.wnodes, wide_collapse);
+    return hipGetLastError();
+}
+
+hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
+    const TraceConfig cfg = config_snapshot();
+    hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
+    if (e != hipSuccess) return e;
+    if ((e = launch_topo_local(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
+    return n ? launch_cross(b, n, cfg.wide_collapse, s) : hipSuccess;
+}
+
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages) {
+    const TraceConfig cfg = config_snapshot();
     hipError_t e;
     auto rec = [&](int i) -> hipError_t {
         return (ev && (stages || i == 0 || i == 6)) ? hipEventRecord(ev->e[i], s) : hipSuccess;
@@ -1068,7 +1100,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
     if (!n) hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
-    const bool msb = n >= 2 && n <= kMsbMaxN && g_trace_config.sort_msb;
+    const bool msb = n >= 2 && n <= kMsbMaxN && cfg.sort_msb;
     if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
                                 b.zero + kZHist, counts[0], s, msb)) != hipSuccess)
         return e;
@@ -1079,15 +1111,9 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     else e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
     if (e != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;
-    if (n) {
-        const uint32_t m = cdiv(n, kRefitT);
-        hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
-                           b.parent, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.wnodes, g_trace_config.wide_collapse);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    if ((e = launch_topo_local(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
-    if (n && (e = launch_cross(b, n, s)) != hipSuccess) return e;
+    if (n && (e = launch_cross(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
     if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K4/K6 (records written with the boxes)
     return hipSuccess;

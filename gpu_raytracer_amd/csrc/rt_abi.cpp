@@ -1,18 +1,26 @@
 // rt_abi.cpp -- extern "C" boundary of librtamd.so (include/gpu_raytracer_amd.h).
 //
-// Host C++ around the gfx950 kernels: scene objects, device buffers kept
-// resident per scene, one HIP stream per scene, hipEvent timing, error
-// mapping (HIP -> RT_EDEVICE) and a thread-local error message.  There is no
-// CPU compute path here: without a gfx950 device every compute entry point
-// returns RT_EDEVICE.
+// Host C++ around the gfx950 kernels: scene objects holding one BVH replica
+// per device (the BVH is replicated, every device builds its
+// own bit-identical copy), one HIP stream per replica, hipEvent timing, the
+// in-library multi-GPU render (tiles dealt round-robin to the replicas, packed
+// slabs gathered to the root with RCCL over xGMI, unpacked there), error
+// mapping (HIP -> RT_EDEVICE, RCCL -> RT_ECOMM) and a thread-local error
+// message.  There is no CPU compute path here: without a gfx950 device every
+// compute entry point returns RT_EDEVICE.
 #include "../../include/gpu_raytracer_amd.h"
 #include "rt_device.h"
 #include "rt_launch.h"
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types and prototypes only: RCCL is dlopen'ed on first multi-GPU use
+
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -23,11 +31,12 @@ bool save_soup(const char* path, const float* tris, uint64_t n, std::string& err
 void soup_generate(uint32_t n, uint64_t seed, float* tris);
 }  // namespace rtio
 
-struct rt_scene {
-    std::vector<float> tris;  // host copy, n*9
-    uint32_t n = 0;
+namespace {
+
+// One device's copy of a scene's BVH plus that device's render scratch.
+struct Replica {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // the replica's own stream (builds, synchronous renders)
     rt::BuildBufs bufs;
     bool uploaded = false, built = false;
     rt::BuildEvents ev;
@@ -43,8 +52,41 @@ struct rt_scene {
     size_t order_cap = 0;
     rt::TileSched sched;
     uint32_t sched_key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the cost map
-    rt::PathBufs path;           // wavefront path-mode state (grown on demand)
+    rt::PathBufs path;                        // wavefront path-mode state (grown on demand)
     hipEvent_t r0 = nullptr, r1 = nullptr;
+    // multi-GPU render: this rank's packed slabs; the root's gathered slabs
+    void* d_slab = nullptr;
+    size_t slab_cap = 0;
+    void* d_slab_hits = nullptr;
+    size_t slab_hits_cap = 0;
+    void* d_recv = nullptr;
+    size_t recv_cap = 0;
+    void* d_recv_hits = nullptr;
+    size_t recv_hits_cap = 0;
+    // Ordering of device work issued on caller streams (the *_device entry
+    // points): every launch of this replica waits for the previous one when
+    // it runs on another stream, and build / load / free wait for the last
+    // one -- so a rebuild never overwrites, and a free never releases, buffers
+    // a trace on a caller stream is still reading, and the tile-order maps
+    // are written and read in launch order.
+    hipEvent_t last = nullptr;
+    hipStream_t last_stream = nullptr;  // stream `last` was recorded on (nullptr: none)
+};
+
+// RCCL communicators of one device list (rt_render(ngpus > 1)).
+struct Comms {
+    std::vector<int> devs;
+    std::vector<ncclComm_t> comms;
+};
+
+}  // namespace
+
+struct rt_scene {
+    std::vector<float> tris;  // host copy, n*9
+    uint32_t n = 0;
+    int device = 0;                                 // the primary replica's device
+    std::vector<std::unique_ptr<Replica>> reps;     // reps[0] = primary; rank r of a multi-GPU render = reps[r]
+    Comms comm;
 };
 
 namespace {
@@ -64,48 +106,210 @@ rt_status hip_fail(hipError_t e, const char* where) {
         hipError_t _e = (expr);                             \
         if (_e != hipSuccess) return hip_fail(_e, #expr);   \
     } while (0)
+#define RTR(expr)                  \
+    do {                           \
+        rt_status _s = (expr);     \
+        if (_s != RT_OK) return _s; \
+    } while (0)
+
+int visible_devices() {
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess) return 0;
+    return cnt;
+}
 
 rt_status ensure_device(int dev) {
-    int cnt = 0;
-    hipError_t e = hipGetDeviceCount(&cnt);
-    if (e != hipSuccess || cnt == 0)
-        return fail(RT_EDEVICE, "no HIP device available (librtamd has no CPU path)");
+    const int cnt = visible_devices();
+    if (cnt == 0) return fail(RT_EDEVICE, "no HIP device available (librtamd has no CPU path)");
     if (dev < 0 || dev >= cnt) return fail(RT_EINVAL, "device index out of range");
     HIPR(hipSetDevice(dev));
     return RT_OK;
 }
 
-rt_status ensure_stream(rt_scene* s) {
-    rt_status st = ensure_device(s->device);
-    if (st) return st;
-    if (!s->stream) {
-        HIPR(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-        // timing-only events: no system-scope fence (L2 writeback + invalidate)
-        // at each record, which would add ~4.7 us per event to the GPU
-        // timeline between the kernels being timed.  Every host read of
-        // results goes through a stream synchronize or a blocking copy.
-        const unsigned fl = rt::g_trace_config.event_fence ? hipEventDefault : hipEventDisableSystemFence;
-        for (auto& e : s->ev.e) HIPR(hipEventCreateWithFlags(&e, fl));
-        s->ev.valid = true;
-        HIPR(hipEventCreateWithFlags(&s->r0, fl));
-        HIPR(hipEventCreateWithFlags(&s->r1, fl));
-        HIPR(hipMalloc((void**)&s->d_work, 4096));  // kPoolCounters x 128 B
+// ---- RCCL, loaded on first use (a host that never renders on several GPUs
+// never maps it).  An RCCL already in the process (e.g. torch's) is reused.
+struct Rccl {
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGather) gather = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    std::string why;  // load failure
+};
+
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = RTLD_DEFAULT;
+        if (!dlsym(h, "ncclGather")) {
+            h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+            if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        }
+        if (!h) {
+            const char* e = dlerror();
+            r.why = std::string("cannot load librccl.so.1: ") + (e ? e : "?");
+            return;
+        }
+        r.init_all = reinterpret_cast<decltype(r.init_all)>(dlsym(h, "ncclCommInitAll"));
+        r.destroy = reinterpret_cast<decltype(r.destroy)>(dlsym(h, "ncclCommDestroy"));
+        r.group_start = reinterpret_cast<decltype(r.group_start)>(dlsym(h, "ncclGroupStart"));
+        r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
+        r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(h, "ncclGather"));
+        r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+        if (!r.init_all || !r.destroy || !r.group_start || !r.group_end || !r.gather || !r.error_string) {
+            r.init_all = nullptr;
+            r.why = "librccl.so.1 lacks ncclCommInitAll/ncclGather";
+        }
+    });
+    return r;
+}
+
+rt_status nccl_fail(ncclResult_t e, const char* where) {
+    const Rccl& R = rccl();
+    return fail(RT_ECOMM, std::string(where) + ": " + (R.error_string ? R.error_string(e) : "RCCL error"));
+}
+
+#define NCCLR(expr)                                           \
+    do {                                                      \
+        ncclResult_t _r = (expr);                             \
+        if (_r != ncclSuccess) return nccl_fail(_r, #expr);   \
+    } while (0)
+
+void free_comms(Comms& c) {
+    const Rccl& R = rccl();
+    for (ncclComm_t cm : c.comms)
+        if (cm && R.destroy) (void)R.destroy(cm);
+    c.comms.clear();
+    c.devs.clear();
+}
+
+// ---- replicas
+rt_status replica_init(Replica& r) {
+    RTR(ensure_device(r.device));
+    if (r.stream) return RT_OK;
+    HIPR(hipStreamCreateWithFlags(&r.stream, hipStreamNonBlocking));
+    // timing-only events: no system-scope fence (L2 writeback + invalidate)
+    // at each record, which would add ~4.7 us per event to the GPU timeline
+    // between the kernels being timed.  Every host read of results goes
+    // through a stream synchronize or a blocking copy.
+    const unsigned fl = rt::config_snapshot().event_fence ? hipEventDefault : hipEventDisableSystemFence;
+    for (auto& e : r.ev.e) HIPR(hipEventCreateWithFlags(&e, fl));
+    r.ev.valid = true;
+    HIPR(hipEventCreateWithFlags(&r.r0, fl));
+    HIPR(hipEventCreateWithFlags(&r.r1, fl));
+    HIPR(hipEventCreateWithFlags(&r.last, hipEventDisableTiming | hipEventDisableSystemFence));
+    HIPR(hipMalloc((void**)&r.d_work, 4096));  // kPoolCounters x 128 B
+    return RT_OK;
+}
+
+void replica_free(Replica& r) {
+    if (!r.stream) return;
+    (void)hipSetDevice(r.device);
+    if (r.last_stream) (void)hipEventSynchronize(r.last);  // device work on a caller stream
+    (void)hipStreamSynchronize(r.stream);
+    rt::free_build(r.bufs);
+    rt::free_path(r.path);
+    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.d_order, r.d_slab, r.d_slab_hits, r.d_recv,
+                    r.d_recv_hits})
+        if (p) (void)hipFree(p);
+    for (auto& e : r.ev.e) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(r.r0);
+    (void)hipEventDestroy(r.r1);
+    (void)hipEventDestroy(r.last);
+    (void)hipStreamDestroy(r.stream);
+    r.stream = nullptr;
+}
+
+// the primary replica (created on the scene's device on first use)
+rt_status primary(rt_scene* s, Replica** out) {
+    if (s->reps.empty()) {
+        std::unique_ptr<Replica> r(new (std::nothrow) Replica);
+        if (!r) return fail(RT_ENOMEM, "host allocation failed");
+        r->device = s->device;
+        s->reps.push_back(std::move(r));
+    }
+    Replica* r = s->reps[0].get();
+    RTR(replica_init(*r));
+    *out = r;
+    return RT_OK;
+}
+
+Replica* primary_built(const rt_scene* s) {
+    return (!s->reps.empty() && s->reps[0]->built) ? s->reps[0].get() : nullptr;
+}
+
+// Before device work on stream hs: order it after this replica's previous
+// device work when that ran on another stream.
+rt_status order_before(Replica& r, hipStream_t hs) {
+    if (r.last_stream && r.last_stream != hs) HIPR(hipStreamWaitEvent(hs, r.last, 0));
+    return RT_OK;
+}
+// After device work on a caller stream hs: remember it (see Replica::last).
+rt_status order_after(Replica& r, hipStream_t hs) {
+    if (hs == r.stream) {
+        r.last_stream = nullptr;  // the replica's own stream orders itself
+        return RT_OK;
+    }
+    HIPR(hipEventRecord(r.last, hs));
+    r.last_stream = hs;
+    return RT_OK;
+}
+// Before the replica's own stream rewrites or frees its buffers.
+rt_status join_caller_work(Replica& r) {
+    if (r.last_stream) {
+        HIPR(hipStreamWaitEvent(r.stream, r.last, 0));
+        r.last_stream = nullptr;
     }
     return RT_OK;
 }
 
-rt_status upload(rt_scene* s) {
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    if (s->uploaded) return RT_OK;
-    if (s->bufs.cap_n != s->n || !s->bufs.tris) {
-        hipError_t e = rt::alloc_build(s->bufs, s->n);
+rt_status upload(const rt_scene* s, Replica& r) {
+    RTR(replica_init(r));
+    if (r.uploaded) return RT_OK;
+    if (r.bufs.cap_n != s->n || !r.bufs.tris) {
+        hipError_t e = rt::alloc_build(r.bufs, s->n);
         if (e == hipErrorOutOfMemory) return fail(RT_ENOMEM, "device allocation failed");
         if (e != hipSuccess) return hip_fail(e, "alloc_build");
     }
-    if (s->n) HIPR(hipMemcpyAsync(s->bufs.tris, s->tris.data(), (size_t)s->n * 36, hipMemcpyHostToDevice, s->stream));
-    HIPR(hipStreamSynchronize(s->stream));
-    s->uploaded = true;
+    if (s->n) HIPR(hipMemcpyAsync(r.bufs.tris, s->tris.data(), (size_t)s->n * 36, hipMemcpyHostToDevice, r.stream));
+    HIPR(hipStreamSynchronize(r.stream));
+    r.uploaded = true;
+    return RT_OK;
+}
+
+// Build the BVH on every replica in `targets` concurrently (one stream each),
+// then wait for all; ms_out = the longest build.
+rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, double* ms_out) {
+    const bool stages = rt::config_snapshot().stage_events != 0;
+    for (Replica* r : targets) {
+        RTR(upload(s, *r));
+        HIPR(hipSetDevice(r->device));
+        RTR(join_caller_work(*r));
+        hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages);
+        if (e != hipSuccess) return hip_fail(e, "launch_build");
+    }
+    double worst = 0.0;
+    for (Replica* r : targets) {
+        HIPR(hipSetDevice(r->device));
+        HIPR(hipStreamSynchronize(r->stream));
+        float t[6] = {0, 0, 0, 0, 0, 0};
+        if (stages)
+            for (int i = 0; i < 6; ++i) HIPR(hipEventElapsedTime(&t[i], r->ev.e[i], r->ev.e[i + 1]));
+        r->times.bounds = t[0];
+        r->times.morton = t[1];
+        r->times.sort = t[2];
+        r->times.topology = t[3];
+        r->times.refit = t[4];
+        r->times.wide = t[5];
+        float tot = 0;
+        HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
+        r->times.total = tot;
+        r->built = true;
+        worst = std::max(worst, (double)tot);
+    }
+    if (ms_out) *ms_out = worst;
     return RT_OK;
 }
 
@@ -123,34 +327,38 @@ rt_status grow(void** p, size_t* cap, size_t need) {
 
 // Tile-order state for a frame of this shape (DESIGN.md "Tile order"): the
 // cost map of the previous frame with the same w, h, spp, rank, nranks
-// drives this frame's dispatch order (nullptr: row-major, no map).
-rt::TileSched* sched_for(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks) {
+// drives this frame's dispatch order.  A failed allocation is reported
+// (RT_ENOMEM / RT_EDEVICE), never silently replaced by row-major order.
+rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
+                    rt::TileSched** out) {
     const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     const uint32_t key[5] = {w, h, spp, rank, nranks};
-    const bool same = std::memcmp(key, s->sched_key, sizeof(key)) == 0;
+    const bool same = std::memcmp(key, r.sched_key, sizeof(key)) == 0;
     // [order][cost A][cost B] u32, [px A][px B] u16 x 256 per tile slot
     const size_t need = 3ull * nb * 4 + 2ull * nb * 512;
-    if (!same || s->order_cap < need) {
-        if (grow(&s->d_order, &s->order_cap, need)) return nullptr;
-        uint32_t* b = static_cast<uint32_t*>(s->d_order);
-        s->sched.order = b;
-        s->sched.cost_prev = b + nb;
-        s->sched.cost_cur = b + 2 * nb;
-        s->sched.px_prev = reinterpret_cast<uint16_t*>(b + 3 * nb);
-        s->sched.px_cur = s->sched.px_prev + (size_t)nb * 256;
-        s->sched.have_prev = false;
-        s->sched.fresh = true;
-        std::memcpy(s->sched_key, key, sizeof(key));
+    if (!same || r.order_cap < need) {
+        std::memset(r.sched_key, 0, sizeof(r.sched_key));  // invalid until the maps exist
+        RTR(grow(&r.d_order, &r.order_cap, need));
+        uint32_t* b = static_cast<uint32_t*>(r.d_order);
+        r.sched.order = b;
+        r.sched.cost_prev = b + nb;
+        r.sched.cost_cur = b + 2 * nb;
+        r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 3 * nb);
+        r.sched.px_cur = r.sched.px_prev + (size_t)nb * 256;
+        r.sched.have_prev = false;
+        r.sched.fresh = true;
+        std::memcpy(r.sched_key, key, sizeof(key));
     }
-    return &s->sched;
+    *out = &r.sched;
+    return RT_OK;
 }
 
 // after a launch that used sched_for: this frame's map becomes the previous one
-void sched_done(rt_scene* s) {
-    if (!rt::g_trace_config.tile_order) return;
-    std::swap(s->sched.cost_prev, s->sched.cost_cur);
-    std::swap(s->sched.px_prev, s->sched.px_cur);
-    s->sched.have_prev = true;
+void sched_done(Replica& r, const rt::TraceConfig& cfg) {
+    if (!cfg.tile_order) return;
+    std::swap(r.sched.cost_prev, r.sched.cost_cur);
+    std::swap(r.sched.px_prev, r.sched.px_cur);
+    r.sched.have_prev = true;
 }
 
 rt::CamF camf(const rt_camera* c) {
@@ -170,40 +378,55 @@ struct DevBuf {
     T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+rt_status check_frame(uint32_t w, uint32_t h, uint32_t spp) {
+    if (!w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
+    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
+    return RT_OK;
+}
+
+rt_status need_built(rt_scene* s, Replica** out) {
+    if (!primary_built(s)) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
+    return primary(s, out);
+}
+
+bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
+    const std::string k(key);
+    if (k == "trace.variant" && value >= 0 && value <= 2) c.variant = (uint32_t)value;
+    else if (k == "trace.stack_cap" && value >= 1 && value <= 14) c.stack_cap = (uint32_t)value;
+    else if (k == "trace.wg" && (value == 64 || value == 256)) c.wg = (uint32_t)value;
+    else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) c.wg_tiles = (uint32_t)value;
+    else if (k == "trace.tile_order" && (value == 0 || value == 1)) c.tile_order = (uint32_t)value;
+    else if (k == "trace.px_sort" && value >= 0 && value <= 2) c.px_sort = (uint32_t)value;
+    else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
+    else if (k == "build.sort" && (value == 0 || value == 1)) c.sort_msb = (uint32_t)value;
+    else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
+    else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;
+    else if (k == "timing.event_fence" && (value == 0 || value == 1)) c.event_fence = (uint32_t)value;
+    else if (k == "path.wavefront" && (value == 0 || value == 1)) c.path_wave = (uint32_t)value;
+    else if (k == "path.wg" && (value == 64 || value == 256)) c.path_wg = (uint32_t)value;
+    else if (k == "path.sort" && value >= 0 && value <= 4) c.path_sort = (uint32_t)value;
+    else if (k == "path.batch" && value >= 0 && value <= (1 << 28)) c.path_batch = (uint32_t)value;
+    else if (k == "render.emulate" && (value == 0 || value == 1)) c.render_emulate = (uint32_t)value;
+    else if (k == "render.rccl1" && (value == 0 || value == 1)) c.render_rccl1 = (uint32_t)value;
+    else return false;
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
-const char* rt_version(void) { return "gpu_raytracer_amd 0.1 (gfx950)"; }
+const char* rt_version(void) { return "gpu_raytracer_amd 0.2 (gfx950)"; }
 
 rt_status rt_config_set(const char* key, int64_t value) {
     if (!key) return fail(RT_EINVAL, "null key");
-    const std::string k(key);
-    if (k == "trace.variant" && value >= 0 && value <= 2) rt::g_trace_config.variant = (uint32_t)value;
-    else if (k == "trace.stack_cap" && value >= 1 && value <= 14) rt::g_trace_config.stack_cap = (uint32_t)value;
-    else if (k == "trace.wg" && (value == 64 || value == 256)) rt::g_trace_config.wg = (uint32_t)value;
-    else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) rt::g_trace_config.wg_tiles = (uint32_t)value;
-    else if (k == "trace.tile_order" && (value == 0 || value == 1)) rt::g_trace_config.tile_order = (uint32_t)value;
-    else if (k == "trace.px_sort" && value >= 0 && value <= 2) rt::g_trace_config.px_sort = (uint32_t)value;
-    else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) rt::g_trace_config.blocks = (uint32_t)value;
-    else if (k == "build.sort" && (value == 0 || value == 1)) rt::g_trace_config.sort_msb = (uint32_t)value;
-    else if (k == "build.wide_collapse" && (value == 0 || value == 1)) rt::g_trace_config.wide_collapse = (uint32_t)value;
-    else if (k == "build.stage_events" && (value == 0 || value == 1)) rt::g_trace_config.stage_events = (uint32_t)value;
-    else if (k == "timing.event_fence" && (value == 0 || value == 1)) rt::g_trace_config.event_fence = (uint32_t)value;
-    else if (k == "path.wavefront" && (value == 0 || value == 1)) rt::g_trace_config.path_wave = (uint32_t)value;
-    else if (k == "path.wg" && (value == 64 || value == 256)) rt::g_trace_config.path_wg = (uint32_t)value;
-    else if (k == "path.sort" && value >= 0 && value <= 4) rt::g_trace_config.path_sort = (uint32_t)value;
-    else if (k == "path.batch" && value >= 0 && value <= (1 << 28)) rt::g_trace_config.path_batch = (uint32_t)value;
-    else return fail(RT_EINVAL, "unknown config key or value out of range: " + k);
+    if (!rt::config_apply(apply_config, key, value))
+        return fail(RT_EINVAL, std::string("unknown config key or value out of range: ") + key);
     return RT_OK;
 }
 
-int rt_device_count(void) {
-    int c = 0;
-    if (hipGetDeviceCount(&c) != hipSuccess) return 0;
-    return c;
-}
+int rt_device_count(void) { return visible_devices(); }
 
 // ------------------------------------------------------------------ scenes
 rt_status rt_scene_from_soup(const float* tris, uint32_t n, rt_scene** out) {
@@ -274,44 +497,35 @@ rt_status rt_scene_get_tris(const rt_scene* s, float* out) {
 
 rt_status rt_scene_set_device(rt_scene* s, int device) {
     if (!s) return fail(RT_EINVAL, "null argument");
-    if (s->stream) return fail(RT_EINVAL, "device must be set before the first build");
+    if (!s->reps.empty()) return fail(RT_EINVAL, "device must be set before the first build");
+    if (device < 0) return fail(RT_EINVAL, "device index out of range");
     s->device = device;
     return RT_OK;
 }
 
 void rt_scene_free(rt_scene* s) {
     if (!s) return;
-    if (s->stream) {
-        (void)hipSetDevice(s->device);
-        (void)hipStreamSynchronize(s->stream);
-        rt::free_build(s->bufs);
-        rt::free_path(s->path);
-        if (s->d_hits) (void)hipFree(s->d_hits);
-        if (s->d_rgba) (void)hipFree(s->d_rgba);
-        if (s->d_ctr) (void)hipFree(s->d_ctr);
-        if (s->d_work) (void)hipFree(s->d_work);
-        if (s->d_order) (void)hipFree(s->d_order);
-        for (auto& e : s->ev.e) (void)hipEventDestroy(e);
-        (void)hipEventDestroy(s->r0);
-        (void)hipEventDestroy(s->r1);
-        (void)hipStreamDestroy(s->stream);
-    }
+    for (auto& r : s->reps) replica_free(*r);
+    free_comms(s->comm);
     delete s;
 }
 
 rt_status rt_scene_stream(rt_scene* s, void** stream_out) {
     if (!s || !stream_out) return fail(RT_EINVAL, "null argument");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    *stream_out = (void*)s->stream;
+    Replica* r = nullptr;
+    RTR(primary(s, &r));
+    *stream_out = (void*)r->stream;
     return RT_OK;
 }
 
 rt_status rt_scene_sync(rt_scene* s) {
     if (!s) return fail(RT_EINVAL, "null argument");
-    if (!s->stream) return RT_OK;
-    HIPR(hipSetDevice(s->device));
-    HIPR(hipStreamSynchronize(s->stream));
+    for (auto& r : s->reps) {
+        if (!r->stream) continue;
+        HIPR(hipSetDevice(r->device));
+        if (r->last_stream) HIPR(hipEventSynchronize(r->last));
+        HIPR(hipStreamSynchronize(r->stream));
+    }
     return RT_OK;
 }
 
@@ -348,59 +562,83 @@ rt_status rt_camera_look_at(const double eye[3], const double at[3], const doubl
 }
 
 // ------------------------------------------------------------------ build
-rt_status rt_bvh_build(rt_scene* s, double* ms_out) {
+rt_status rt_bvh_build(rt_scene* s, int backend, uint32_t device_mask, double* ms_out) {
     if (!s) return fail(RT_EINVAL, "null scene");
-    rt_status st = upload(s);
-    if (st) return st;
-    const bool stages = rt::g_trace_config.stage_events != 0;
-    hipError_t e = rt::launch_build(s->bufs, s->n, s->stream, &s->ev, stages);
-    if (e != hipSuccess) return hip_fail(e, "launch_build");
-    HIPR(hipStreamSynchronize(s->stream));
-    float t[6] = {0, 0, 0, 0, 0, 0};
-    if (stages)
-        for (int i = 0; i < 6; ++i) HIPR(hipEventElapsedTime(&t[i], s->ev.e[i], s->ev.e[i + 1]));
-    s->times.bounds = t[0];
-    s->times.morton = t[1];
-    s->times.sort = t[2];
-    s->times.topology = t[3];
-    s->times.refit = t[4];
-    s->times.wide = t[5];
-    float tot = 0;
-    HIPR(hipEventElapsedTime(&tot, s->ev.e[0], s->ev.e[6]));
-    s->times.total = tot;
-    if (ms_out) *ms_out = tot;
-    s->built = true;
-    return RT_OK;
+    if (backend == RT_BACKEND_CPU)
+        return fail(RT_EINVAL, "librtamd has no CPU backend (the CPU oracle under oracle/ is test infrastructure)");
+    if (backend != RT_BACKEND_HIP) return fail(RT_EINVAL, "unknown backend");
+    const int cnt = visible_devices();
+    if (cnt == 0) return fail(RT_EDEVICE, "no HIP device available (librtamd has no CPU path)");
+    if (cnt < 32 && (device_mask >> cnt)) return fail(RT_EDEVICE, "device_mask names a device that is not visible");
+    std::vector<Replica*> targets;
+    if (!device_mask) {
+        Replica* r = nullptr;
+        RTR(primary(s, &r));
+        targets.push_back(r);
+    } else {
+        for (int d = 0; d < 32; ++d) {
+            if (!((device_mask >> d) & 1u)) continue;
+            if (s->reps.empty()) s->device = d;  // the lowest device of the first build is the primary
+            Replica* found = nullptr;
+            for (auto& r : s->reps)
+                if (r->device == d) { found = r.get(); break; }
+            if (!found) {
+                std::unique_ptr<Replica> r(new (std::nothrow) Replica);
+                if (!r) return fail(RT_ENOMEM, "host allocation failed");
+                r->device = d;
+                found = r.get();
+                s->reps.push_back(std::move(r));
+            }
+            targets.push_back(found);
+        }
+    }
+    return build_replicas(s, targets, ms_out);
 }
 
 rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out) {
     if (!s || !out) return fail(RT_EINVAL, "null argument");
-    if (!s->built) return fail(RT_EINVAL, "scene not built");
-    *out = s->times;
+    const Replica* r = primary_built(s);
+    if (!r) return fail(RT_EINVAL, "scene not built");
+    *out = r->times;
     return RT_OK;
 }
 
 rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* keys, uint32_t* vals, uint32_t* parent,
                       float* bounds9) {
     if (!s) return fail(RT_EINVAL, "null scene");
-    if (!s->built) return fail(RT_EINVAL, "scene not built");
-    HIPR(hipSetDevice(s->device));
-    HIPR(hipStreamSynchronize(s->stream));
+    Replica* r = primary_built(s);
+    if (!r) return fail(RT_EINVAL, "scene not built");
+    HIPR(hipSetDevice(r->device));
+    if (r->last_stream) HIPR(hipEventSynchronize(r->last));
+    HIPR(hipStreamSynchronize(r->stream));
     const size_t n = s->n, tot = n ? 2 * n - 1 : 0;
-    if (nodes && tot) HIPR(hipMemcpy(nodes, s->bufs.nodes, tot * 32, hipMemcpyDeviceToHost));
-    if (keys && n) HIPR(hipMemcpy(keys, s->bufs.keys[0], n * 4, hipMemcpyDeviceToHost));
-    if (vals && n) HIPR(hipMemcpy(vals, s->bufs.vals[0], n * 4, hipMemcpyDeviceToHost));
-    if (parent && tot) HIPR(hipMemcpy(parent, s->bufs.parent, tot * 4, hipMemcpyDeviceToHost));
-    if (bounds9) HIPR(hipMemcpy(bounds9, s->bufs.params, 9 * 4, hipMemcpyDeviceToHost));
+    if (nodes && tot) HIPR(hipMemcpy(nodes, r->bufs.nodes, tot * 32, hipMemcpyDeviceToHost));
+    if (keys && n) HIPR(hipMemcpy(keys, r->bufs.keys[0], n * 4, hipMemcpyDeviceToHost));
+    if (vals && n) HIPR(hipMemcpy(vals, r->bufs.vals[0], n * 4, hipMemcpyDeviceToHost));
+    if (parent && tot) HIPR(hipMemcpy(parent, r->bufs.parent, tot * 4, hipMemcpyDeviceToHost));
+    if (bounds9) HIPR(hipMemcpy(bounds9, r->bufs.params, 9 * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
 rt_status rt_bvh_read_wide(const rt_scene* s, void* records) {
     if (!s || !records) return fail(RT_EINVAL, "null argument");
-    if (!s->built) return fail(RT_EINVAL, "scene not built");
-    HIPR(hipSetDevice(s->device));
-    HIPR(hipStreamSynchronize(s->stream));
-    if (s->n >= 2) HIPR(hipMemcpy(records, s->bufs.wnodes, (size_t)(s->n - 1) * 64, hipMemcpyDeviceToHost));
+    Replica* r = primary_built(s);
+    if (!r) return fail(RT_EINVAL, "scene not built");
+    HIPR(hipSetDevice(r->device));
+    HIPR(hipStreamSynchronize(r->stream));
+    if (s->n >= 2) HIPR(hipMemcpy(records, r->bufs.wnodes, (size_t)(s->n - 1) * 64, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_bvh_replicas(const rt_scene* s, uint32_t max, int* devices, uint32_t* count_out) {
+    if (!s || !count_out || (max && !devices)) return fail(RT_EINVAL, "null argument");
+    uint32_t c = 0;
+    for (auto& r : s->reps) {
+        if (!r->built) continue;
+        if (c < max) devices[c] = r->device;
+        ++c;
+    }
+    *count_out = c;
     return RT_OK;
 }
 
@@ -410,7 +648,8 @@ rt_status rt_bvh_read_wide(const rt_scene* s, void* records) {
 // rt_bvh_read use, in order: BuildParams (64 B), sorted keys and vals (n x 4),
 // nodes ((2n-1) x 32), parent ((2n-1) x 4), tri_s (n x 48), wide records
 // ((n-1) x 64).  The tag changes whenever one of those layouts does.
-extern "C++" {
+}  // extern "C"
+
 namespace {
 const char kBvhMagic[8] = {'R', 'T', 'B', 'V', 'H', '1', 0, 0};
 constexpr uint32_t kBvhVersion = 1;
@@ -431,32 +670,41 @@ struct BvhSection {
     size_t bytes;
 };
 
-std::vector<BvhSection> bvh_sections(const rt_scene* s) {
+std::vector<BvhSection> bvh_sections(const rt_scene* s, const Replica& r) {
     const size_t n = s->n, tot = n ? 2 * n - 1 : 0;
     static_assert(sizeof(rt::BuildParams) == 64, "RTBVH1 stores a 64-B BuildParams");
-    return {{s->bufs.params, sizeof(rt::BuildParams)},
-            {s->bufs.keys[0], n * 4},
-            {s->bufs.vals[0], n * 4},
-            {s->bufs.nodes, tot * 32},
-            {s->bufs.parent, tot * 4},
-            {s->bufs.tri_s, n * 48},
-            {s->bufs.wnodes, n >= 2 ? (n - 1) * 64 : 0}};
+    return {{r.bufs.params, sizeof(rt::BuildParams)},
+            {r.bufs.keys[0], n * 4},
+            {r.bufs.vals[0], n * 4},
+            {r.bufs.nodes, tot * 32},
+            {r.bufs.parent, tot * 4},
+            {r.bufs.tri_s, n * 48},
+            {r.bufs.wnodes, n >= 2 ? (n - 1) * 64 : 0}};
 }
+
+struct File {
+    FILE* f = nullptr;
+    ~File() {
+        if (f) std::fclose(f);
+    }
+};
 }  // namespace
-}  // extern "C++"
+
+extern "C" {
 
 rt_status rt_bvh_save(const rt_scene* s, const char* path) {
     if (!s || !path) return fail(RT_EINVAL, "null argument");
-    if (!s->built) return fail(RT_EINVAL, "scene not built");
-    HIPR(hipSetDevice(s->device));
-    HIPR(hipStreamSynchronize(s->stream));
+    Replica* r = primary_built(s);
+    if (!r) return fail(RT_EINVAL, "scene not built");
+    HIPR(hipSetDevice(r->device));
+    HIPR(hipStreamSynchronize(r->stream));
     FILE* f = std::fopen(path, "wb");
     if (!f) return fail(RT_EIO, std::string("cannot create ") + path);
     const uint32_t hv[2] = {kBvhVersion, s->n};
     const uint64_t hh[2] = {fnv1a(s->tris.data(), s->tris.size() * sizeof(float)), kBvhLayout};
     bool ok = std::fwrite(kBvhMagic, 1, 8, f) == 8 && std::fwrite(hv, 4, 2, f) == 2 && std::fwrite(hh, 8, 2, f) == 2;
     std::vector<unsigned char> host;
-    for (const BvhSection& sec : bvh_sections(s)) {
+    for (const BvhSection& sec : bvh_sections(s, *r)) {
         if (!ok || !sec.bytes) continue;
         host.resize(sec.bytes);
         if (hipMemcpy(host.data(), sec.dev, sec.bytes, hipMemcpyDeviceToHost) != hipSuccess) {
@@ -471,48 +719,40 @@ rt_status rt_bvh_save(const rt_scene* s, const char* path) {
 
 rt_status rt_bvh_load(rt_scene* s, const char* path) {
     if (!s || !path) return fail(RT_EINVAL, "null argument");
-    FILE* f = std::fopen(path, "rb");
-    if (!f) return fail(RT_EIO, std::string("cannot open ") + path);
+    File f;
+    f.f = std::fopen(path, "rb");
+    if (!f.f) return fail(RT_EIO, std::string("cannot open ") + path);
     char magic[8];
     uint32_t hv[2] = {0, 0};
     uint64_t hh[2] = {0, 0};
-    const bool hdr = std::fread(magic, 1, 8, f) == 8 && std::fread(hv, 4, 2, f) == 2 && std::fread(hh, 8, 2, f) == 2;
-    if (!hdr || std::memcmp(magic, kBvhMagic, 8) != 0) {
-        std::fclose(f);
-        return fail(RT_EIO, std::string(path) + ": not an RTBVH1 file");
-    }
-    if (hv[0] != kBvhVersion || hh[1] != kBvhLayout) {
-        std::fclose(f);
+    const bool hdr =
+        std::fread(magic, 1, 8, f.f) == 8 && std::fread(hv, 4, 2, f.f) == 2 && std::fread(hh, 8, 2, f.f) == 2;
+    if (!hdr || std::memcmp(magic, kBvhMagic, 8) != 0) return fail(RT_EIO, std::string(path) + ": not an RTBVH1 file");
+    if (hv[0] != kBvhVersion || hh[1] != kBvhLayout)
         return fail(RT_EIO, std::string(path) + ": BVH cache from another library layout");
-    }
-    if (hv[1] != s->n || hh[0] != fnv1a(s->tris.data(), s->tris.size() * sizeof(float))) {
-        std::fclose(f);
+    if (hv[1] != s->n || hh[0] != fnv1a(s->tris.data(), s->tris.size() * sizeof(float)))
         return fail(RT_EINVAL, std::string(path) + ": BVH cache was built for different triangles");
-    }
-    rt_status st = upload(s);
-    if (st) {
-        std::fclose(f);
-        return st;
-    }
+    Replica* r = nullptr;
+    RTR(primary(s, &r));
+    RTR(upload(s, *r));
+    HIPR(hipSetDevice(r->device));
+    RTR(join_caller_work(*r));
+    HIPR(hipStreamSynchronize(r->stream));
+    // from here on the device buffers are being overwritten: any failure
+    // leaves the scene unbuilt (and every other replica is now stale)
+    r->built = false;
+    for (size_t i = 1; i < s->reps.size(); ++i) s->reps[i]->built = false;
     std::vector<unsigned char> host;
-    for (const BvhSection& sec : bvh_sections(s)) {
+    for (const BvhSection& sec : bvh_sections(s, *r)) {
         if (!sec.bytes) continue;
         host.resize(sec.bytes);
-        if (std::fread(host.data(), 1, sec.bytes, f) != sec.bytes) {
-            std::fclose(f);
-            s->built = false;
+        if (std::fread(host.data(), 1, sec.bytes, f.f) != sec.bytes)
             return fail(RT_EIO, std::string(path) + ": truncated BVH cache");
-        }
         HIPR(hipMemcpy(sec.dev, host.data(), sec.bytes, hipMemcpyHostToDevice));
     }
-    const bool extra = std::fgetc(f) != EOF;
-    std::fclose(f);
-    if (extra) {
-        s->built = false;
-        return fail(RT_EIO, std::string(path) + ": trailing bytes in BVH cache");
-    }
-    s->times = rt_build_times{};
-    s->built = true;
+    if (std::fgetc(f.f) != EOF) return fail(RT_EIO, std::string(path) + ": trailing bytes in BVH cache");
+    r->times = rt_build_times{};
+    r->built = true;
     return RT_OK;
 }
 
@@ -520,13 +760,16 @@ rt_status rt_bvh_load(rt_scene* s, const char* path) {
 // broadcasts"): the same sections as the RTBVH1 file, as device pointers.
 rt_status rt_bvh_prepare(rt_scene* s) {
     if (!s) return fail(RT_EINVAL, "null scene");
-    return upload(s);
+    Replica* r = nullptr;
+    RTR(primary(s, &r));
+    return upload(s, *r);
 }
 
 rt_status rt_bvh_device_sections(rt_scene* s, uint32_t max, void** ptrs, uint64_t* bytes, uint32_t* count_out) {
     if (!s || !count_out || (max && (!ptrs || !bytes))) return fail(RT_EINVAL, "null argument");
-    if (!s->uploaded) return fail(RT_EINVAL, "scene not prepared (rt_bvh_prepare or rt_bvh_build)");
-    const std::vector<BvhSection> secs = bvh_sections(s);
+    if (s->reps.empty() || !s->reps[0]->uploaded)
+        return fail(RT_EINVAL, "scene not prepared (rt_bvh_prepare or rt_bvh_build)");
+    const std::vector<BvhSection> secs = bvh_sections(s, *s->reps[0]);
     *count_out = (uint32_t)secs.size();
     for (uint32_t i = 0; i < max && i < secs.size(); ++i) {
         ptrs[i] = secs[i].dev;
@@ -537,203 +780,383 @@ rt_status rt_bvh_device_sections(rt_scene* s, uint32_t max, void** ptrs, uint64_
 
 rt_status rt_bvh_mark_built(rt_scene* s) {
     if (!s) return fail(RT_EINVAL, "null scene");
-    if (!s->uploaded) return fail(RT_EINVAL, "scene not prepared (rt_bvh_prepare)");
-    HIPR(hipSetDevice(s->device));
+    if (s->reps.empty() || !s->reps[0]->uploaded) return fail(RT_EINVAL, "scene not prepared (rt_bvh_prepare)");
+    Replica* r = s->reps[0].get();
+    HIPR(hipSetDevice(r->device));
     HIPR(hipDeviceSynchronize());  // the caller's writes (any stream) land before the first render
-    s->times = rt_build_times{};
-    s->built = true;
+    r->times = rt_build_times{};
+    r->built = true;
     return RT_OK;
 }
 
 // ------------------------------------------------------------------ render
-rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits_out,
-                    uint8_t* rgba_out, double* ms_out) {
-    if (!s || !cam || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    const size_t nh = (size_t)w * h * spp;
-    if (hits_out && (st = grow(&s->d_hits, &s->hits_cap, nh * 16))) return st;
-    if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
-    HIPR(hipEventRecord(s->r0, s->stream));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
-                                    false, hits_out ? s->d_hits : nullptr, s->d_rgba, nullptr, false, s->d_work,
-                                    sched_for(s, w, h, spp, 0, 1), s->stream);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace");
-    sched_done(s);
-    HIPR(hipEventRecord(s->r1, s->stream));
-    HIPR(hipStreamSynchronize(s->stream));
-    float ms = 0;
-    HIPR(hipEventElapsedTime(&ms, s->r0, s->r1));
-    if (ms_out) *ms_out = ms;
-    if (hits_out) HIPR(hipMemcpy(hits_out, s->d_hits, nh * 16, hipMemcpyDeviceToHost));
-    if (rgba_out) HIPR(hipMemcpy(rgba_out, s->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
+}  // extern "C"
+
+namespace {
+
+// Replicas 0..P-1 for a P-rank render: one per device, or
+// all on the scene's device under render.emulate; the missing ones are
+// created and built (concurrently) -- the replicated build of the scheme.
+rt_status ensure_replicas(rt_scene* s, uint32_t P, bool emulate) {
+    Replica* r0 = nullptr;
+    RTR(primary(s, &r0));
+    const int cnt = visible_devices();
+    std::vector<Replica*> todo;
+    if (!r0->built) todo.push_back(r0);
+    while (s->reps.size() < P) {
+        int dev = r0->device;
+        if (!emulate) {
+            dev = -1;
+            for (int d = 0; d < cnt && dev < 0; ++d) {
+                bool used = false;
+                for (auto& r : s->reps) used = used || r->device == d;
+                if (!used) dev = d;
+            }
+            if (dev < 0) return fail(RT_EDEVICE, "not enough devices for the requested ngpus");
+        }
+        std::unique_ptr<Replica> r(new (std::nothrow) Replica);
+        if (!r) return fail(RT_ENOMEM, "host allocation failed");
+        r->device = dev;
+        todo.push_back(r.get());
+        s->reps.push_back(std::move(r));
+    }
+    for (uint32_t i = 1; i < P; ++i) {
+        const int d = s->reps[i]->device;
+        bool clash = emulate ? d != r0->device : false;
+        for (uint32_t j = 0; j < i && !emulate; ++j) clash = clash || s->reps[j]->device == d;
+        if (clash)
+            return fail(RT_EINVAL, emulate ? "render.emulate needs every replica on the scene's device"
+                                           : "two replicas share a device; multi-GPU render needs distinct devices");
+        if (!s->reps[i]->built && std::find(todo.begin(), todo.end(), s->reps[i].get()) == todo.end())
+            todo.push_back(s->reps[i].get());
+    }
+    return todo.empty() ? RT_OK : build_replicas(s, todo, nullptr);
+}
+
+rt_status comms_for(rt_scene* s, const std::vector<int>& devs, std::vector<ncclComm_t>** out) {
+    const Rccl& R = rccl();
+    if (!R.init_all) return fail(RT_ECOMM, R.why);
+    if (s->comm.devs != devs) {
+        free_comms(s->comm);
+        s->comm.comms.assign(devs.size(), nullptr);
+        NCCLR(R.init_all(s->comm.comms.data(), (int)devs.size(), devs.data()));
+        s->comm.devs = devs;
+    }
+    *out = &s->comm.comms;
     return RT_OK;
 }
 
-rt_status rt_render_shadow_device(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
-                                  uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba, void* stream,
-                                  double* ms_out) {
-    if (!s || !cam || !light || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
-    if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace_shadow(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
-                                           w, h, spp, light, ambient, d_hits, d_rgba, nullptr, hs);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace_shadow");
+// rt_render with the tile scheme of SURVEY.md §8(e) inside the library: rank
+// r traces tiles t = r mod P on replica r into a packed slab, RCCL gathers the
+// slabs to rank 0 (one ncclGather per rank in one group, each on its
+// replica's stream), and rank 0 unpacks them into the frame.  ms_out spans
+// first trace launch .. unpack end on the root's stream (every rank's trace
+// and the gather lie inside it).
+rt_status render_tiled(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t P,
+                       rt_hit* hits_out, uint8_t* rgba_out, double* ms_out, const rt::TraceConfig& cfg) {
+    const bool emulate = cfg.render_emulate != 0;
+    RTR(ensure_replicas(s, P, emulate));
+    Replica& root = *s->reps[0];
+    const uint32_t tmax = std::max(rt::tiles_for_rank(w, h, 0, P), 1u);  // rank 0 holds the most tiles
+    const size_t slab = (size_t)tmax * 1024, slab_hits = (size_t)tmax * 256 * spp * 16;
+    std::vector<int> devs;
+    for (uint32_t r = 0; r < P; ++r) {
+        Replica& R = *s->reps[r];
+        devs.push_back(R.device);
+        HIPR(hipSetDevice(R.device));
+        RTR(grow(&R.d_slab, &R.slab_cap, slab));
+        if (hits_out) RTR(grow(&R.d_slab_hits, &R.slab_hits_cap, slab_hits));
+    }
+    HIPR(hipSetDevice(root.device));
+    RTR(grow(&root.d_recv, &root.recv_cap, slab * P));
+    if (hits_out) RTR(grow(&root.d_recv_hits, &root.recv_hits_cap, slab_hits * P));
+    RTR(grow(&root.d_rgba, &root.rgba_cap, (size_t)w * h * 4));
+    if (hits_out) RTR(grow(&root.d_hits, &root.hits_cap, (size_t)w * h * spp * 16));
+    std::vector<ncclComm_t>* comms = nullptr;
+    if (!emulate) RTR(comms_for(s, devs, &comms));
+
+    HIPR(hipEventRecord(root.r0, root.stream));
+    for (uint32_t r = 0; r < P; ++r) {
+        Replica& R = *s->reps[r];
+        HIPR(hipSetDevice(R.device));
+        RTR(join_caller_work(R));
+        if (r) HIPR(hipStreamWaitEvent(R.stream, root.r0, 0));
+        rt::TileSched* sched = nullptr;
+        RTR(sched_for(R, w, h, spp, r, P, &sched));
+        hipError_t e = rt::launch_trace(R.bufs.nodes, R.bufs.wnodes, R.bufs.tri_s, s->n, camf(cam), w, h, spp, r, P,
+                                        true, hits_out ? R.d_slab_hits : nullptr, R.d_slab, nullptr, false, R.d_work,
+                                        sched, R.stream);
+        if (e != hipSuccess) return hip_fail(e, "launch_trace");
+        sched_done(R, cfg);
+    }
+    if (!emulate) {
+        const Rccl& RC = rccl();
+        NCCLR(RC.group_start());
+        for (uint32_t r = 0; r < P; ++r) {
+            Replica& R = *s->reps[r];
+            HIPR(hipSetDevice(R.device));
+            NCCLR(RC.gather(R.d_slab, r == 0 ? root.d_recv : nullptr, slab, ncclUint8, 0, (*comms)[r], R.stream));
+            if (hits_out)
+                NCCLR(RC.gather(R.d_slab_hits, r == 0 ? root.d_recv_hits : nullptr, slab_hits, ncclUint8, 0,
+                                (*comms)[r], R.stream));
+        }
+        NCCLR(RC.group_end());
+    } else {
+        // one device plays every rank: the gather is a device copy per rank
+        HIPR(hipSetDevice(root.device));
+        for (uint32_t r = 0; r < P; ++r) {
+            Replica& R = *s->reps[r];
+            if (r) {
+                HIPR(hipEventRecord(R.r1, R.stream));
+                HIPR(hipStreamWaitEvent(root.stream, R.r1, 0));
+            }
+            HIPR(hipMemcpyAsync((char*)root.d_recv + r * slab, R.d_slab, slab, hipMemcpyDeviceToDevice, root.stream));
+            if (hits_out)
+                HIPR(hipMemcpyAsync((char*)root.d_recv_hits + r * slab_hits, R.d_slab_hits, slab_hits,
+                                    hipMemcpyDeviceToDevice, root.stream));
+        }
+    }
+    HIPR(hipSetDevice(root.device));
+    hipError_t e = rt::launch_unpack(root.d_recv, tmax, w, h, P, root.d_rgba, root.stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_unpack");
+    if (hits_out && (e = rt::launch_unpack_hits(root.d_recv_hits, tmax, w, h, spp, P, root.d_hits, root.stream)) !=
+                        hipSuccess)
+        return hip_fail(e, "launch_unpack_hits");
+    HIPR(hipEventRecord(root.r1, root.stream));
+    for (uint32_t r = 0; r < P; ++r) {
+        HIPR(hipSetDevice(s->reps[r]->device));
+        HIPR(hipStreamSynchronize(s->reps[r]->stream));
+    }
+    HIPR(hipSetDevice(root.device));
+    float ms = 0;
+    HIPR(hipEventElapsedTime(&ms, root.r0, root.r1));
+    if (ms_out) *ms_out = ms;
+    if (hits_out) HIPR(hipMemcpy(hits_out, root.d_hits, (size_t)w * h * spp * 16, hipMemcpyDeviceToHost));
+    if (rgba_out) HIPR(hipMemcpy(rgba_out, root.d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
+                    rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
+    if (!s || !cam) return fail(RT_EINVAL, "bad render arguments");
+    RTR(check_frame(w, h, spp));
+    if (ngpus == 0 || ngpus > 64) return fail(RT_EINVAL, "ngpus must be 1..64");
+    const rt::TraceConfig cfg = rt::config_snapshot();
+    const int cnt = visible_devices();
+    if (cnt == 0) return fail(RT_EDEVICE, "no HIP device available (librtamd has no CPU path)");
+    if ((int)ngpus > cnt && !cfg.render_emulate)
+        return fail(RT_EDEVICE, "ngpus exceeds the " + std::to_string(cnt) + " visible device(s)");
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    if (ngpus > 1 || cfg.render_rccl1) return render_tiled(s, cam, w, h, spp, ngpus, hits_out, rgba_out, ms_out, cfg);
+    const size_t nh = (size_t)w * h * spp;
+    if (hits_out) RTR(grow(&r->d_hits, &r->hits_cap, nh * 16));
+    RTR(grow(&r->d_rgba, &r->rgba_cap, (size_t)w * h * 4));
+    RTR(join_caller_work(*r));
+    rt::TileSched* sched = nullptr;
+    RTR(sched_for(*r, w, h, spp, 0, 1, &sched));
+    HIPR(hipEventRecord(r->r0, r->stream));
+    hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
+                                    false, hits_out ? r->d_hits : nullptr, r->d_rgba, nullptr, false, r->d_work, sched,
+                                    r->stream);
+    if (e != hipSuccess) return hip_fail(e, "launch_trace");
+    sched_done(*r, cfg);
+    HIPR(hipEventRecord(r->r1, r->stream));
+    HIPR(hipStreamSynchronize(r->stream));
+    float ms = 0;
+    HIPR(hipEventElapsedTime(&ms, r->r0, r->r1));
+    if (ms_out) *ms_out = ms;
+    if (hits_out) HIPR(hipMemcpy(hits_out, r->d_hits, nh * 16, hipMemcpyDeviceToHost));
+    if (rgba_out) HIPR(hipMemcpy(rgba_out, r->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+// Shared shape of the *_device entry points: launch `fn` on the caller's
+// stream (or the replica's), ordered after this replica's previous device
+// work, optionally bracketed by events and waited for.
+}  // extern "C"
+
+namespace {
+template <class F>
+rt_status device_launch(Replica& r, void* stream, double* ms_out, const char* what, F&& fn) {
+    hipStream_t hs = stream ? (hipStream_t)stream : r.stream;
+    HIPR(hipSetDevice(r.device));
+    RTR(order_before(r, hs));
+    if (ms_out) HIPR(hipEventRecord(r.r0, hs));
+    const hipError_t e = fn(hs);
+    if (e != hipSuccess) return hip_fail(e, what);
+    if (ms_out) HIPR(hipEventRecord(r.r1, hs));
+    RTR(order_after(r, hs));
     if (ms_out) {
-        HIPR(hipEventRecord(s->r1, hs));
-        HIPR(hipEventSynchronize(s->r1));
+        HIPR(hipEventSynchronize(r.r1));
         float ms = 0;
-        HIPR(hipEventElapsedTime(&ms, s->r0, s->r1));
+        HIPR(hipEventElapsedTime(&ms, r.r0, r.r1));
         *ms_out = ms;
     }
     return RT_OK;
 }
+}  // namespace
+
+extern "C" {
+
+rt_status rt_render_shadow_device(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
+                                  uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba, void* stream,
+                                  double* ms_out) {
+    if (!s || !cam || !light) return fail(RT_EINVAL, "bad render arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    return device_launch(*r, stream, ms_out, "launch_trace_shadow", [&](hipStream_t hs) {
+        return rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, r->bufs.tris, s->n, camf(cam), w,
+                                       h, spp, light, ambient, d_hits, d_rgba, nullptr, hs);
+    });
+}
 
 rt_status rt_render_shadow(rt_scene* s, const rt_camera* cam, const float light[3], float ambient, uint32_t w,
                            uint32_t h, uint32_t spp, rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
-    if (!s || !cam || !light || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
+    if (!s || !cam || !light) return fail(RT_EINVAL, "bad render arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
     const size_t nh = (size_t)w * h * spp;
-    if (hits_out && (st = grow(&s->d_hits, &s->hits_cap, nh * 16))) return st;
-    if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
-    st = rt_render_shadow_device(s, cam, light, ambient, w, h, spp, hits_out ? s->d_hits : nullptr, s->d_rgba,
-                                 nullptr, ms_out);
-    if (st) return st;
-    HIPR(hipStreamSynchronize(s->stream));
-    if (hits_out) HIPR(hipMemcpy(hits_out, s->d_hits, nh * 16, hipMemcpyDeviceToHost));
-    if (rgba_out) HIPR(hipMemcpy(rgba_out, s->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
+    if (hits_out) RTR(grow(&r->d_hits, &r->hits_cap, nh * 16));
+    RTR(grow(&r->d_rgba, &r->rgba_cap, (size_t)w * h * 4));
+    RTR(rt_render_shadow_device(s, cam, light, ambient, w, h, spp, hits_out ? r->d_hits : nullptr, r->d_rgba, nullptr,
+                                ms_out));
+    HIPR(hipStreamSynchronize(r->stream));
+    if (hits_out) HIPR(hipMemcpy(hits_out, r->d_hits, nh * 16, hipMemcpyDeviceToHost));
+    if (rgba_out) HIPR(hipMemcpy(rgba_out, r->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
 rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float light[3], float ambient, uint32_t w,
                                 uint32_t h, uint32_t spp, uint64_t counters_out[2]) {
-    if (!s || !cam || !light || !counters_out || !w || !h || !spp) return fail(RT_EINVAL, "bad arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
-    HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
-    hipError_t e = rt::launch_trace_shadow(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam),
-                                           w, h, spp, light, ambient, nullptr, nullptr, s->d_ctr, s->stream);
+    if (!s || !cam || !light || !counters_out) return fail(RT_EINVAL, "bad arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    RTR(join_caller_work(*r));
+    if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
+    HIPR(hipMemsetAsync(r->d_ctr, 0, 16, r->stream));
+    hipError_t e = rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, r->bufs.tris, s->n, camf(cam),
+                                           w, h, spp, light, ambient, nullptr, nullptr, r->d_ctr, r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace_shadow");
-    HIPR(hipStreamSynchronize(s->stream));
-    HIPR(hipMemcpy(counters_out, s->d_ctr, 16, hipMemcpyDeviceToHost));
+    HIPR(hipStreamSynchronize(r->stream));
+    HIPR(hipMemcpy(counters_out, r->d_ctr, 16, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
+}  // extern "C"
+
 // Path mode: the megakernel, or the wavefront schedule with ray reordering
-// (config path.wavefront); the wavefront reads each depth's queue length back
-// to the host, so it synchronizes the stream between depths.
-static rt_status path_launch(rt_scene* s, const rt_camera* cam, const float light[3], float sky, uint32_t max_depth,
-                             uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
-                             unsigned long long* ctr, hipStream_t hs) {
-    hipError_t e;
-    if (rt::g_trace_config.path_wave) {
+// (config path.wavefront); with a sorted queue the wavefront reads each
+// depth's queue length back to the host, so it synchronizes between depths.
+static hipError_t path_launch(rt_scene* s, Replica& r, const rt_camera* cam, const float light[3], float sky,
+                              uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
+                              unsigned long long* ctr, hipStream_t hs, std::string& err) {
+    const rt::TraceConfig cfg = rt::config_snapshot();
+    if (cfg.path_wave) {
         const uint64_t per_tile = 256ull * spp;
         const uint64_t tiles = rt::tiles_for_rank(w, h, 0, 1);
-        const uint64_t want = rt::g_trace_config.path_batch ? rt::g_trace_config.path_batch : (1u << 22);
+        const uint64_t want = cfg.path_batch ? cfg.path_batch : (1u << 22);
         uint64_t cap = std::min<uint64_t>(tiles * per_tile, std::max<uint64_t>(per_tile, want / per_tile * per_tile));
-        if (cap > (1u << 30)) return fail(RT_EINVAL, "path batch exceeds 2^30 paths (lower spp or path.batch)");
-        if (s->path.cap < cap) {
-            if ((e = rt::alloc_path(s->path, (uint32_t)cap)) != hipSuccess) {
-                rt::free_path(s->path);
-                return hip_fail(e, "alloc_path");
+        if (cap > (1u << 30)) {
+            err = "path batch exceeds 2^30 paths (lower spp or path.batch)";
+            return hipErrorInvalidValue;
+        }
+        if (r.path.cap < cap) {
+            hipError_t e = rt::alloc_path(r.path, (uint32_t)cap);
+            if (e != hipSuccess) {
+                rt::free_path(r.path);
+                err = "alloc_path";
+                return e;
             }
         }
-        e = rt::launch_path_wavefront(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->bufs.params, s->n,
-                                      camf(cam), w, h, spp, light, sky, max_depth, d_hits, d_rgba, ctr, s->path,
-                                      rt::g_trace_config.path_sort, hs);
-        if (e != hipSuccess) return hip_fail(e, "launch_path_wavefront");
-        return RT_OK;
+        return rt::launch_path_wavefront(r.bufs.nodes, r.bufs.wnodes, r.bufs.tri_s, r.bufs.tris, r.bufs.params, s->n,
+                                         camf(cam), w, h, spp, light, sky, max_depth, d_hits, d_rgba, ctr, r.path,
+                                         cfg.path_sort, hs);
     }
-    e = rt::launch_trace_path(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->bufs.tris, s->n, camf(cam), w, h, spp,
-                              light, sky, max_depth, d_hits, d_rgba, ctr, hs);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace_path");
-    return RT_OK;
+    return rt::launch_trace_path(r.bufs.nodes, r.bufs.wnodes, r.bufs.tri_s, r.bufs.tris, s->n, camf(cam), w, h, spp,
+                                 light, sky, max_depth, d_hits, d_rgba, ctr, hs);
 }
+
+extern "C" {
 
 rt_status rt_render_path_device(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
                                 uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
                                 void* stream, double* ms_out) {
-    if (!s || !cam || !light || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
+    if (!s || !cam || !light) return fail(RT_EINVAL, "bad render arguments");
+    RTR(check_frame(w, h, spp));
     if (max_depth > 64) return fail(RT_EINVAL, "max_depth exceeds 64");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
-    if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    if ((st = path_launch(s, cam, light, sky, max_depth, w, h, spp, d_hits, d_rgba, nullptr, hs))) return st;
-    if (ms_out) {
-        HIPR(hipEventRecord(s->r1, hs));
-        HIPR(hipEventSynchronize(s->r1));
-        float ms = 0;
-        HIPR(hipEventElapsedTime(&ms, s->r0, s->r1));
-        *ms_out = ms;
-    }
-    return RT_OK;
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    std::string err;
+    rt_status st = device_launch(*r, stream, ms_out, "launch_path", [&](hipStream_t hs) {
+        return path_launch(s, *r, cam, light, sky, max_depth, w, h, spp, d_hits, d_rgba, nullptr, hs, err);
+    });
+    if (st && !err.empty()) g_err = err + ": " + g_err;
+    return st;
 }
 
 rt_status rt_render_path(rt_scene* s, const rt_camera* cam, const float light[3], float sky, uint32_t max_depth,
                          uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
-    if (!s || !cam || !light || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
+    if (!s || !cam || !light) return fail(RT_EINVAL, "bad render arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
     const size_t nh = (size_t)w * h * spp;
-    if (hits_out && (st = grow(&s->d_hits, &s->hits_cap, nh * 16))) return st;
-    if ((st = grow(&s->d_rgba, &s->rgba_cap, (size_t)w * h * 4))) return st;
-    st = rt_render_path_device(s, cam, light, sky, max_depth, w, h, spp, hits_out ? s->d_hits : nullptr, s->d_rgba,
-                               nullptr, ms_out);
-    if (st) return st;
-    HIPR(hipStreamSynchronize(s->stream));
-    if (hits_out) HIPR(hipMemcpy(hits_out, s->d_hits, nh * 16, hipMemcpyDeviceToHost));
-    if (rgba_out) HIPR(hipMemcpy(rgba_out, s->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
+    if (hits_out) RTR(grow(&r->d_hits, &r->hits_cap, nh * 16));
+    RTR(grow(&r->d_rgba, &r->rgba_cap, (size_t)w * h * 4));
+    RTR(rt_render_path_device(s, cam, light, sky, max_depth, w, h, spp, hits_out ? r->d_hits : nullptr, r->d_rgba,
+                              nullptr, ms_out));
+    HIPR(hipStreamSynchronize(r->stream));
+    if (hits_out) HIPR(hipMemcpy(hits_out, r->d_hits, nh * 16, hipMemcpyDeviceToHost));
+    if (rgba_out) HIPR(hipMemcpy(rgba_out, r->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
 rt_status rt_render_path_work(rt_scene* s, const rt_camera* cam, const float light[3], float sky, uint32_t max_depth,
                               uint32_t w, uint32_t h, uint32_t spp, uint64_t counters_out[3]) {
-    if (!s || !cam || !light || !counters_out || !w || !h || !spp) return fail(RT_EINVAL, "bad arguments");
+    if (!s || !cam || !light || !counters_out) return fail(RT_EINVAL, "bad arguments");
+    RTR(check_frame(w, h, spp));
     if (max_depth > 64) return fail(RT_EINVAL, "max_depth exceeds 64");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
-    HIPR(hipMemsetAsync(s->d_ctr, 0, 32, s->stream));
-    if ((st = path_launch(s, cam, light, sky, max_depth, w, h, spp, nullptr, nullptr, s->d_ctr, s->stream))) return st;
-    HIPR(hipStreamSynchronize(s->stream));
-    HIPR(hipMemcpy(counters_out, s->d_ctr, 24, hipMemcpyDeviceToHost));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    RTR(join_caller_work(*r));
+    if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
+    HIPR(hipMemsetAsync(r->d_ctr, 0, 32, r->stream));
+    std::string err;
+    hipError_t e = path_launch(s, *r, cam, light, sky, max_depth, w, h, spp, nullptr, nullptr, r->d_ctr, r->stream, err);
+    if (e != hipSuccess) return hip_fail(e, err.empty() ? "launch_path" : err.c_str());
+    HIPR(hipStreamSynchronize(r->stream));
+    HIPR(hipMemcpy(counters_out, r->d_ctr, 24, hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
+}  // extern "C"
+
 static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                                uint32_t rank, uint32_t nranks, bool packed, bool binary, uint64_t counters_out[2]) {
-    if (!s || !cam || !counters_out || !w || !h || !spp || !nranks || rank >= nranks)
-        return fail(RT_EINVAL, "bad arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    if (!s->d_ctr) HIPR(hipMalloc((void**)&s->d_ctr, 32));
-    HIPR(hipMemsetAsync(s->d_ctr, 0, 16, s->stream));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
-                                    nranks, packed, nullptr, nullptr, s->d_ctr, binary, s->d_work, nullptr,
-                                    s->stream);
+    if (!s || !cam || !counters_out || !nranks || rank >= nranks) return fail(RT_EINVAL, "bad arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    RTR(join_caller_work(*r));
+    if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
+    HIPR(hipMemsetAsync(r->d_ctr, 0, 16, r->stream));
+    hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
+                                    nranks, packed, nullptr, nullptr, r->d_ctr, binary, r->d_work, nullptr, r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
-    HIPR(hipStreamSynchronize(s->stream));
-    HIPR(hipMemcpy(counters_out, s->d_ctr, 16, hipMemcpyDeviceToHost));
+    HIPR(hipStreamSynchronize(r->stream));
+    HIPR(hipMemcpy(counters_out, r->d_ctr, 16, hipMemcpyDeviceToHost));
     return RT_OK;
 }
+
+extern "C" {
 
 rt_status rt_render_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                              uint64_t counters_out[2]) {
@@ -750,27 +1173,25 @@ rt_status rt_render_tiles_counters(rt_scene* s, const rt_camera* cam, uint32_t w
     return counters_impl(s, cam, w, h, spp, rank, nranks, true, true, counters_out);
 }
 
+rt_status rt_render_tiles_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
+                               uint32_t rank, uint32_t nranks, uint64_t counters_out[2]) {
+    return counters_impl(s, cam, w, h, spp, rank, nranks, true, false, counters_out);
+}
+
 rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, void* d_hits,
                            void* d_rgba, void* stream, double* ms_out) {
-    if (!s || !cam || !w || !h || !spp) return fail(RT_EINVAL, "bad render arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    if ((uint64_t)w * h * spp > 0xFFFFFFFFull) return fail(RT_EINVAL, "w*h*spp exceeds 2^32 samples");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
-    if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
-                                    false, d_hits, d_rgba, nullptr, false, s->d_work,
-                                    sched_for(s, w, h, spp, 0, 1), hs);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace");
-    sched_done(s);
-    if (ms_out) {
-        HIPR(hipEventRecord(s->r1, hs));
-        HIPR(hipEventSynchronize(s->r1));
-        float ms = 0;
-        HIPR(hipEventElapsedTime(&ms, s->r0, s->r1));
-        *ms_out = ms;
-    }
+    if (!s || !cam) return fail(RT_EINVAL, "bad render arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    const rt::TraceConfig cfg = rt::config_snapshot();
+    rt::TileSched* sched = nullptr;
+    RTR(sched_for(*r, w, h, spp, 0, 1, &sched));
+    RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
+        return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
+                                d_hits, d_rgba, nullptr, false, r->d_work, sched, hs);
+    }));
+    sched_done(*r, cfg);
     return RT_OK;
 }
 
@@ -781,32 +1202,25 @@ uint32_t rt_tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nrank
 rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                                  uint32_t rank, uint32_t nranks, void* d_packed_rgba, void* d_packed_hits,
                                  void* stream, double* ms_out) {
-    if (!s || !cam || !w || !h || !spp || !nranks || rank >= nranks) return fail(RT_EINVAL, "bad arguments");
-    if (!s->built) return fail(RT_EINVAL, "scene not built (call rt_bvh_build)");
-    rt_status st = ensure_stream(s);
-    if (st) return st;
-    hipStream_t hs = stream ? (hipStream_t)stream : s->stream;
-    if (ms_out) HIPR(hipEventRecord(s->r0, hs));
-    hipError_t e = rt::launch_trace(s->bufs.nodes, s->bufs.wnodes, s->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
-                                    nranks, true, d_packed_hits, d_packed_rgba, nullptr, false, s->d_work,
-                                    sched_for(s, w, h, spp, rank, nranks), hs);
-    if (e != hipSuccess) return hip_fail(e, "launch_trace");
-    sched_done(s);
-    if (ms_out) {
-        HIPR(hipEventRecord(s->r1, hs));
-        HIPR(hipEventSynchronize(s->r1));
-        float ms = 0;
-        HIPR(hipEventElapsedTime(&ms, s->r0, s->r1));
-        *ms_out = ms;
-    }
+    if (!s || !cam || !nranks || rank >= nranks) return fail(RT_EINVAL, "bad arguments");
+    RTR(check_frame(w, h, spp));
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    const rt::TraceConfig cfg = rt::config_snapshot();
+    rt::TileSched* sched = nullptr;
+    RTR(sched_for(*r, w, h, spp, rank, nranks, &sched));
+    RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
+        return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks,
+                                true, d_packed_hits, d_packed_rgba, nullptr, false, r->d_work, sched, hs);
+    }));
+    sched_done(*r, cfg);
     return RT_OK;
 }
 
 rt_status rt_unpack_tiles_device(const void* d_slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h,
                                  uint32_t nranks, void* d_rgba, int device, void* stream) {
     if (!d_slabs || !d_rgba || !w || !h || !nranks) return fail(RT_EINVAL, "bad arguments");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     hipError_t e = rt::launch_unpack(d_slabs, tiles_per_slab, w, h, nranks, d_rgba, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "launch_unpack");
     return RT_OK;
@@ -815,8 +1229,7 @@ rt_status rt_unpack_tiles_device(const void* d_slabs, uint32_t tiles_per_slab, u
 // ------------------------------------------------------------------ stage entry points
 rt_status rt_stage_bounds(int device, const float* tris, uint32_t n, float bounds9[9]) {
     if ((n && !tris) || !bounds9) return fail(RT_EINVAL, "null argument");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     DevBuf dt, dp, dpar;
     HIPR(dt.alloc((size_t)n * 36));
     HIPR(dp.alloc((size_t)rt::bounds_grid(n) * 24));
@@ -831,8 +1244,7 @@ rt_status rt_stage_bounds(int device, const float* tris, uint32_t n, float bound
 rt_status rt_stage_morton(int device, const float* tris, uint32_t n, const float lo[3], const float inv[3],
                           uint32_t* keys, uint32_t* vals) {
     if ((n && (!tris || !keys || !vals)) || !lo || !inv) return fail(RT_EINVAL, "null argument");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     if (!n) return RT_OK;
     DevBuf dt, dpar, dk, dv, dh, dc;
     HIPR(dt.alloc((size_t)n * 36));
@@ -857,8 +1269,7 @@ rt_status rt_stage_morton(int device, const float* tris, uint32_t n, const float
 rt_status rt_stage_sort(int device, uint32_t* keys, uint32_t* vals, uint32_t n) {
     if (n && (!keys || !vals)) return fail(RT_EINVAL, "null argument");
     if (n > (1u << 30)) return fail(RT_EINVAL, "n exceeds 2^30");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     if (n <= 1) return RT_OK;
     DevBuf k0, k1, v0, v1, gh, cnt;
     const size_t cs = (size_t)rt::sort_tiles(n) * 256;
@@ -887,8 +1298,7 @@ rt_status rt_stage_sort(int device, uint32_t* keys, uint32_t* vals, uint32_t n) 
 rt_status rt_stage_topology(int device, const uint32_t* sorted_keys, uint32_t n, uint32_t* topo, uint32_t* parent,
                             uint32_t* leaf_esc) {
     if (n && !sorted_keys) return fail(RT_EINVAL, "null argument");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     if (!n) return RT_OK;
     // K4 also emits the leaves; feed it identity indices and a zero soup
     DevBuf dk, dv, dtr, dt, dp, dn, dts;
@@ -917,11 +1327,41 @@ rt_status rt_stage_topology(int device, const uint32_t* sorted_keys, uint32_t n,
     return RT_OK;
 }
 
+// K4 + K5 + K6 (+ K7w) over already sorted keys/vals: the refit stage as the
+// build runs it (fused with the topology in k_topo_refit, crossing nodes in
+// k_refit_cross).  nodes_out: (2n-1) x 32-B records.
+rt_status rt_stage_refit(int device, const uint32_t* sorted_keys, const uint32_t* sorted_vals, const float* tris,
+                         uint32_t n, rt_node* nodes_out) {
+    if (n && (!sorted_keys || !sorted_vals || !tris || !nodes_out)) return fail(RT_EINVAL, "null argument");
+    if (n > (1u << 30)) return fail(RT_EINVAL, "n exceeds 2^30");
+    RTR(ensure_device(device));
+    if (!n) return RT_OK;
+    for (uint32_t i = 0; i < n; ++i)
+        if (sorted_vals[i] >= n) return fail(RT_EINVAL, "sorted_vals holds an index >= n");
+    rt::BuildBufs b;
+    hipError_t e = rt::alloc_build(b, n);
+    if (e != hipSuccess) {
+        rt::free_build(b);
+        return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "alloc_build");
+    }
+    struct Guard {
+        rt::BuildBufs& b;
+        ~Guard() { rt::free_build(b); }
+    } guard{b};
+    HIPR(hipMemcpy(b.tris, tris, (size_t)n * 36, hipMemcpyHostToDevice));
+    HIPR(hipMemcpy(b.keys[0], sorted_keys, (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPR(hipMemcpy(b.vals[0], sorted_vals, (size_t)n * 4, hipMemcpyHostToDevice));
+    HIPR(rt::launch_refit_stage(b, n, 0));
+    HIPR(hipDeviceSynchronize());
+    HIPR(hipMemcpy(nodes_out, b.nodes, (size_t)(2 * n - 1) * 32, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const float* tris, const rt_camera* cam,
                          uint32_t w, uint32_t h, uint32_t spp, rt_hit* hits, uint8_t* rgba, uint64_t counters[2]) {
-    if ((n && (!nodes || !tris)) || !cam || !w || !h || !spp) return fail(RT_EINVAL, "bad arguments");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    if ((n && (!nodes || !tris)) || !cam) return fail(RT_EINVAL, "bad arguments");
+    RTR(check_frame(w, h, spp));
+    RTR(ensure_device(device));
     const size_t tot = n ? 2 * (size_t)n - 1 : 1, nh = (size_t)w * h * spp;
     DevBuf dn, dt, dh, dr, dc;
     HIPR(dn.alloc(tot * 32));
@@ -950,8 +1390,7 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
 rt_status rt_stage_intersect(int device, uint32_t count, const float* o, const float* d, const float* tri,
                              const float* t_best, uint32_t* hit, float* tuv) {
     if (count && (!o || !d || !tri || !t_best || !hit || !tuv)) return fail(RT_EINVAL, "null argument");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     if (!count) return RT_OK;
     DevBuf a, b, c, e, f, g;
     HIPR(a.alloc(count * 12ull));
@@ -974,8 +1413,7 @@ rt_status rt_stage_intersect(int device, uint32_t count, const float* o, const f
 
 rt_status rt_stage_minmax(int device, uint32_t count, const float* a, const float* b, float* out) {
     if (count && (!a || !b || !out)) return fail(RT_EINVAL, "null argument");
-    rt_status st = ensure_device(device);
-    if (st) return st;
+    RTR(ensure_device(device));
     if (!count) return RT_OK;
     DevBuf da, db, dout;
     HIPR(da.alloc(count * 4ull));
@@ -1019,7 +1457,12 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path) {
 // diagnostic build only: copy the per-block phase stamps (8 x u64 per block)
 // of the build kernels (which = 0) or the sort kernels (which = 1)
 rt_status rt_debug_tile_order(const uint32_t* d_order) {
-    rt::g_trace_config.order_override = d_order;
+    rt::config_apply(
+        [](rt::TraceConfig& c, const char*, int64_t v) {
+            c.order_override = reinterpret_cast<const uint32_t*>(v);
+            return true;
+        },
+        "", (int64_t)(intptr_t)d_order);
     return RT_OK;
 }
 

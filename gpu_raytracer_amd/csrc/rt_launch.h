@@ -55,6 +55,10 @@ struct BuildEvents { hipEvent_t e[7]; bool valid = false; };
 // between the stages when `stages`.
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev, bool stages);
 
+// K4..K7w alone (rt_stage_refit): sorted keys/vals already in keys[0]/vals[0]
+// and the soup in tris.
+hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t stream);
+
 // Stage launchers for parity entry points (buffers sized by the caller).
 hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, BuildParams* params, hipStream_t s);
 hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,
@@ -92,6 +96,9 @@ struct TraceConfig {
                                 // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbMaxN, 0 = 4-pass LSB always
+    uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
+                                  // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
+    uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };
 
@@ -105,7 +112,14 @@ struct TileSched {
     bool have_prev = false;
     bool fresh = true;              // maps (re)allocated: clear both before the first launch
 };
-extern TraceConfig g_trace_config;
+// The process-wide knobs (rt_config_set).  Every launcher works on one
+// consistent copy taken under the config lock, so a concurrent rt_config_set
+// on another thread never tears a launch's settings.
+TraceConfig config_snapshot();
+// apply f to the config under the lock; f returns false to reject (no change)
+bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key, int64_t value);
+// highest device index the per-device caches cover
+constexpr int kMaxDevices = 64;
 
 // sched: the scene's tile-order state for this frame shape (nullptr:
 // row-major order, no cost map).
@@ -164,6 +178,9 @@ hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, con
                            uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,
                          void* img, hipStream_t s);
+// the same for packed hit slabs [rank][tile][256 px][spp] -> hits[(y*w+x)*spp+s]
+hipError_t launch_unpack_hits(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t spp,
+                              uint32_t nranks, void* hits, hipStream_t s);
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);
 hipError_t launch_intersect(uint32_t count, const float* o, const float* d, const float* tri, const float* tb,
                             uint32_t* hit, float* tuv, hipStream_t s);

@@ -11,6 +11,9 @@
 #include "rt_device.h"
 #include "rt_launch.h"
 
+#include <atomic>
+#include <mutex>
+
 namespace rt {
 
 #ifdef RT_STAMPS
@@ -1209,6 +1212,21 @@ __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ sla
     if (x < W && y < H) img[(uint64_t)y * W + x] = slabs[(uint64_t)blockIdx.x * 256 + threadIdx.x];
 }
 
+// Gathered hit slabs [rank][tile][256 px][spp] -> hits[(y*W+x)*spp + s].
+__global__ __launch_bounds__(256) void k_unpack_hits(const float4* __restrict__ slabs, uint32_t tiles_per_slab,
+                                                     uint32_t W, uint32_t H, uint32_t spp, uint32_t nranks,
+                                                     uint32_t tilesX, uint32_t ntiles, float4* __restrict__ hits) {
+    const uint32_t rk = blockIdx.x / tiles_per_slab, b = blockIdx.x % tiles_per_slab;
+    const uint32_t t = rk + b * nranks;
+    if (t >= ntiles) return;
+    const uint32_t tx = t % tilesX, ty = t / tilesX;
+    const uint32_t lx = threadIdx.x & 15, ly = threadIdx.x >> 4;
+    const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
+    if (x >= W || y >= H) return;
+    const uint64_t src = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * spp, dst = ((uint64_t)y * W + x) * spp;
+    for (uint32_t s = 0; s < spp; ++s) hits[dst + s] = slabs[src + s];
+}
+
 // KAT entry point: Moller-Trumbore per (o, d, tri, t_best).
 __global__ void k_intersect(uint32_t count, const float* __restrict__ o, const float* __restrict__ d,
                             const float* __restrict__ tri, const float* __restrict__ tbest,
@@ -1314,12 +1332,29 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) 
     return (nt - rank + nranks - 1) / nranks;
 }
 
+namespace {
 TraceConfig g_trace_config;
+std::mutex g_config_mu;
+}  // namespace
+
+TraceConfig config_snapshot() {
+    std::lock_guard<std::mutex> lk(g_config_mu);
+    return g_trace_config;
+}
+
+bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key, int64_t value) {
+    std::lock_guard<std::mutex> lk(g_config_mu);
+    TraceConfig c = g_trace_config;
+    if (!f(c, key, value)) return false;
+    g_trace_config = c;
+    return true;
+}
 
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tris, uint32_t n, const CamF& c,
                         uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits,
                         void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
                         TileSched* sched, hipStream_t s) {
+    const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
     if (!nb) return hipSuccess;
     Cam cam;
@@ -1329,25 +1364,31 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     const uint32_t tilesX = (w + 15) / 16;
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
-    const uint32_t cap = g_trace_config.stack_cap;
-    if (g_trace_config.variant == 1 && wnodes && n >= 2 && !binary_counts && work) {
+    const uint32_t cap = cfg.stack_cap;
+    if (cfg.variant == 1 && wnodes && n >= 2 && !binary_counts && work) {
         const uint32_t nunits = nb * 4;
         hipError_t me = hipMemsetAsync(work, 0, kPoolCounters * 128, s);
         if (me != hipSuccess) return me;
-        uint32_t blocks = g_trace_config.blocks;
+        uint32_t blocks = cfg.blocks;
         if (!blocks) {  // auto: exactly the resident capacity (one wave per SIMD slot, no second round)
-            static uint32_t resident = 0;
-            if (!resident) {
-                int per_cu = 0, dev = 0, cus = 0;
-                hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            // per device (a process may drive several), computed once each
+            static std::atomic<uint32_t> resident[kMaxDevices];
+            int dev = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e != hipSuccess) return e;
+            if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+            uint32_t r = resident[dev].load(std::memory_order_relaxed);
+            if (!r) {
+                int per_cu = 0, cus = 0;
+                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
                     &per_cu, reinterpret_cast<const void*>(k_trace_pool<false, false>), 256, 0);
                 if (e != hipSuccess) return e;
-                if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
                 if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
                     return e;
-                resident = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
+                r = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
+                resident[dev].store(r, std::memory_order_relaxed);
             }
-            blocks = resident;
+            blocks = r;
         }
         const uint32_t grid = min(blocks, (nunits + 3) / 4);
 #define RT_POOL(C, P)                                                                                               \
@@ -1363,12 +1404,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     }
     // wide (4-ary) traversal unless asked for the binary one: variant 2, no
     // K7w records (stage entry points), n < 2, or binary work counters
-    const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2 && !binary_counts;
-    const bool small = (nranks > 1 ? g_trace_config.wg_tiles : g_trace_config.wg) == 64;
+    const bool wide = wnodes && n >= 2 && cfg.variant != 2 && !binary_counts;
+    const bool small = (nranks > 1 ? cfg.wg_tiles : cfg.wg) == 64;
     // costliest tiles first from the previous frame's map (DESIGN.md "Tile order")
     const uint32_t* order = nullptr;
     uint32_t* cost_out = nullptr;
-    if (sched && g_trace_config.tile_order && nb <= 1024 * kOrderPerThread) {
+    if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
             hipError_t me = hipMemsetAsync(sched->cost_prev, 0, (size_t)nb * 4, s);
             if (me == hipSuccess) me = hipMemsetAsync(sched->cost_cur, 0, (size_t)nb * 4, s);
@@ -1381,7 +1422,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         }
         cost_out = sched->cost_cur;
     }
-    if (g_trace_config.order_override) order = g_trace_config.order_override;
+    if (cfg.order_override) order = cfg.order_override;
     const uint16_t* px_prev = nullptr;
     uint16_t* px_cost = nullptr;
     // full frames only by default: a frame is issue-bound and the sort cuts the
@@ -1391,7 +1432,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     // (DESIGN.md "Pixel order").  256-thread blocks only (the ranking is per
     // block).
     if (cost_out && !small && sched->px_cur &&
-        (g_trace_config.px_sort == 2 || (g_trace_config.px_sort == 1 && nranks == 1))) {
+        (cfg.px_sort == 2 || (cfg.px_sort == 1 && nranks == 1))) {
         if (sched->have_prev) px_prev = sched->px_prev;
         px_cost = sched->px_cur;
     }
@@ -1421,6 +1462,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
 hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
                                uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
                                float ambient, void* hits, void* rgba, unsigned long long* counters, hipStream_t s) {
+    const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, 0, 1);
     if (!nb) return hipSuccess;
     Cam cam;
@@ -1433,8 +1475,8 @@ hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const flo
     const uint32_t tilesX = (w + 15) / 16;
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
-    const bool wide = wnodes && n >= 2 && g_trace_config.variant != 2;
-    const uint32_t cap = g_trace_config.stack_cap;
+    const bool wide = wnodes && n >= 2 && cfg.variant != 2;
+    const uint32_t cap = cfg.stack_cap;
 #define RT_SHADOW(C, WI)                                                                                        \
     hipLaunchKernelGGL((k_trace<C, false, WI, 256, true>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, tri_s, \
                        n, cam, w, h, spp, 0u, 1u, tilesX, H, R, counters, tris, lt)
@@ -1451,6 +1493,7 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float
                              uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
                              float sky, uint32_t max_depth, void* hits, void* rgba, unsigned long long* counters,
                              hipStream_t s) {
+    const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, 0, 1);
     if (!nb) return hipSuccess;
     Cam cam;
@@ -1465,9 +1508,9 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     // K7w records unless the binary traversal is asked for (variant 2)
-    const uint4* wn = (g_trace_config.variant != 2) ? wnodes : nullptr;
-    const uint32_t cap = g_trace_config.stack_cap;
-    const bool small = g_trace_config.path_wg == 64;
+    const uint4* wn = (cfg.variant != 2) ? wnodes : nullptr;
+    const uint32_t cap = cfg.stack_cap;
+    const bool small = cfg.path_wg == 64;
 #define RT_PATH(C, NT)                                                                                            \
     hipLaunchKernelGGL((k_path<C, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, cam, \
                        w, h, spp, tilesX, pc, H, R, counters)
@@ -1515,6 +1558,7 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const f
                                  uint32_t spp, const float light[3], float sky, uint32_t max_depth, void* hits,
                                  void* rgba, unsigned long long* counters, PathBufs& pb, uint32_t sort_digits,
                                  hipStream_t s) {
+    const TraceConfig cfg = config_snapshot();
     const uint32_t nt = tiles_for_rank(w, h, 0, 1);
     if (!nt) return hipSuccess;
     const uint32_t per_tile = 256 * spp;
@@ -1528,8 +1572,8 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const f
     pc.sky = sky;
     pc.max_depth = max_depth;
     const uint32_t tilesX = (w + 15) / 16;
-    const uint4* wn = (g_trace_config.variant != 2) ? wnodes : nullptr;
-    const uint32_t wcap = g_trace_config.stack_cap;
+    const uint4* wn = (cfg.variant != 2) ? wnodes : nullptr;
+    const uint32_t wcap = cfg.stack_cap;
     const uint32_t batch = pb.cap / per_tile;
     float4* H = reinterpret_cast<float4*>(hits);
     hipError_t e;
@@ -1590,6 +1634,15 @@ hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w,
     const uint32_t tilesX = (w + 15) / 16, nt = tilesX * ((h + 15) / 16);
     hipLaunchKernelGGL(k_unpack, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const uint32_t*)slabs, tiles_per_slab,
                        w, h, nranks, tilesX, nt, (uint32_t*)img);
+    return hipGetLastError();
+}
+
+hipError_t launch_unpack_hits(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t spp,
+                              uint32_t nranks, void* hits, hipStream_t s) {
+    if (!tiles_per_slab || !nranks) return hipSuccess;
+    const uint32_t tilesX = (w + 15) / 16, nt = tilesX * ((h + 15) / 16);
+    hipLaunchKernelGGL(k_unpack_hits, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const float4*)slabs,
+                       tiles_per_slab, w, h, spp, nranks, tilesX, nt, (float4*)hits);
     return hipGetLastError();
 }
 

@@ -13,7 +13,7 @@ from dataclasses import dataclass
 
 import numpy as np
 
-from ._lib import SENTINEL, call, lib, rt_build_times, rt_camera
+from ._lib import RT_BACKEND_HIP, SENTINEL, call, lib, rt_build_times, rt_camera
 
 NODE_DTYPE = np.dtype([("lo", "<f4", (3,)), ("hi", "<f4", (3,)), ("a", "<u4"), ("esc", "<u4")])
 HIT_DTYPE = np.dtype([("t", "<f4"), ("u", "<f4"), ("v", "<f4"), ("prim", "<u4")])
@@ -118,10 +118,20 @@ class Scene:
         call("rt_scene_set_device", self._h, int(device))
 
     # -- build
-    def build(self) -> float:
+    def build(self, device_mask: int = 0, backend: int = RT_BACKEND_HIP) -> float:
+        """rt_bvh_build: replicas on the devices of device_mask (0 = the
+        scene's device); returns the device time of the (longest) build."""
         ms = C.c_double()
-        call("rt_bvh_build", self._h, C.byref(ms))
+        call("rt_bvh_build", self._h, int(backend), int(device_mask), C.byref(ms))
         return ms.value
+
+    def replicas(self) -> list:
+        """Devices holding a built BVH replica, primary first."""
+        cnt = C.c_uint32()
+        call("rt_bvh_replicas", self._h, 0, None, C.byref(cnt))
+        devs = (C.c_int * max(cnt.value, 1))()
+        call("rt_bvh_replicas", self._h, cnt.value, devs, C.byref(cnt))
+        return [int(devs[i]) for i in range(cnt.value)]
 
     def save_bvh(self, path: str) -> None:
         """RTBVH1 cache of the built BVH."""
@@ -156,12 +166,14 @@ class Scene:
                     lo=bounds[0:3].copy(), hi=bounds[3:6].copy(), inv=bounds[6:9].copy())
 
     # -- render
-    def render(self, cam: rt_camera, w: int, h: int, spp: int = 1, hits: bool = True, rgba: bool = True):
-        """Returns (hits[h*w*spp] HIT_DTYPE or None, rgba[h*w*4] uint8 or None, trace_ms)."""
+    def render(self, cam: rt_camera, w: int, h: int, spp: int = 1, hits: bool = True, rgba: bool = True,
+               ngpus: int = 1):
+        """Returns (hits[h*w*spp] HIT_DTYPE or None, rgba[h*w*4] uint8 or None, frame_ms).
+        ngpus > 1: the in-library multi-GPU render (replicas + RCCL gather)."""
         hb = np.zeros(w * h * spp, HIT_DTYPE) if hits else None
         rb = np.zeros(w * h * 4, np.uint8) if rgba else None
         ms = C.c_double()
-        call("rt_render", self._h, C.byref(cam), w, h, spp, _p(hb) if hits else None,
+        call("rt_render", self._h, C.byref(cam), w, h, spp, int(ngpus), _p(hb) if hits else None,
              _p(rb) if rgba else None, C.byref(ms))
         return hb, rb, ms.value
 
@@ -260,6 +272,12 @@ class Scene:
         call("rt_render_tiles_counters", self._h, C.byref(cam), w, h, spp, rank, nranks, _p(c))
         return c
 
+    def render_tiles_work(self, cam, w, h, spp, rank, nranks) -> np.ndarray:
+        """The trace kernel's own fetches (records, triangle records) for one rank's tiles."""
+        c = np.zeros(2, np.uint64)
+        call("rt_render_tiles_work", self._h, C.byref(cam), w, h, spp, rank, nranks, _p(c))
+        return c
+
     def render_tiles_device(self, cam, w, h, spp, rank, nranks, d_rgba: int, d_hits: int = 0,
                             stream: int = 0, timed: bool = False):
         ms = C.c_double()
@@ -340,6 +358,19 @@ def stage_topology(sorted_keys, device: int = 0):
     return topo[: max(n - 1, 0)], parent[: max(2 * n - 1, 0)], lesc[:n]
 
 
+def stage_refit(sorted_keys, sorted_vals, tris, device: int = 0) -> np.ndarray:
+    """K5 + K6 (+ K7w) over sorted keys/vals: the (2n-1) node records."""
+    k = np.ascontiguousarray(sorted_keys, np.uint32)
+    v = np.ascontiguousarray(sorted_vals, np.uint32)
+    t = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    n = len(k)
+    if len(v) != n or len(t) != n:
+        raise ValueError("keys, vals and tris must have the same length")
+    nodes = np.zeros(max(2 * n - 1, 1), NODE_DTYPE)
+    call("rt_stage_refit", device, _p(k) if n else None, _p(v) if n else None, _p(t) if n else None, n, _p(nodes))
+    return nodes[: max(2 * n - 1, 0)]
+
+
 def stage_trace(nodes, tris, cam: rt_camera, w, h, spp=1, device: int = 0):
     t = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     nd = np.ascontiguousarray(nodes, NODE_DTYPE)
@@ -374,4 +405,4 @@ def stage_minmax(a, b, device: int = 0):
 
 __all__ = ["Scene", "config_set", "camera_look_at", "camera_array", "tiles_for_rank", "unpack_tiles_device", "dump_ppm",
            "dump_hits", "device_count", "stage_bounds", "stage_morton", "stage_sort", "stage_topology",
-           "stage_trace", "stage_intersect", "stage_minmax", "NODE_DTYPE", "HIT_DTYPE", "SENTINEL"]
+           "stage_refit", "stage_trace", "stage_intersect", "stage_minmax", "NODE_DTYPE", "HIT_DTYPE", "SENTINEL"]

@@ -16,7 +16,15 @@
  *   - the caller owns every pointer argument; the library copies inputs and
  *     writes into caller buffers; scenes are opaque, freed by rt_scene_free;
  *   - distinct scenes may be used from distinct threads; calls on one scene
- *     are not reentrant;
+ *     are not reentrant; rt_config_set may be called from any thread (every
+ *     launch works on one consistent snapshot of the knobs);
+ *   - a scene holds one BVH replica per device it was built on (SURVEY.md
+ *     §8(e): the BVH is replicated); multi-GPU rendering is internal to
+ *     rt_render(ngpus > 1) -- replicas, tile deal, RCCL gather, unpack;
+ *   - device work the *_device entry points queue on a caller stream is
+ *     ordered by the library: a later launch of the same scene on another
+ *     stream waits for it, and rt_bvh_build / rt_bvh_load / rt_scene_free
+ *     wait for it before touching the scene's buffers;
  *   - HIP failures map to RT_EDEVICE, RCCL-side failures to RT_ECOMM;
  *   - there is NO CPU fallback: without a usable gfx950 device every compute
  *     entry point fails with RT_EDEVICE.
@@ -36,6 +44,11 @@ extern "C" {
 #endif
 
 #define RT_SENTINEL 0xFFFFFFFFu
+/* rt_bvh_build backends: the library has no CPU backend --
+ * RT_BACKEND_CPU is rejected with RT_EINVAL (the CPU oracle under oracle/ is
+ * test infrastructure, never a fallback). */
+#define RT_BACKEND_CPU 0
+#define RT_BACKEND_HIP 1
 
 typedef struct rt_scene rt_scene; /* opaque, owned by the library */
 
@@ -79,11 +92,17 @@ void rt_scene_free(rt_scene* s);
 rt_status rt_camera_look_at(const double eye[3], const double at[3], const double up[3],
                             double vfov_deg, uint32_t w, uint32_t h, rt_camera* out);
 
-/* ---- BVH build (SURVEY.md §8(b) rt_bvh_build; device mask replaced by the
- * scene's device -- one process per GPU).  Uploads the soup once (H2D is not
- * part of ms_out), then runs K0..K6 on the scene's stream.  ms_out: device
- * time of the build (hipEvents around it). */
-rt_status rt_bvh_build(rt_scene* s, double* ms_out);
+/* ---- BVH build (SURVEY.md §8(b) rt_bvh_build(scene, backend, device_mask,
+ * ms)).  backend: RT_BACKEND_HIP (RT_BACKEND_CPU -> RT_EINVAL).  device_mask:
+ * bit d = build a replica on device d, concurrently, one stream each (the
+ * lowest device of a scene's first build becomes its primary device); 0 = the
+ * scene's device (rt_scene_set_device, default 0).  A bit naming a device
+ * that is not visible -> RT_EDEVICE.  Uploads the soup once per device (H2D
+ * is not part of ms_out), then runs K0..K7w.  ms_out: device time of the
+ * build (hipEvents around it; the longest replica). */
+rt_status rt_bvh_build(rt_scene* s, int backend, uint32_t device_mask, double* ms_out);
+/* devices holding a built replica, primary first (call with max = 0 to size) */
+rt_status rt_bvh_replicas(const rt_scene* s, uint32_t max, int* devices, uint32_t* count_out);
 /* times of the last build: `total` always; the per-stage fields only when
  * the build ran with rt_config_set("build.stage_events", 1) (0 otherwise --
  * the extra events cost GPU time, so timed builds run without them) */
@@ -114,10 +133,17 @@ rt_status rt_bvh_load(rt_scene* s, const char* path);
  * node (layout: gpu_raytracer_amd/csrc/rt_device.h); nothing for n < 2. */
 rt_status rt_bvh_read_wide(const rt_scene* s, void* records);
 
-/* ---- render (SURVEY.md §8(b) rt_render).  hits_out: w*h*spp records,
- * rgba_out: w*h*4 bytes; either may be NULL.  Single GPU; multi-GPU is the
- * tile API below driven by one process per GPU (bench.py / torch.distributed). */
-rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
+/* ---- render (SURVEY.md §8(b) rt_render(scene, cam, w, h, spp, ngpus, hits,
+ * rgba)).  hits_out: w*h*spp records, rgba_out: w*h*4 bytes; either may be
+ * NULL.  ngpus = 1: the primary replica renders the frame.  ngpus > 1
+ * (SURVEY.md §3(iii), §8(e)): replicas on ngpus devices (the scene's build
+ * replicas first, the missing ones built on the lowest free devices), tile t
+ * traced by replica t mod ngpus into a packed slab, the slabs gathered to
+ * the primary with RCCL (ncclGather over xGMI, one communicator per device
+ * list, cached on the scene) and unpacked there.  ngpus > visible devices ->
+ * RT_EDEVICE; RCCL failures -> RT_ECOMM.  The image and hits are identical
+ * for every ngpus.  ms_out: device time of the frame (trace .. unpack). */
+rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
                     rt_hit* hits_out, uint8_t* rgba_out, double* ms_out);
 /* deterministic work counters of a render with the §9.7 binary traversal
  * (the oracle's counters): [0] nodes fetched, [1] tris tested */
@@ -178,6 +204,9 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
 rt_status rt_render_tiles_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,
                                    uint32_t spp, uint32_t rank, uint32_t nranks,
                                    uint64_t counters_out[2]);
+/* the trace kernel's own fetches for `rank`'s tiles (rt_render_work's counters) */
+rt_status rt_render_tiles_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
+                               uint32_t rank, uint32_t nranks, uint64_t counters_out[2]);
 /* Unpack nranks gathered slabs (each tiles_per_slab*1024 B, slab r = rank r)
  * into a w*h*4 device image. */
 rt_status rt_unpack_tiles_device(const void* d_slabs, uint32_t tiles_per_slab, uint32_t w,
@@ -197,6 +226,10 @@ rt_status rt_stage_sort(int device, uint32_t* keys, uint32_t* vals, uint32_t n);
  * range_hi} per internal node; parent[2n-1]; leaf_esc[n]. */
 rt_status rt_stage_topology(int device, const uint32_t* sorted_keys, uint32_t n, uint32_t* topo,
                             uint32_t* parent, uint32_t* leaf_esc);
+/* K5 + K6 (+ K7w) over sorted keys/vals (the build fuses them with K4 in
+ * k_topo_refit): nodes_out[2n-1] with every AABB, child and escape link. */
+rt_status rt_stage_refit(int device, const uint32_t* sorted_keys, const uint32_t* sorted_vals, const float* tris,
+                         uint32_t n, rt_node* nodes_out);
 rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const float* tris,
                          const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                          rt_hit* hits, uint8_t* rgba, uint64_t counters[2]);
@@ -227,7 +260,11 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * (default); "path.sort" 0..4 = top key bytes each queue is radix-sorted by
  * for coherence (ray kind, direction octant, Morton code of the origin; 0 =
  * unsorted, the default; sorting reads each queue length back to the host);
- * "path.batch" paths per wavefront batch (0 = 4M).  "build.stage_events"
+ * "path.batch" paths per wavefront batch (0 = 4M).  "render.emulate" 0/1:
+ * rt_render(ngpus > 1) puts every rank's replica on the scene's device and
+ * gathers with device copies instead of RCCL (multi-rank tests on one GPU);
+ * "render.rccl1" 0/1: rt_render(ngpus = 1) through the tiled + RCCL path
+ * (a 1-rank communicator).  "build.stage_events"
  * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
  * 0/1: timing events of scenes created afterwards record with the
  * system-scope fence (default 0: no L2 writeback at each record).  Results

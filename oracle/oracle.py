@@ -40,6 +40,18 @@ def build_oracle() -> str:
     return _LIB_PATH
 
 
+def use_native_build() -> str:
+    """Switch this process to the -march=native build of the same source
+    (bench.py's timed CPU baseline; compiled on the host that runs it).
+    Must be called before the first lib()."""
+    global _LIB_PATH
+    if _lib is not None:
+        raise RuntimeError("oracle already loaded")
+    subprocess.run(["make", "-s", "-C", _HERE, "native"], check=True)
+    _LIB_PATH = os.path.join(_HERE, "build", "liboracle_native.so")
+    return _LIB_PATH
+
+
 _lib = None
 
 

@@ -11,6 +11,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <stdatomic.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -378,16 +379,27 @@ static void trace_ray(const orc_node* nodes, uint32_t n, const float* tris, cons
 typedef struct {
     const orc_node* nodes; uint32_t n; const float* tris; const orc_camera* cam;
     uint32_t w, h, spp, row0, row_step; orc_hit* hits;
-    int tid, nthreads; uint64_t cn, ct;
+    atomic_uint_fast64_t* next;  /* shared work cursor: 64-pixel row segments */
+    uint64_t cn, ct;
 } trace_job;
 
+/* Work is dealt dynamically in 64-pixel row segments (the rows the camera
+ * sees differ ~100x in cost), and each thread keeps its counters in locals:
+ * per-ray updates of adjacent job structs would false-share a cache line.
+ * Every ray's result lands at its own index, so the output and the counter
+ * sums are the same for any thread count and schedule. */
 static void* trace_worker(void* arg) {
     trace_job* j = (trace_job*)arg;
     const orc_camera* c = j->cam;
-    uint32_t k = 0;
-    for (uint64_t y = j->row0; y < j->h; y += j->row_step, ++k) {
-        if ((int)(k % (uint32_t)j->nthreads) != j->tid) continue;
-        for (uint32_t x = 0; x < j->w; ++x) {
+    const uint64_t rows = j->row0 < j->h ? (j->h - j->row0 + j->row_step - 1) / j->row_step : 0;
+    const uint64_t segs_per_row = (j->w + 63) / 64, units = rows * segs_per_row;
+    uint64_t cn = 0, ct = 0;
+    for (;;) {
+        const uint64_t u = atomic_fetch_add_explicit(j->next, 1, memory_order_relaxed);
+        if (u >= units) break;
+        const uint64_t y = j->row0 + (u / segs_per_row) * j->row_step;
+        const uint32_t x0 = (uint32_t)(u % segs_per_row) * 64u, x1 = x0 + 64u < j->w ? x0 + 64u : j->w;
+        for (uint32_t x = x0; x < x1; ++x) {
             for (uint32_t s = 0; s < j->spp; ++s) {
                 const uint32_t sidx = (uint32_t)((y * j->w + x) * j->spp + s);
                 float jx = 0.5f, jy = 0.5f;
@@ -399,10 +411,12 @@ static void* trace_worker(void* arg) {
                 const float px = (float)x + jx, py = (float)y + jy;
                 float d[3];
                 for (int a = 0; a < 3; ++a) d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
-                trace_ray(j->nodes, j->n, j->tris, c->eye, d, &j->hits[sidx], &j->cn, &j->ct);
+                trace_ray(j->nodes, j->n, j->tris, c->eye, d, &j->hits[sidx], &cn, &ct);
             }
         }
     }
+    j->cn = cn;
+    j->ct = ct;
     return NULL;
 }
 
@@ -413,8 +427,10 @@ void orc_trace(const orc_node* nodes, uint32_t n, const float* tris, const orc_c
     if (row_step < 1) row_step = 1;
     trace_job* jobs = (trace_job*)calloc((size_t)nthreads, sizeof(trace_job));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    atomic_uint_fast64_t next;
+    atomic_init(&next, 0);
     for (int t = 0; t < nthreads; ++t) {
-        trace_job jb = {nodes, n, tris, cam, w, h, spp, row0, row_step, hits, t, nthreads, 0, 0};
+        trace_job jb = {nodes, n, tris, cam, w, h, spp, row0, row_step, hits, &next, 0, 0};
         jobs[t] = jb;
         if (nthreads > 1) pthread_create(&th[t], NULL, trace_worker, &jobs[t]);
     }

@@ -106,9 +106,44 @@ def test_tile_partition(rt, w, h, P):
 
 
 def test_invalid_arguments(rt):
-    with pytest.raises(rt.RtError) as e:
-        rt.Scene.from_soup(np.zeros((0, 9), np.float32)).render(rt.camera_look_at((0, 0, -1), (0, 0, 0), (0, 1, 0), 45, 8, 8), 8, 8)
-    assert e.value.status == -1  # not built
+    cam = rt.camera_look_at((0, 0, -1), (0, 0, 0), (0, 1, 0), 45, 8, 8)
+    with rt.Scene.from_soup(np.zeros((3, 9), np.float32)) as s:
+        for args, kw in [((0, 8), {}), ((8, 8), {"ngpus": 0}), ((8, 8), {"ngpus": 65}), ((8, 8, 0), {})]:
+            with pytest.raises(rt.RtError) as e:
+                s.render(cam, *args, **kw)
+            assert e.value.status == -1, (args, kw)
+        # an unbuilt scene: RT_EINVAL on a GPU box, RT_EDEVICE without a device
+        with pytest.raises(rt.RtError) as e:
+            s.render(cam, 8, 8)
+        assert e.value.status == (-1 if rt.device_count() else -4)
+
+
+def test_render_ngpus_beyond_visible_devices(rt):
+    """rt_render(ngpus > visible devices) -> RT_EDEVICE (SURVEY.md §8(b):
+    multi-GPU is internal to rt_render), checked before any device work."""
+    cam = rt.camera_look_at((0, 0, -1), (0, 0, 0), (0, 1, 0), 45, 8, 8)
+    with rt.Scene.from_soup(np.zeros((3, 9), np.float32)) as s:
+        for ngpus in (rt.device_count() + 1, 64):
+            with pytest.raises(rt.RtError) as e:
+                s.render(cam, 8, 8, ngpus=ngpus)
+            assert e.value.status == -4, ngpus
+
+
+def test_build_backend_and_mask(rt):
+    """rt_bvh_build(scene, backend, device_mask, ms): the CPU backend does not
+    exist (RT_EINVAL, never a silent oracle fallback); a mask naming a device
+    that is not visible is RT_EDEVICE."""
+    with rt.Scene.from_soup(np.zeros((3, 9), np.float32)) as s:
+        with pytest.raises(rt.RtError) as e:
+            s.build(backend=rt.RT_BACKEND_CPU)
+        assert e.value.status == -1 and "no CPU backend" in str(e.value)
+        with pytest.raises(rt.RtError) as e:
+            s.build(backend=7)
+        assert e.value.status == -1
+        with pytest.raises(rt.RtError) as e:
+            s.build(device_mask=1 << max(rt.device_count(), 1))
+        assert e.value.status == -4
+        assert s.replicas() == []
 
 
 def test_no_cpu_fallback(rt):
@@ -206,6 +241,8 @@ CONFIG_KEYS = {
     "path.wg": ([64, 256], [100], 64),
     "path.sort": ([0, 4], [5], 0),
     "path.batch": ([0, 1 << 20], [-1], 0),
+    "render.emulate": ([0, 1], [2], 0),
+    "render.rccl1": ([0, 1], [2], 0),
 }
 
 

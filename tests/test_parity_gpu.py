@@ -378,12 +378,25 @@ def _successive_frames(R, oracle, s_tris, exp):
         cam = _cam(R, SOUP_VIEW, w, h)
         _, full, _ = s.render(cam, w, h, spp, hits=False)
         tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
-        for _ in range(3):  # per-rank maps: frames 2 and 3 reordered
-            slabs = torch.zeros((P, tmax * 256), dtype=torch.int32, device="cuda")
-            for r in range(P):
-                s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr())
-            s.sync()
-            img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
-            R.unpack_tiles_device(slabs.data_ptr(), tmax, w, h, P, img.data_ptr())
-            torch.cuda.synchronize()
-            assert np.array_equal(img.cpu().numpy().view(np.uint8), full)
+        # per-rank maps: 3 successive frames of the SAME rank, so frames 2 and
+        # 3 run reordered from that rank's own cost map (a scene keeps one
+        # map per frame shape, and rank is part of the shape)
+        for wg in (64, 256):
+            R.config_set("trace.wg_tiles", wg)
+            try:
+                slabs = torch.zeros((P, tmax * 256), dtype=torch.int32, device="cuda")
+                for r in range(P):
+                    first = None
+                    for frame in range(3):
+                        s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr())
+                        s.sync()
+                        cur = slabs[r].cpu().numpy().copy()
+                        if first is None:
+                            first = cur
+                        assert np.array_equal(cur, first), (wg, r, frame)
+                img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+                R.unpack_tiles_device(slabs.data_ptr(), tmax, w, h, P, img.data_ptr())
+                torch.cuda.synchronize()
+                assert np.array_equal(img.cpu().numpy().view(np.uint8), full), wg
+            finally:
+                R.config_set("trace.wg_tiles", 64)
