@@ -31,10 +31,11 @@ ranks come from the environment.
 roofline: the trace launch (k_tile_order + k_trace) -- the bytes the kernel
   requests (64 B per K7w record + 48 B per triangle record fetched, its own
   deterministic counters, + 16 B hit + 4 B RGBA written per ray) over its
-  event-timed duration, against the 8.0 TB/s HBM peak; beside it the PMC
-  measured HBM bytes (hbm_frac) and VALU issue (issue_frac) of the same
-  kernel from the committed profile (profiles/pmc_summary.json); `bound` is
-  the largest of the three.  The SURVEY.md §8(d) binary-traversal byte model
+  event-timed duration, against the 8.0 TB/s HBM peak (frac) and the
+  aggregate L2 bandwidth (l2_frac); beside it the PMC-measured HBM bytes
+  (hbm_frac) and VALU issue (issue_frac) of the same kernel from the committed
+  profile (profiles/pmc_summary.json, tools/profile_r02.sh); `limiter` names
+  the largest fraction.  The SURVEY.md §8(d) binary-traversal byte model
   is kept as algo_bytes_binary_model (it charges node visits the wide kernel
   does not make, so its fraction is not a roofline of this kernel).
 cpu_baseline (rank 0, N=1 only): the CPU oracle (oracle/, a port of the same
@@ -59,6 +60,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # /opt/skills/guides/MI355X_MICROARCH.md: 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCD L2s
 BUILD_BYTES_PER_PRIM = 404  # SURVEY.md §8(d) canonical build byte model
 METRIC = "Mrays/s @1920×1080×1spp + BVH build Mprims/s, 1M-tri scene, 1/2/4/8 GPUs"
 ORBIT_DEG = 0.25  # camera motion per step
@@ -78,6 +80,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     ap.add_argument("--dump", default="", help="write the rank-0 image as PPM")
+    ap.add_argument("--only-timed", action="store_true",
+                    help="warm-up + timed steps only (the PMC passes of tools/profile_r02.sh)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for the benchmark; gloo only to rehearse N>1 on one GPU")
     return ap.parse_args()
@@ -116,18 +120,37 @@ def orbit_view(view, step):
     return (view.at[0] + rx, view.at[1] + ey, view.at[2] + rz)
 
 
-def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters):
-    """Oracle (-march=native build) build on 1 thread + full-frame trace on
-    `threads` threads; returns dict."""
+def cpu_quota():
+    """CPUs this process's cgroup may run on at once (cpu.max quota/period),
+    or None when unlimited / unknown."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(p), 2)
+    except Exception:
+        return None
+
+
+def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters, min_seconds=10.0):
+    """Oracle (-march=native build): the same 1M-soup BVH built on 1 thread,
+    then full frames of the bench's orbiting camera traced on `threads`
+    threads until at least `min_seconds` of wall time (a bounded sample of the
+    same workload); returns dict.  The first frame's counters are checked
+    against the GPU's (static camera)."""
     from oracle import oracle as O  # cpu_baseline leg only
     O.use_native_build()
     t0 = time.perf_counter()
     b = O.build(tris)
     t_build = time.perf_counter() - t0
     cam = O.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
-    t0 = time.perf_counter()
     _, cnt = O.trace(b["nodes"], tris, cam, w, h, spp, nthreads=threads)
-    t_trace = time.perf_counter() - t0
+    frames, t_trace, i = 0, 0.0, 0
+    while t_trace < min_seconds:
+        c = O.camera_look_at(orbit_view(view, i), view.at, view.up, view.vfov, w, h)
+        t0 = time.perf_counter()
+        O.trace(b["nodes"], tris, c, w, h, spp, nthreads=threads)
+        t_trace += time.perf_counter() - t0
+        frames += 1
+        i += 1
     model = "unknown"
     try:
         for line in open("/proc/cpuinfo"):
@@ -136,14 +159,14 @@ def cpu_baseline(tris, view, w, h, spp, threads, gpu_counters):
                 break
     except OSError:
         pass
-    rays = w * h * spp
+    rays = w * h * spp * frames
     return {
         "value": rays / t_trace / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
         "threads_used": threads, "cores_available": len(os.sched_getaffinity(0)),
-        "cpus_in_machine": os.cpu_count(),
-        "sample": f"full frame {w}x{h}x{spp} (static camera) traced on {threads} threads ({t_trace:.2f} s); "
-                  f"full {len(tris)}-tri BVH built on 1 thread ({t_build:.2f} s); oracle built -O3 -march=native "
-                  f"-ffp-contract=off on this host",
+        "cpus_in_machine": os.cpu_count(), "cgroup_cpu_quota": cpu_quota(),
+        "sample": f"{frames} full frames {w}x{h}x{spp} of the bench's orbiting camera traced on {threads} threads "
+                  f"({t_trace:.1f} s); full {len(tris)}-tri BVH built on 1 thread ({t_build:.2f} s); oracle built "
+                  f"-O3 -march=native -ffp-contract=off on this host",
         "build_mprims_per_s": len(tris) / t_build / 1e6, "build_threads": 1,
         "cpu_model": model,
         "counters_match_gpu": bool(int(cnt[0]) == int(gpu_counters[0]) and int(cnt[1]) == int(gpu_counters[1])),
@@ -251,7 +274,9 @@ def other_config(R, S, key, torch, dev, steps=8, warmup=2):
             "build_mprims_per_s": round(cfg.n / (bd * 1e-3) / 1e6, 2),
             "build_roofline_frac": round(BUILD_BYTES_PER_PRIM * cfg.n / (bd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "kernel_bytes_per_launch": kb,
-            "kernel_frac": round(kb / (tr * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            # requested bytes mostly hit L2/MALL (they can exceed the HBM peak),
+            # so they are priced against the aggregate L2 bandwidth
+            "kernel_l2_frac": round(kb / (tr * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
             "scene_variant": "splitmix64 soup (SURVEY.md §9.9)" if cfg.scene == "soup"
             else "procedural substitute (SURVEY.md §9.9; no asset files offline)"}
 
@@ -260,6 +285,11 @@ def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args))
+    # stdout carries exactly one line, the JSON result: anything else a
+    # library prints there (gloo's connection notes, RCCL banners) goes to stderr
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -353,6 +383,15 @@ def main():
     wall = time.perf_counter() - t0
     per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, gather (ms)
     rank_trace_ms = float(per[:, 1].mean())
+    if args.only_timed:  # profiler passes: the dispatches after the warm-up are the timed ones
+        if rank == 0:
+            json_out.write(json.dumps({"only_timed": True, "trace_ms_rank0": rank_trace_ms,
+                                       "build_ms_rank0": float(per[:, 0].mean())}) + "\n")
+            json_out.flush()
+        scene.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     # ---- beside the timed steps (untimed by the step contract)
     # the same moving sequence with row-major dispatch = every frame cold
@@ -434,8 +473,11 @@ def main():
                 hbm_frac = traffic / (rank_trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
             if pmc.get("valu_insts_per_launch") and pmc.get("cycles_per_launch"):
                 issue_frac = pmc["valu_insts_per_launch"] / (VALU_ISSUE_PER_CYCLE * pmc["cycles_per_launch"])
-        cands = {"memory_requests": frac, "hbm": hbm_frac, "valu_issue": issue_frac}
-        bound = max((k for k in cands if cands[k] is not None), key=lambda k: cands[k])
+        l2_frac = achieved / L2_PEAK_GBS
+        # which resource is closest to its ceiling (the contract's `bound` stays
+        # the memory roofline this integer/branchy path is priced against)
+        cands = {"hbm_requested": frac, "hbm_measured": hbm_frac, "l2_requests": l2_frac, "valu_issue": issue_frac}
+        limiter = max((k for k in cands if cands[k] is not None), key=lambda k: cands[k])
         build_gbs = BUILD_BYTES_PER_PRIM * n_tris / (build_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
@@ -477,26 +519,33 @@ def main():
                                      "total_with_stage_events": round(stage_total_ms, 4)},
             "trace_counters_rank0_static": {"nodes_fetched": int(cnt_static[0]), "tris_tested": int(cnt_static[1]),
                                             "rays": rank_rays},
-            "roofline": {"bound": bound, "kernel": "trace launch: k_tile_order + k_trace<wide>",
+            "roofline": {"bound": "hbm", "kernel": "trace launch: k_tile_order + k_trace<wide>",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(frac, 4), "traffic": traffic,
                          "bytes_per_launch": kernel_bytes,
                          "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
+                         "l2_frac": round(l2_frac, 4), "l2_peak": L2_PEAK_GBS,
                          "issue_frac": round(issue_frac, 4) if issue_frac is not None else None,
+                         "limiter": limiter,
                          "pmc_source": (os.path.relpath(args.pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]")
                          if pmc else None,
                          "algo_bytes_binary_model": algo_bytes,
-                         "note": "bytes the wide kernel requests per launch (64 B per K7w record + 48 B per "
-                                 "triangle record, its own counters, + 16 B hit + 4 B RGBA per ray) over the "
-                                 "event-timed launch; traffic = PMC HBM bytes per launch (2*FETCH_SIZE + "
-                                 "WRITE_SIZE, gfx950 correction); issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 "
-                                 "x cycles); algo_bytes_binary_model = SURVEY.md §8(d) 32/node + 36/tri + 16/ray "
-                                 "over the §9.7 binary traversal (not what this kernel fetches)"},
+                         "note": "achieved = bytes the wide kernel requests per launch (64 B per K7w record + "
+                                 "48 B per triangle record, its own counters, + 16 B hit + 4 B RGBA per ray) over "
+                                 "the event-timed launch, priced against HBM (frac) and the aggregate L2 (l2_frac: "
+                                 "every request passes L2); traffic = PMC HBM bytes per launch (2*FETCH_SIZE + "
+                                 "WRITE_SIZE, gfx950 correction), hbm_frac = traffic over the same time; "
+                                 "issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 x GRBM_GUI_ACTIVE/8); limiter = "
+                                 "the largest fraction; algo_bytes_binary_model = SURVEY.md §8(d) 32/node + 36/tri "
+                                 "+ 16/ray over the §9.7 binary traversal (not what this kernel fetches)"},
             "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM,
+                               "traffic": pmc.get("build_hbm_bytes") if pmc else None,
+                               "kernel_sum_ms": pmc.get("build_kernel_sum_ms") if pmc else None,
                                "note": "SURVEY.md §8(d) 404 B/prim over the event-timed build (launch gaps "
-                                       "included; the rocprof kernel sum is in profiles/)"},
+                                       "included); traffic = PMC HBM bytes of one build's kernels, kernel_sum_ms = "
+                                       "their rocprof durations (profiles/pmc_summary.json)"},
             "cpu_baseline": None,
         }
         # the static frame: same CRC for every N (bit-exact tiles)
@@ -512,7 +561,10 @@ def main():
                                               static_ms)
             out["path"] = path_tracing(S, scene, cfg, cam_static, w, h, spp, img, args, torch, dev)
         if world == 1 and not args.no_cpu_baseline:
-            threads = args.cpu_threads or len(os.sched_getaffinity(0))
+            # every CPU this process may run on at once: the affinity set,
+            # capped by the cgroup quota (oversubscribing a quota only adds switches)
+            q = cpu_quota()
+            threads = args.cpu_threads or max(1, min(len(os.sched_getaffinity(0)), int(q) if q else 1 << 30))
             out["cpu_baseline"] = cpu_baseline(scene.tris(), view, w, h, spp, threads, cnt_static)
     elif world > 1 and rank != 0:
         frame(cam_static)  # rank 0's CRC frame needs every rank's tiles
@@ -527,7 +579,8 @@ def main():
             except Exception as exc:  # a side measurement: never lose the headline line over it
                 out["other_configs"][f"config{key}"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        json_out.write(json.dumps(out) + "\n")
+        json_out.flush()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -13,4 +13,4 @@ tail -3 gpurun_out/t_$TAG.log
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cut -c1-600 gpurun_out/bench_$TAG.json
 timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --steps 5 --no-cpu-baseline --no-extra > gpurun_out/bench2_$TAG.json 2> gpurun_out/bench2_$TAG.err || { tail -20 gpurun_out/bench2_$TAG.err; exit 1; }
-python3 -c "import json;d=json.load(open('gpurun_out/bench2_$TAG.json'));print('N=2 gloo', d['value'], d['image_crc32'])"
+python3 -c "import json;d=json.loads(open('gpurun_out/bench2_$TAG.json').read().strip().splitlines()[-1]);print('N=2 gloo', d['value'], d['image_crc32'])"
