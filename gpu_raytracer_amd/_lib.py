@@ -40,7 +40,7 @@ EXPORTED = [
     "rt_render_shadow", "rt_render_shadow_device", "rt_render_shadow_work",
     "rt_render_path", "rt_render_path_device", "rt_render_path_work",
     "rt_bvh_prepare", "rt_bvh_device_sections", "rt_bvh_mark_built", "rt_bvh_replicas",
-    "rt_render_tiles_counters", "rt_render_tiles_work", "rt_tiles_for_rank",
+    "rt_render_tiles_counters", "rt_render_tiles_work", "rt_render_step_map", "rt_tiles_for_rank",
     "rt_render_tiles_device", "rt_unpack_tiles_device", "rt_scene_stream", "rt_scene_sync",
     "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_refit", "rt_stage_trace",
     "rt_stage_intersect", "rt_stage_minmax", "rt_framebuffer_dump_ppm", "rt_hits_dump",
@@ -117,6 +117,7 @@ def lib() -> C.CDLL:
         "rt_render_device": [P, cam, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_render_tiles_counters": [P, cam, u32, u32, u32, u32, u32, P],
         "rt_render_tiles_work": [P, cam, u32, u32, u32, u32, u32, P],
+        "rt_render_step_map": [P, u32, u32, u32, u32, u32, P, C.c_size_t],
         "rt_render_tiles_device": [P, cam, u32, u32, u32, u32, u32, P, P, P, C.POINTER(dbl)],
         "rt_unpack_tiles_device": [P, u32, u32, u32, u32, P, i32, P],
         "rt_scene_stream": [P, PP],

@@ -1178,6 +1178,23 @@ rt_status rt_render_tiles_work(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     return counters_impl(s, cam, w, h, spp, rank, nranks, true, false, counters_out);
 }
 
+rt_status rt_render_step_map(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
+                             uint16_t* out, size_t count) {
+    if (!s || !out || !nranks || rank >= nranks) return fail(RT_EINVAL, "bad step-map arguments");
+    Replica* r = nullptr;
+    RTR(need_built(s, &r));
+    const uint32_t key[5] = {w, h, spp, rank, nranks};
+    if (!r->sched.have_prev || std::memcmp(key, r->sched_key, sizeof(key)) != 0)
+        return fail(RT_EINVAL, "no previous frame of this shape");
+    const size_t nb = rt::tiles_for_rank(w, h, rank, nranks);
+    if (count < nb * 256) return fail(RT_EINVAL, "step map buffer too small");
+    HIPR(hipSetDevice(r->device));
+    if (r->last_stream) HIPR(hipEventSynchronize(r->last));
+    HIPR(hipStreamSynchronize(r->stream));
+    HIPR(hipMemcpy(out, r->sched.px_prev, nb * 256 * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
 rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, void* d_hits,
                            void* d_rgba, void* stream, double* ms_out) {
     if (!s || !cam) return fail(RT_EINVAL, "bad render arguments");

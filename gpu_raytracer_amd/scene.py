@@ -278,6 +278,14 @@ class Scene:
         call("rt_render_tiles_work", self._h, C.byref(cam), w, h, spp, rank, nranks, _p(c))
         return c
 
+    def step_map(self, w, h, spp=1, rank=0, nranks=1) -> np.ndarray:
+        """Per-pixel wide-traversal step counts of the previous full frame of
+        this shape, tile-slot-major (rt_render_step_map)."""
+        nb = tiles_for_rank(w, h, rank, nranks)
+        out = np.zeros(nb * 256, np.uint16)
+        call("rt_render_step_map", self._h, w, h, spp, rank, nranks, _p(out), out.size)
+        return out
+
     def render_tiles_device(self, cam, w, h, spp, rank, nranks, d_rgba: int, d_hits: int = 0,
                             stream: int = 0, timed: bool = False):
         ms = C.c_double()

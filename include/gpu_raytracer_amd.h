@@ -207,6 +207,13 @@ rt_status rt_render_tiles_counters(rt_scene* s, const rt_camera* cam, uint32_t w
 /* the trace kernel's own fetches for `rank`'s tiles (rt_render_work's counters) */
 rt_status rt_render_tiles_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                                uint32_t rank, uint32_t nranks, uint64_t counters_out[2]);
+/* diagnostics: per-pixel wide-traversal step counts of the previous frame of
+ * this shape (w, h, spp, rank, nranks), tile-slot-major (256 per 16x16 tile
+ * slot, local pixel ly*16+lx; a ray finished by the binary hand-off is
+ * charged 64 extra).  Written by the full-frame primary kernel only (the
+ * trace.px_sort path); RT_EINVAL without such a frame. */
+rt_status rt_render_step_map(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
+                             uint16_t* out, size_t count);
 /* Unpack nranks gathered slabs (each tiles_per_slab*1024 B, slab r = rank r)
  * into a w*h*4 device image. */
 rt_status rt_unpack_tiles_device(const void* d_slabs, uint32_t tiles_per_slab, uint32_t w,
