@@ -536,19 +536,24 @@ rt_status rt_camera_look_at(const double eye[3], const double at[3], const doubl
                             uint32_t w, uint32_t h, rt_camera* out) {
     if (!eye || !at || !up || !out || !w || !h) return fail(RT_EINVAL, "bad camera arguments");
     double f[3] = {at[0] - eye[0], at[1] - eye[1], at[2] - eye[2]};
+    // a degenerate frame (eye == at, up parallel to the view direction,
+    // non-finite inputs) has no basis: refused rather than NaN rays
     auto norm = [](double* v) {
         const double l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+        if (!(l > 0.0) || !std::isfinite(l)) return false;
         v[0] /= l; v[1] /= l; v[2] /= l;
+        return true;
     };
     auto cross = [](const double* a, const double* b, double* o) {
         o[0] = a[1] * b[2] - a[2] * b[1];
         o[1] = a[2] * b[0] - a[0] * b[2];
         o[2] = a[0] * b[1] - a[1] * b[0];
     };
-    norm(f);
+    if (!(vfov_deg > 0.0 && vfov_deg < 180.0)) return fail(RT_EINVAL, "camera: vfov outside (0, 180)");
+    if (!norm(f)) return fail(RT_EINVAL, "camera: eye == at or non-finite");
     double r[3], u[3];
     cross(f, up, r);
-    norm(r);
+    if (!norm(r)) return fail(RT_EINVAL, "camera: up parallel to the view direction");
     cross(r, f, u);
     const double th = std::tan(vfov_deg * 3.14159265358979323846 / 360.0);
     const double aspect = (double)w / (double)h;
