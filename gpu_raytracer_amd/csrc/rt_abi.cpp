@@ -334,9 +334,15 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
     const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     const uint32_t key[5] = {w, h, spp, rank, nranks};
     const bool same = std::memcmp(key, r.sched_key, sizeof(key)) == 0;
-    // [order][cost A][cost B] u32, [px A][px B] u16 x 256 per tile slot
-    const size_t need = 3ull * nb * 4 + 2ull * nb * 512;
-    if (!same || r.order_cap < need) {
+    // [order][cost A][cost B] u32, [px A][px B] u16 x 256 per tile slot,
+    // then (trace.coop_cap) 2 queue counters and the heavy-ray queue
+    const rt::TraceConfig cfg = rt::config_snapshot();
+    // (64 shards of equal size, 2 x 64 counters)
+    const uint32_t qcap = (cfg.coop_cap || cfg.coop_cap_tiles) ? (cfg.coop_max + 63u) & ~63u : 0u;
+    const size_t maps = 3ull * nb * 4 + 2ull * nb * 512;
+    const size_t qoff = (maps + 255) & ~size_t(255);
+    const size_t need = qcap ? qoff + 512 + 32ull * qcap : maps;
+    if (!same || r.order_cap < need || r.sched.coop_qcap != qcap) {
         std::memset(r.sched_key, 0, sizeof(r.sched_key));  // invalid until the maps exist
         RTR(grow(&r.d_order, &r.order_cap, need));
         uint32_t* b = static_cast<uint32_t*>(r.d_order);
@@ -345,6 +351,12 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
         r.sched.cost_cur = b + 2 * nb;
         r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 3 * nb);
         r.sched.px_cur = r.sched.px_prev + (size_t)nb * 256;
+        char* qb = static_cast<char*>(r.d_order) + qoff;
+        r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(qb) : nullptr;
+        r.sched.coop_q = qcap ? reinterpret_cast<uint4*>(qb + 512) : nullptr;
+        r.sched.coop_qcap = qcap;
+        r.sched.coop_par = 0;
+        r.sched.coop_fresh = true;
         r.sched.have_prev = false;
         r.sched.fresh = true;
         std::memcpy(r.sched_key, key, sizeof(key));
@@ -408,6 +420,9 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "path.batch" && value >= 0 && value <= (1 << 28)) c.path_batch = (uint32_t)value;
     else if (k == "render.emulate" && (value == 0 || value == 1)) c.render_emulate = (uint32_t)value;
     else if (k == "render.rccl1" && (value == 0 || value == 1)) c.render_rccl1 = (uint32_t)value;
+    else if (k == "trace.coop_cap" && value >= 0 && value <= (1 << 20)) c.coop_cap = (uint32_t)value;
+    else if (k == "trace.coop_cap_tiles" && value >= 0 && value <= (1 << 20)) c.coop_cap_tiles = (uint32_t)value;
+    else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
     else return false;
     return true;
 }
@@ -1153,8 +1168,12 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     RTR(join_caller_work(*r));
     if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
     HIPR(hipMemsetAsync(r->d_ctr, 0, 16, r->stream));
+    // the kernels' own work counters include the heavy-ray queue's pass when
+    // it is on (trace.coop_cap*), which needs the frame shape's queue
+    rt::TileSched* sched = nullptr;
+    if (!binary) RTR(sched_for(*r, w, h, spp, rank, nranks, &sched));
     hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
-                                    nranks, packed, nullptr, nullptr, r->d_ctr, binary, r->d_work, nullptr, r->stream);
+                                    nranks, packed, nullptr, nullptr, r->d_ctr, binary, r->d_work, sched, r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(r->stream));
     HIPR(hipMemcpy(counters_out, r->d_ctr, 16, hipMemcpyDeviceToHost));

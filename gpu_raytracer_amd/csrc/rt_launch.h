@@ -99,6 +99,10 @@ struct TraceConfig {
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
     uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
+    uint32_t coop_cap = 0;        // primary full frames: rays past this many wide steps finish in k_trace_coop
+                                  // (one wave per ray); 0 = off
+    uint32_t coop_cap_tiles = 96; // the same for one rank's tiles of a multi-GPU frame (tools/coop_sweep.py)
+    uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };
 
@@ -109,6 +113,11 @@ struct TileSched {
     uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
     uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
     uint16_t* px_cur = nullptr;     // [nb][256] this frame's
+    uint4* coop_q = nullptr;        // [coop_qcap][2] heavy-ray queue (trace.coop_cap)
+    uint32_t* coop_ctr = nullptr;   // [2] queue counters, alternating frames
+    uint32_t coop_qcap = 0;
+    uint32_t coop_par = 0;          // which counter this frame uses
+    bool coop_fresh = true;         // queue (re)allocated: zero both counters before the first launch
     bool have_prev = false;
     bool fresh = true;              // maps (re)allocated: clear both before the first launch
 };

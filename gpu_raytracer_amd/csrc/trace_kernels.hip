@@ -509,6 +509,42 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
     return s_perm[tid];
 }
 
+// Heavy-ray queue (trace.coop_cap, DESIGN.md "Cooperative heavy rays"): a
+// primary ray still traversing after coop_cap wide steps stops, and its
+// pixel -- from that sample on, with the colour sums of the samples before
+// it -- is queued for k_trace_coop, which traces it with a whole wave.
+// 32-B entries {x, y, first sample, output pixel index} {r, g, b, 0}, in
+// kCoopShards shards of `cap` entries, each with its own reservation counter
+// (wave gw reserves in shard gw mod kCoopShards): tens of thousands of
+// returning atomics on ONE device-scope counter serialise (~10 ns each, a
+// full-frame pass 1 went 0.33 -> 0.42 ms), spread over 64 they do not.  A
+// counter may pass `cap`: lanes that find their shard full go on tracing.
+constexpr uint32_t kCoopShards = 64;
+struct CoopQ {
+    uint4* q = nullptr;
+    uint32_t* ctr = nullptr;       // [kCoopShards] this frame's reservation counters
+    uint32_t* ctr_next = nullptr;  // [kCoopShards] the next frame's, zeroed by k_trace_coop
+    uint32_t cap = 0;              // entries per shard
+};
+
+// Called by the lanes that reach the step cap in this step (divergent): one
+// atomic per wave reserves their entries.  Returns 3 (deferred) with the
+// entry index, or 0 (shard full: keep tracing).
+__device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t& qslot) {
+    const uint64_t mm = __ballot(1);
+    const uint32_t leader = (uint32_t)__builtin_ctzll(mm);
+    const uint32_t sh = gw & (kCoopShards - 1);
+    uint32_t base = 0;
+    if (__lane_id() == leader) base = atomicAdd(cq.ctr + sh, (uint32_t)__popcll(mm));
+    base = __builtin_amdgcn_readlane(base, leader);
+    const uint32_t p = base + lanes_below(mm);
+    if (p < cq.cap) {
+        qslot = sh * cq.cap + p;
+        return 3;
+    }
+    return 0;
+}
+
 template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false>
 __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
@@ -520,7 +556,8 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                                const uint32_t* __restrict__ order = nullptr,
                                                uint32_t* __restrict__ cost_out = nullptr,
                                                const uint16_t* __restrict__ px_prev = nullptr,
-                                               uint16_t* __restrict__ px_cost = nullptr) {
+                                               uint16_t* __restrict__ px_cost = nullptr,
+                                               uint32_t coop_cap = 0, CoopQ cq = CoopQ{}) {
     __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
     // tile slot from the block id: consecutive tiles go to different XCDs
@@ -551,6 +588,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
     uint32_t cn = 0, ct = 0, steps = 0;
+    uint32_t qslot = 0, dsamp = RT_SENT;  // heavy-ray queue entry, deferred sample
     const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
 #ifdef RT_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
@@ -576,15 +614,23 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                 wray_init(cam.eye, d, R);
                 int st = R.fin ? 0 : 2;
                 const char* nd = reinterpret_cast<const char*>(nodes);
-                while (st == 0) st = wide_step<COUNT, NT, false, PACKED || SHADOW>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
-                                                          s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct);
+                while (st == 0) {
+                    st = wide_step<COUNT, NT, false, PACKED || SHADOW>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
+                                                                      s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct);
+                    if (!SHADOW && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
+                }
+                if (PX) steps += R.steps;
+                if (st == 3) {  // heavy: k_trace_coop finishes this pixel from sample s on
+                    dsamp = s;
+                    break;
+                }
                 if (st == 2) {
                     if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
                     trace_ray_from<COUNT>(nd, tri_s, n, cam.eye, d, R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1),
                                           R.tb, R.hu, R.hv, R.hp, cn, ct);
                 }
                 tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
-                if (PX) steps += R.steps + (st == 2 ? 64u : 0u);  // a binary finish: a nominal charge
+                if (PX && st == 2) steps += 64u;  // a binary finish: a nominal charge
             } else {
                 trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
             }
@@ -613,10 +659,13 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                 r = r + 0.0f; g = g + 0.0f; b = b + 0.0f;
             }
         }
-        if (rgba) {
+        const uint32_t pi = PACKED ? slot * 256 + ly * 16 + lx : y * W + x;
+        if (dsamp != RT_SENT) {
+            cq.q[2 * (uint64_t)qslot] = make_uint4(x, y, dsamp, pi);
+            cq.q[2 * (uint64_t)qslot + 1] = make_uint4(__float_as_uint(r), __float_as_uint(g), __float_as_uint(b), 0u);
+        } else if (rgba) {
             const float sc = 1.0f / (float)spp;
             const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
-            const uint64_t pi = PACKED ? (uint64_t)slot * 256 + ly * 16 + lx : (uint64_t)y * W + x;
             rgba[pi] = px;
         }
     }
@@ -658,6 +707,245 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
         atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
     }
 }
+
+// ------------------------------------------------------ cooperative heavy rays
+// DESIGN.md "Cooperative heavy rays".  One wave traces one queued ray: a
+// frame's (or one rank's share's) duration is set by its slowest wave, and
+// the slowest waves hold rays that need 100-250 dependent record fetches
+// (rays grazing the soup, whose §9.7 preorder enters far subtrees while tb
+// is still infinite).  Here the ray's pending subtrees form a frontier list
+// in preorder (an LDS stack, head on top), and each step the wave takes the
+// first m <= 64 entries at once: a record entry is fetched and its children
+// tested against the current tb (pushed in order), a leaf entry's triangle
+// is fetched and tested (exact leaf box + Moller-Trumbore) and becomes a
+// "resolved" entry carrying (tn, t, u, v).  Resolved entries are folded
+// into (tb, hit) only when they reach the head, i.e. in preorder, by §9.7's
+// leaf rule: accept iff tn <= tb && t < tb, then tb = t.
+//
+// Why this is exactly §9.7.  §9.7's result is the fold over all leaves in
+// preorder of that leaf rule (a box test on an ancestor passes whenever it
+// passes on the contained leaf box: the monotonicity argument of wide_step),
+// and the rule is monotone in tb: a leaf it rejects at some tb it rejects at
+// every smaller tb.  Our tb at any moment is the fold over a preorder prefix
+// of the leaves before every pending entry, so it is >= §9.7's tb at that
+// entry's position: culling records (conservative quantized tn > tb) and
+// dropping leaves that fail the rule at our tb only removes leaves §9.7
+// rejects too, and every leaf §9.7 might accept is folded in preorder with
+// §9.7's own tb.  A frontier that would overflow hands over to the binary
+// traversal from its head entry with the current tb (every leaf before the
+// head in preorder is folded: the hand-off of wide_step).
+constexpr uint32_t kCoopCap = 256;          // frontier entries per ray
+constexpr uint32_t kCoopRes = 0x40000000u;  // frontier entry: resolved leaf (kWideLeaf | kCoopRes | k)
+constexpr uint32_t kCoopWaves = 4;          // rays (waves) per 256-thread block
+constexpr uint32_t kCoopGrid = 2048;        // persistent blocks: 8 per CU (LDS-bound), one round
+
+struct CoopLds {
+    uint32_t ref[kCoopCap];
+    float tn[kCoopCap], t[kCoopCap], u[kCoopCap], v[kCoopCap];
+};
+
+__device__ __forceinline__ float readlane_f(float x, uint32_t l) {
+    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(x), l));
+}
+
+// Whole wave, one ray (o, d uniform), 1/d finite on every axis.  hp = prim.
+template <bool COUNT>
+__device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                           const float4* __restrict__ tri_s, uint32_t n, const float* o,
+                                           const float* d, CoopLds& L, float& tb_out, float& hu_out, float& hv_out,
+                                           uint32_t& hp_out, uint32_t& cn, uint32_t& ct) {
+    const uint32_t lane = __lane_id();
+    WRay R;
+    wray_init(o, d, R);
+    float tb = __builtin_inff(), hu = 0.0f, hv = 0.0f;
+    uint32_t hk = RT_SENT;  // tri_s slot of the current best (its prim is read at the end)
+    if (lane == 0) {
+        L.ref[0] = 0u;  // the root record
+        L.tn[0] = 0.0f;
+    }
+    __builtin_amdgcn_wave_barrier();
+    uint32_t sp = 1;
+    const uint32_t limit = 4 * n + 16;
+    bool handoff = false;
+    for (uint32_t guard = 0; sp > 0; ++guard) {
+        uint32_t m = min(64u, sp);
+        if (sp + 3 * m > kCoopCap) m = (kCoopCap - sp) / 3;  // a record adds at most 3 entries
+        if (m == 0 || guard > limit) {
+            handoff = true;
+            break;
+        }
+        const bool act = lane < m;
+        uint32_t ref = 0u;
+        float etn = 0.0f, et = 0.0f, eu = 0.0f, ev = 0.0f;
+        if (act) {
+            const uint32_t pos = sp - 1 - lane;
+            ref = L.ref[pos]; etn = L.tn[pos]; et = L.t[pos]; eu = L.u[pos]; ev = L.v[pos];
+        }
+        __builtin_amdgcn_wave_barrier();
+        __asm__ volatile("" ::: "memory");
+        const bool res = (ref & kCoopRes) != 0u;
+        // 1. fold the head run of resolved leaves, in preorder
+        const uint64_t nonres = __ballot(act && !res);
+        const uint32_t j = nonres ? (uint32_t)__builtin_ctzll(nonres) : m;
+        int last = -1;
+        for (;;) {
+            const uint64_t cm = __ballot((int)lane > last && lane < j && tb >= etn && tb > et);
+            if (!cm) break;
+            last = (int)__builtin_ctzll(cm);
+            tb = readlane_f(et, (uint32_t)last);
+            hu = readlane_f(eu, (uint32_t)last);
+            hv = readlane_f(ev, (uint32_t)last);
+            hk = __builtin_amdgcn_readlane(ref, (uint32_t)last) & ~(kWideLeaf | kCoopRes);
+        }
+        // 2. expand entries j..m-1 against the folded tb
+        R.tb = tb;
+        bool h[4] = {false, false, false, false};
+        uint32_t cref[4] = {ref, 0u, 0u, 0u};
+        float ctn[4] = {etn, 0.0f, 0.0f, 0.0f};
+        if (act && lane >= j && etn <= tb) {
+            if (res) {
+                h[0] = true;  // not at the head yet: stays pending
+            } else if (ref & kWideLeaf) {
+                if (COUNT) ++ct;
+                const float4* tp = tri_s + (uint64_t)(ref & ~kWideLeaf) * 3;
+                const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
+                const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
+                float lo[3], hi[3], tn;
+                tri_bounds(tv, lo, hi);
+                float t, u, v;
+                if (slab_hit(lo, hi, o, R.invd, tb, tn) && intersect_tri(o, d, tv, tb, t, u, v)) {
+                    h[0] = true;
+                    cref[0] = ref | kCoopRes;
+                    ctn[0] = tn;
+                    et = t; eu = u; ev = v;
+                }
+            } else {
+                if (COUNT) ++cn;
+                const uint4* wp = wnodes + (uint64_t)ref * 4;
+                const uint4 w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3];
+                float tn[4];
+                const bool wild = record_test(R, o, w0, w1, w2, h, tn);
+                const uint32_t flags = w0.w >> 24;
+                cref[0] = w2.z; cref[1] = w2.w; cref[2] = w3.x; cref[3] = w3.y;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    h[i] = ((flags >> (4 + i)) & 1u) && (h[i] || wild);
+                    ctn[i] = wild ? 0.0f : tn[i];
+                }
+            }
+        }
+        // 3. the outputs in preorder (lane order, then child order) replace
+        // the m entries taken: output g lands at spn - 1 - g
+        const uint32_t c = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
+        const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
+        const uint32_t pre = lanes_below(b0) + 2u * lanes_below(b1) + 4u * lanes_below(b2);
+        const uint32_t total = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+        const uint32_t spn = sp - m + total;
+        uint32_t g = pre;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (h[i]) {
+                const uint32_t p = spn - 1 - g;
+                L.ref[p] = cref[i];
+                L.tn[p] = ctn[i];
+                if (i == 0) { L.t[p] = et; L.u[p] = eu; L.v[p] = ev; }
+                ++g;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __asm__ volatile("" ::: "memory");
+        sp = spn;
+    }
+    uint32_t hp = hk == RT_SENT ? RT_SENT : __float_as_uint(tri_s[(uint64_t)hk * 3 + 2].y);
+    if (handoff) {
+        if (lane == 0) {
+            const uint32_t head = sp ? L.ref[sp - 1] & ~kCoopRes : RT_SENT;
+            trace_ray_from<COUNT>(nodes, tri_s, n, o, d, head == RT_SENT ? RT_SENT : bin_of(head, n - 1), tb, hu,
+                                  hv, hp, cn, ct);
+        }
+        tb = readlane_f(tb, 0); hu = readlane_f(hu, 0); hv = readlane_f(hv, 0);
+        hp = __builtin_amdgcn_readlane(hp, 0);
+    }
+    tb_out = tb; hu_out = hu; hv_out = hv; hp_out = hp;
+}
+
+// Pass 2 of a primary frame with trace.coop_cap: the queued heavy pixels,
+// one wave each (kCoopWaves per block, a persistent grid striding over the
+// queue), from the queued sample on; writes their hits and RGBA exactly as
+// k_trace would.  Block 0 zeroes the next frame's queue counter.
+template <bool COUNT, bool PACKED>
+__global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                                    const float4* __restrict__ tri_s, uint32_t n, Cam cam,
+                                                    uint32_t W, uint32_t spp, CoopQ cq, float4* __restrict__ hits,
+                                                    uint32_t* __restrict__ rgba,
+                                                    unsigned long long* __restrict__ counters) {
+    __shared__ CoopLds s_l[kCoopWaves];
+    static_assert(kCoopShards == 64, "one shard per lane");
+    if (blockIdx.x == 0 && threadIdx.x < kCoopShards) cq.ctr_next[threadIdx.x] = 0u;
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    // the shards' filled lengths and their exclusive prefix, lane k = shard k
+    const uint32_t len = min(cq.ctr[lane], cq.cap);
+    uint32_t incl = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    const uint32_t excl = incl - len;
+    const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
+    uint32_t cn = 0, ct = 0;
+    for (uint32_t e = blockIdx.x * kCoopWaves + wv; e < cnt; e += gridDim.x * kCoopWaves) {
+        // queued ray e lives in the last shard whose prefix is <= e
+        const uint64_t le = __ballot(excl <= e && len > 0);
+        const uint32_t sh = 63u - (uint32_t)__builtin_clzll(le);
+        const uint32_t slot = sh * cq.cap + (e - __builtin_amdgcn_readlane(excl, sh));
+        const uint4 a = cq.q[2 * (uint64_t)slot], b = cq.q[2 * (uint64_t)slot + 1];
+        const uint32_t x = a.x, y = a.y, pi = a.w;
+        float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
+        for (uint32_t s = a.z; s < spp; ++s) {
+            const uint32_t sidx = (y * W + x) * spp + s;
+            float jx = 0.5f, jy = 0.5f;
+            if (s > 0) {
+                const uint32_t hh = pcg_hash(sidx);
+                jx = (float)(hh >> 8) * 0x1p-24f;
+                jy = (float)(pcg_hash(hh) >> 8) * 0x1p-24f;
+            }
+            const float px = (float)x + jx, py = (float)y + jy;
+            float d[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+            float tb, hu, hv;
+            uint32_t hp;
+            coop_trace<COUNT>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[wv], tb, hu, hv,
+                              hp, cn, ct);
+            if (hits && lane == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
+            if (hp != RT_SENT) {
+                r = r + hu;
+                g = g + hv;
+                bl = bl + ((1.0f - hu) - hv);
+            } else {
+                r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
+            }
+        }
+        if (rgba && lane == 0) {
+            const float sc = 1.0f / (float)spp;
+            rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
+        }
+    }
+    if (COUNT) {
+        unsigned long long a = cn, bs = ct;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            a += __shfl_xor(a, o, 64);
+            bs += __shfl_xor(bs, o, 64);
+        }
+        if (lane == 0 && (a || bs)) {
+            atomicAdd(&counters[0], a);
+            atomicAdd(&counters[1], bs);
+        }
+    }
+}
+
 
 // ---------------------------------------------------------------- path mode
 // Path mode [SPEC, DESIGN.md "Path mode"; SURVEY.md §8(f) row 3]: per
@@ -1436,10 +1724,24 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         if (sched->have_prev) px_prev = sched->px_prev;
         px_cost = sched->px_cur;
     }
+    // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
+    const uint32_t coop_cap = wide && sched && sched->coop_q ? (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) : 0u;
+    CoopQ cq;
+    if (coop_cap) {
+        if (sched->coop_fresh) {
+            hipError_t me = hipMemsetAsync(sched->coop_ctr, 0, 2 * kCoopShards * sizeof(uint32_t), s);
+            if (me != hipSuccess) return me;
+            sched->coop_fresh = false;
+        }
+        cq.q = sched->coop_q;
+        cq.ctr = sched->coop_ctr + sched->coop_par * kCoopShards;
+        cq.ctr_next = sched->coop_ctr + (sched->coop_par ^ 1u) * kCoopShards;
+        cq.cap = sched->coop_qcap / kCoopShards;
+    }
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
     hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
                        cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, cost_out, \
-                       px_prev, px_cost)
+                       px_prev, px_cost, coop_cap, cq)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \
@@ -1456,6 +1758,20 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
 #undef RT_TRACE_W
 #undef RT_TRACE
 #undef RT_TRACE_NT
+    if (coop_cap) {
+        hipError_t le = hipGetLastError();
+        if (le != hipSuccess) return le;
+#define RT_COOP(C, P)                                                                                                \
+    hipLaunchKernelGGL((k_trace_coop<C, P>), dim3(kCoopGrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, spp, \
+                       cq, H, R, counters)
+        if (counters) {
+            if (packed) RT_COOP(true, true); else RT_COOP(true, false);
+        } else {
+            if (packed) RT_COOP(false, true); else RT_COOP(false, false);
+        }
+#undef RT_COOP
+        sched->coop_par ^= 1u;
+    }
     return hipGetLastError();
 }
 

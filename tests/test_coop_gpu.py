@@ -1,0 +1,159 @@
+"""Cooperative heavy rays (trace.coop_cap / trace.coop_cap_tiles, DESIGN.md
+"Cooperative heavy rays"): primary rays still traversing after the cap are
+queued and finished by k_trace_coop, one wave per ray, folding the leaves in
+§9.7 preorder.  Every frame must stay bit-identical to the CPU oracle (hits
+and RGBA) whatever the cap, the queue capacity (a full queue leaves rays to
+their own lane), the samples per pixel (a pixel resumes at its deferred
+sample with the colour sums of the earlier ones), the full-frame and the
+per-rank tiled kernels, successive frames (tile/pixel order on), and the
+frontier hand-off to the binary traversal (a scene of identical triangles,
+whose boxes all overlap, overflows the 256-entry frontier)."""
+import numpy as np
+import pytest
+
+from conftest import bits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R(rt):
+    if rt.device_count() < 1:
+        pytest.fail("no GPU visible to librtamd")
+    return rt
+
+
+@pytest.fixture()
+def cfg(R):
+    keys = []
+
+    def set_(k, v, default):
+        keys.append((k, default))
+        R.config_set(k, v)
+    yield set_
+    for k, d in reversed(keys):
+        R.config_set(k, d)
+
+
+def _frame(oracle, tris, view, w, h, spp):
+    exp = oracle.build(tris)
+    cam = oracle.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    eh, _ = oracle.trace(exp["nodes"], tris, cam, w, h, spp)
+    return eh, oracle.shade(eh, w, h, spp)
+
+
+def _same_hits(a, b):
+    return all(np.array_equal(bits(a[k]), bits(b[k])) for k in ("t", "u", "v", "prim"))
+
+
+def _soup_view():
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    return SOUP_VIEW
+
+
+@pytest.mark.parametrize("cap", [1, 2, 5, 16, 40])
+@pytest.mark.parametrize("spp", [1, 3])
+def test_coop_full_frame(R, oracle, cfg, cap, spp):
+    V = _soup_view()
+    tris = oracle.soup(40000, 11).reshape(-1, 9)
+    w, h = 200, 120
+    eh, er = _frame(oracle, tris, V, w, h, spp)
+    cfg("trace.coop_cap", cap, 0)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for frame in range(3):  # frames 2 and 3 also run the tile and pixel order
+            hits, rgba, _ = s.render(cam, w, h, spp)
+            assert np.array_equal(rgba, er), (cap, spp, frame)
+            assert _same_hits(hits, eh), (cap, spp, frame)
+
+
+def test_coop_changes_work_not_result(R, oracle, cfg):
+    """The queue really runs: the kernels' own fetch counters change with the
+    cap (the cooperative pass speculates), the image does not."""
+    V = _soup_view()
+    tris = oracle.soup(40000, 12).reshape(-1, 9)
+    w, h = 160, 96
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        base = s.render_work(cam, w, h, 1)
+        _, img0, _ = s.render(cam, w, h, 1)
+        cfg("trace.coop_cap", 2, 0)
+        coop = s.render_work(cam, w, h, 1)
+        _, img1, _ = s.render(cam, w, h, 1)
+    assert np.array_equal(img0, img1)
+    assert not np.array_equal(base, coop)
+
+
+@pytest.mark.parametrize("qmax", [1, 7, 100])
+def test_coop_queue_full(R, oracle, cfg, qmax):
+    V = _soup_view()
+    tris = oracle.soup(30000, 13).reshape(-1, 9)
+    w, h, spp = 150, 100, 2
+    eh, er = _frame(oracle, tris, V, w, h, spp)
+    cfg("trace.coop_max", qmax, 65536)
+    cfg("trace.coop_cap", 3, 0)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for frame in range(2):
+            hits, rgba, _ = s.render(cam, w, h, spp)
+            assert np.array_equal(rgba, er), (qmax, frame)
+            assert _same_hits(hits, eh), (qmax, frame)
+
+
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("cap", [2, 24])
+def test_coop_tiles(R, oracle, cfg, P, cap):
+    """One rank's tiles (packed slabs, 64-thread blocks) through the queue:
+    emulated P-rank frames == the oracle, three successive frames."""
+    V = _soup_view()
+    tris = oracle.soup(30000, 14).reshape(-1, 9)
+    w, h, spp = 170, 90, 2
+    eh, er = _frame(oracle, tris, V, w, h, spp)
+    cfg("render.emulate", 1, 0)
+    cfg("trace.coop_cap_tiles", cap, 96)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for frame in range(3):
+            hits, rgba, _ = s.render(cam, w, h, spp, ngpus=P)
+            assert np.array_equal(rgba, er), (P, cap, frame)
+            assert _same_hits(hits, eh), (P, cap, frame)
+
+
+def test_coop_frontier_handoff(R, oracle, cfg):
+    """All-overlapping boxes (600 copies of a few triangles, and a cluster):
+    the frontier outgrows its 256 entries and hands over to the binary
+    traversal from its head entry -- still the oracle's hits."""
+    base = oracle.soup(8, 21).reshape(-1, 9)
+    tris = np.concatenate([np.repeat(base, 75, axis=0), oracle.soup(2000, 22).reshape(-1, 9) * 0.05 + 0.45])
+    tris = np.ascontiguousarray(tris, np.float32)
+    V = _soup_view()
+    w, h = 96, 64
+    eh, er = _frame(oracle, tris, V, w, h, 1)
+    cfg("trace.coop_cap", 1, 0)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        hits, rgba, _ = s.render(cam, w, h, 1)
+    assert np.array_equal(rgba, er)
+    assert _same_hits(hits, eh)
+
+
+def test_coop_headline_1m(R, oracle, cfg):
+    """The soup-1M 1080p frame with the tile default cap applied to the full
+    frame (the rays past 48 wide steps, ~10 % of the frame) == the oracle."""
+    V = _soup_view()
+    tris = oracle.soup(1_000_000, 1).reshape(-1, 9)
+    w, h = 1920, 1080
+    eh, er = _frame(oracle, tris, V, w, h, 1)
+    cfg("trace.coop_cap", 48, 0)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for frame in range(2):
+            hits, rgba, _ = s.render(cam, w, h, 1)
+            assert np.array_equal(rgba, er), frame
+            assert _same_hits(hits, eh), frame
