@@ -422,6 +422,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "render.rccl1" && (value == 0 || value == 1)) c.render_rccl1 = (uint32_t)value;
     else if (k == "trace.coop_cap" && value >= 0 && value <= (1 << 20)) c.coop_cap = (uint32_t)value;
     else if (k == "trace.coop_cap_tiles" && value >= 0 && value <= (1 << 20)) c.coop_cap_tiles = (uint32_t)value;
+    else if (k == "trace.coop_lanes" && (value == 16 || value == 32 || value == 64)) c.coop_lanes = (uint32_t)value;
     else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
     else return false;
     return true;

@@ -102,6 +102,7 @@ struct TraceConfig {
     uint32_t coop_cap = 0;        // primary full frames: rays past this many wide steps finish in k_trace_coop
                                   // (one wave per ray); 0 = off
     uint32_t coop_cap_tiles = 96; // the same for one rank's tiles of a multi-GPU frame (tools/coop_sweep.py)
+    uint32_t coop_lanes = 64;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
     uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };

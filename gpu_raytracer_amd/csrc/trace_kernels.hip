@@ -709,18 +709,19 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
 }
 
 // ------------------------------------------------------ cooperative heavy rays
-// DESIGN.md "Cooperative heavy rays".  One wave traces one queued ray: a
-// frame's (or one rank's share's) duration is set by its slowest wave, and
-// the slowest waves hold rays that need 100-250 dependent record fetches
-// (rays grazing the soup, whose §9.7 preorder enters far subtrees while tb
-// is still infinite).  Here the ray's pending subtrees form a frontier list
-// in preorder (an LDS stack, head on top), and each step the wave takes the
-// first m <= 64 entries at once: a record entry is fetched and its children
-// tested against the current tb (pushed in order), a leaf entry's triangle
-// is fetched and tested (exact leaf box + Moller-Trumbore) and becomes a
-// "resolved" entry carrying (tn, t, u, v).  Resolved entries are folded
-// into (tb, hit) only when they reach the head, i.e. in preorder, by §9.7's
-// leaf rule: accept iff tn <= tb && t < tb, then tb = t.
+// DESIGN.md "Cooperative heavy rays".  A group of G lanes (16, 32 or 64:
+// trace.coop_lanes) traces one queued ray: a frame's (or one rank's
+// share's) duration is set by its slowest waves, and those hold rays that
+// need 100-250 dependent record fetches (rays grazing the soup, whose §9.7
+// preorder enters far subtrees while tb is still infinite).  Here the ray's
+// pending subtrees form a frontier list in preorder (an LDS stack per group,
+// head on top), and each step the group takes the first m <= G entries at
+// once: a record entry is fetched and its children tested against the
+// current tb (pushed in order), a leaf entry's triangle is fetched and tested
+// (exact leaf box + Moller-Trumbore) and becomes a "resolved" entry carrying
+// (tn, t, u, v).  Resolved entries are folded into (tb, hit) only when they
+// reach the head, i.e. in preorder, by §9.7's leaf rule: accept iff
+// tn <= tb && t < tb, then tb = t.
 //
 // Why this is exactly §9.7.  §9.7's result is the fold over all leaves in
 // preorder of that leaf rule (a box test on an ancestor passes whenever it
@@ -734,75 +735,104 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
 // §9.7's own tb.  A frontier that would overflow hands over to the binary
 // traversal from its head entry with the current tb (every leaf before the
 // head in preorder is folded: the hand-off of wide_step).
-constexpr uint32_t kCoopCap = 256;          // frontier entries per ray
+//
+// Groups narrower than a wave run side by side in it: every group-level
+// value (sp, m, j, tb, ...) is held identically by the group's lanes, the
+// ballots are cut to the group's bits and lane reads go through ds_bpermute
+// (__shfl) from the group's own lanes.  A finished group's lanes idle until
+// the wave's other groups are done.
 constexpr uint32_t kCoopRes = 0x40000000u;  // frontier entry: resolved leaf (kWideLeaf | kCoopRes | k)
-constexpr uint32_t kCoopWaves = 4;          // rays (waves) per 256-thread block
-constexpr uint32_t kCoopGrid = 2048;        // persistent blocks: 8 per CU (LDS-bound), one round
+constexpr uint32_t kCoopGrid = 2048;        // persistent 256-thread blocks (replaced by the resident capacity)
 
-struct CoopLds {
-    uint32_t ref[kCoopCap];
-    float tn[kCoopCap], t[kCoopCap], u[kCoopCap], v[kCoopCap];
+// frontier entries per group: a step takes m <= G entries and a record
+// entry adds at most 3, so the list needs room for the growth of a few steps
+template <int G>
+struct CoopCfg {
+    static constexpr uint32_t cap = G == 64 ? 256u : G == 32 ? 192u : 112u;
+    static constexpr uint32_t groups = 256u / G;  // per 256-thread block
 };
 
-__device__ __forceinline__ float readlane_f(float x, uint32_t l) {
-    return __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(x), l));
+template <int G>
+struct CoopLds {
+    uint32_t ref[CoopCfg<G>::cap];
+    float tn[CoopCfg<G>::cap], t[CoopCfg<G>::cap], u[CoopCfg<G>::cap], v[CoopCfg<G>::cap];
+};
+
+// this group's bits of a wave-wide ballot, shifted to bit 0
+template <int G>
+__device__ __forceinline__ uint64_t gballot(bool p, uint32_t gbase) {
+    const uint64_t b = __ballot(p);
+    if (G == 64) return b;
+    return (b >> gbase) & ((1ull << G) - 1ull);
 }
 
-// Whole wave, one ray (o, d uniform), 1/d finite on every axis.  hp = prim.
-template <bool COUNT>
+__device__ __forceinline__ float gread_f(float x, uint32_t src) {
+    return __uint_as_float((uint32_t)__shfl((int)__float_as_uint(x), (int)src, 64));
+}
+__device__ __forceinline__ uint32_t gread_u(uint32_t x, uint32_t src) {
+    return (uint32_t)__shfl((int)x, (int)src, 64);
+}
+
+// One group, one ray (o, d the same in all its lanes), 1/d finite on every
+// axis.  hp = prim.
+template <bool COUNT, int G>
 __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                            const float4* __restrict__ tri_s, uint32_t n, const float* o,
-                                           const float* d, CoopLds& L, float& tb_out, float& hu_out, float& hv_out,
-                                           uint32_t& hp_out, uint32_t& cn, uint32_t& ct) {
+                                           const float* d, CoopLds<G>& L, float& tb_out, float& hu_out,
+                                           float& hv_out, uint32_t& hp_out, uint32_t& cn, uint32_t& ct) {
+    constexpr uint32_t CAP = CoopCfg<G>::cap;
     const uint32_t lane = __lane_id();
+    const uint32_t gl = lane & (G - 1), gbase = lane & ~(uint32_t)(G - 1);
     WRay R;
     wray_init(o, d, R);
     float tb = __builtin_inff(), hu = 0.0f, hv = 0.0f;
     uint32_t hk = RT_SENT;  // tri_s slot of the current best (its prim is read at the end)
-    if (lane == 0) {
+    if (gl == 0) {
         L.ref[0] = 0u;  // the root record
         L.tn[0] = 0.0f;
     }
     __builtin_amdgcn_wave_barrier();
+    __asm__ volatile("" ::: "memory");
     uint32_t sp = 1;
     const uint32_t limit = 4 * n + 16;
     bool handoff = false;
     for (uint32_t guard = 0; sp > 0; ++guard) {
-        uint32_t m = min(64u, sp);
-        if (sp + 3 * m > kCoopCap) m = (kCoopCap - sp) / 3;  // a record adds at most 3 entries
+        uint32_t m = min((uint32_t)G, sp);
+        if (sp + 3 * m > CAP) m = (CAP - sp) / 3;  // a record adds at most 3 entries
         if (m == 0 || guard > limit) {
             handoff = true;
             break;
         }
-        const bool act = lane < m;
+        const bool act = gl < m;
         uint32_t ref = 0u;
         float etn = 0.0f, et = 0.0f, eu = 0.0f, ev = 0.0f;
         if (act) {
-            const uint32_t pos = sp - 1 - lane;
+            const uint32_t pos = sp - 1 - gl;
             ref = L.ref[pos]; etn = L.tn[pos]; et = L.t[pos]; eu = L.u[pos]; ev = L.v[pos];
         }
         __builtin_amdgcn_wave_barrier();
         __asm__ volatile("" ::: "memory");
         const bool res = (ref & kCoopRes) != 0u;
         // 1. fold the head run of resolved leaves, in preorder
-        const uint64_t nonres = __ballot(act && !res);
+        const uint64_t nonres = gballot<G>(act && !res, gbase);
         const uint32_t j = nonres ? (uint32_t)__builtin_ctzll(nonres) : m;
         int last = -1;
         for (;;) {
-            const uint64_t cm = __ballot((int)lane > last && lane < j && tb >= etn && tb > et);
+            const uint64_t cm = gballot<G>((int)gl > last && gl < j && tb >= etn && tb > et, gbase);
             if (!cm) break;
             last = (int)__builtin_ctzll(cm);
-            tb = readlane_f(et, (uint32_t)last);
-            hu = readlane_f(eu, (uint32_t)last);
-            hv = readlane_f(ev, (uint32_t)last);
-            hk = __builtin_amdgcn_readlane(ref, (uint32_t)last) & ~(kWideLeaf | kCoopRes);
+            const uint32_t src = gbase + (uint32_t)last;
+            tb = gread_f(et, src);
+            hu = gread_f(eu, src);
+            hv = gread_f(ev, src);
+            hk = gread_u(ref, src) & ~(kWideLeaf | kCoopRes);
         }
         // 2. expand entries j..m-1 against the folded tb
         R.tb = tb;
         bool h[4] = {false, false, false, false};
         uint32_t cref[4] = {ref, 0u, 0u, 0u};
         float ctn[4] = {etn, 0.0f, 0.0f, 0.0f};
-        if (act && lane >= j && etn <= tb) {
+        if (act && gl >= j && etn <= tb) {
             if (res) {
                 h[0] = true;  // not at the head yet: stays pending
             } else if (ref & kWideLeaf) {
@@ -837,8 +867,10 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
         // 3. the outputs in preorder (lane order, then child order) replace
         // the m entries taken: output g lands at spn - 1 - g
         const uint32_t c = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
-        const uint64_t b0 = __ballot(c & 1u), b1 = __ballot(c & 2u), b2 = __ballot(c & 4u);
-        const uint32_t pre = lanes_below(b0) + 2u * lanes_below(b1) + 4u * lanes_below(b2);
+        const uint64_t b0 = gballot<G>(c & 1u, gbase), b1 = gballot<G>(c & 2u, gbase), b2 = gballot<G>(c & 4u, gbase);
+        const uint64_t below = (1ull << gl) - 1ull;
+        const uint32_t pre = (uint32_t)__popcll(b0 & below) + 2u * (uint32_t)__popcll(b1 & below) +
+                             4u * (uint32_t)__popcll(b2 & below);
         const uint32_t total = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
         const uint32_t spn = sp - m + total;
         uint32_t g = pre;
@@ -858,31 +890,32 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
     }
     uint32_t hp = hk == RT_SENT ? RT_SENT : __float_as_uint(tri_s[(uint64_t)hk * 3 + 2].y);
     if (handoff) {
-        if (lane == 0) {
+        if (gl == 0) {
             const uint32_t head = sp ? L.ref[sp - 1] & ~kCoopRes : RT_SENT;
             trace_ray_from<COUNT>(nodes, tri_s, n, o, d, head == RT_SENT ? RT_SENT : bin_of(head, n - 1), tb, hu,
                                   hv, hp, cn, ct);
         }
-        tb = readlane_f(tb, 0); hu = readlane_f(hu, 0); hv = readlane_f(hv, 0);
-        hp = __builtin_amdgcn_readlane(hp, 0);
+        tb = gread_f(tb, gbase); hu = gread_f(hu, gbase); hv = gread_f(hv, gbase);
+        hp = gread_u(hp, gbase);
     }
     tb_out = tb; hu_out = hu; hv_out = hv; hp_out = hp;
 }
 
-// Pass 2 of a primary frame with trace.coop_cap: the queued heavy pixels,
-// one wave each (kCoopWaves per block, a persistent grid striding over the
-// queue), from the queued sample on; writes their hits and RGBA exactly as
-// k_trace would.  Block 0 zeroes the next frame's queue counter.
-template <bool COUNT, bool PACKED>
+// Pass 2 of a primary frame with trace.coop_cap*: the queued heavy pixels,
+// one group of G lanes each (a persistent grid striding over the queue), from
+// the queued sample on; writes their hits and RGBA exactly as k_trace would.
+// Block 0 zeroes the next frame's queue counters.
+template <bool COUNT, bool PACKED, int G>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
                                                     uint32_t W, uint32_t spp, CoopQ cq, float4* __restrict__ hits,
                                                     uint32_t* __restrict__ rgba,
                                                     unsigned long long* __restrict__ counters) {
-    __shared__ CoopLds s_l[kCoopWaves];
+    constexpr uint32_t NG = CoopCfg<G>::groups;
+    __shared__ CoopLds<G> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
     if (blockIdx.x == 0 && threadIdx.x < kCoopShards) cq.ctr_next[threadIdx.x] = 0u;
-    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63, grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
     // the shards' filled lengths and their exclusive prefix, lane k = shard k
     const uint32_t len = min(cq.ctr[lane], cq.cap);
     uint32_t incl = len;
@@ -891,14 +924,25 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
         const uint32_t y = __shfl_up(incl, o, 64);
         if (lane >= (uint32_t)o) incl += y;
     }
-    const uint32_t excl = incl - len;
+    // the shard table goes through LDS: inside the divergent loop below the
+    // lanes of finished groups are inactive, and a lane read (readlane or a
+    // shuffle) of a value the compiler computes there would see stale lanes
+    __shared__ uint32_t s_excl[kCoopShards], s_len[kCoopShards];
+    if (threadIdx.x < 64) {
+        s_excl[lane] = incl - len;
+        s_len[lane] = len;
+    }
+    __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
     uint32_t cn = 0, ct = 0;
-    for (uint32_t e = blockIdx.x * kCoopWaves + wv; e < cnt; e += gridDim.x * kCoopWaves) {
-        // queued ray e lives in the last shard whose prefix is <= e
-        const uint64_t le = __ballot(excl <= e && len > 0);
-        const uint32_t sh = 63u - (uint32_t)__builtin_clzll(le);
-        const uint32_t slot = sh * cq.cap + (e - __builtin_amdgcn_readlane(excl, sh));
+    for (uint32_t e = blockIdx.x * NG + grp; e < cnt; e += gridDim.x * NG) {
+        // queued ray e lives in the last non-empty shard whose prefix is <= e
+        uint32_t sh = 0, sbase = 0;
+        for (uint32_t k = 0; k < 64; ++k) {
+            const uint32_t ek = s_excl[k];
+            if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
+        }
+        const uint32_t slot = sh * cq.cap + (e - sbase);
         const uint4 a = cq.q[2 * (uint64_t)slot], b = cq.q[2 * (uint64_t)slot + 1];
         const uint32_t x = a.x, y = a.y, pi = a.w;
         float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
@@ -916,9 +960,9 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
             for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
             float tb, hu, hv;
             uint32_t hp;
-            coop_trace<COUNT>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[wv], tb, hu, hv,
-                              hp, cn, ct);
-            if (hits && lane == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
+            coop_trace<COUNT, G>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp], tb,
+                                 hu, hv, hp, cn, ct);
+            if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
             if (hp != RT_SENT) {
                 r = r + hu;
                 g = g + hv;
@@ -927,7 +971,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                 r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
             }
         }
-        if (rgba && lane == 0) {
+        if (rgba && gl == 0) {
             const float sc = 1.0f / (float)spp;
             rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
         }
@@ -1761,15 +1805,42 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     if (coop_cap) {
         hipError_t le = hipGetLastError();
         if (le != hipSuccess) return le;
-#define RT_COOP(C, P)                                                                                                \
-    hipLaunchKernelGGL((k_trace_coop<C, P>), dim3(kCoopGrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, spp, \
+        uint32_t cgrid = kCoopGrid;
+        {  // persistent grid = the resident capacity (per device and group width, computed once)
+            static std::atomic<uint32_t> resident[kMaxDevices][3];
+            int dev = 0;
+            hipError_t e = hipGetDevice(&dev);
+            if (e != hipSuccess) return e;
+            if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+            const int gi = cfg.coop_lanes == 16 ? 0 : cfg.coop_lanes == 32 ? 1 : 2;
+            uint32_t r = resident[dev][gi].load(std::memory_order_relaxed);
+            if (!r) {
+                int per_cu = 0, cus = 0;
+                const void* kf = gi == 0 ? reinterpret_cast<const void*>(k_trace_coop<false, false, 16>)
+                               : gi == 1 ? reinterpret_cast<const void*>(k_trace_coop<false, false, 32>)
+                                         : reinterpret_cast<const void*>(k_trace_coop<false, false, 64>);
+                if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 256, 0)) != hipSuccess) return e;
+                if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+                    return e;
+                r = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
+                resident[dev][gi].store(r, std::memory_order_relaxed);
+            }
+            cgrid = r;
+        }
+#define RT_COOP_G(C, P, G)                                                                                         \
+    hipLaunchKernelGGL((k_trace_coop<C, P, G>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, spp, \
                        cq, H, R, counters)
+#define RT_COOP(C, P)                                       \
+    if (cfg.coop_lanes == 16) RT_COOP_G(C, P, 16);          \
+    else if (cfg.coop_lanes == 32) RT_COOP_G(C, P, 32);     \
+    else RT_COOP_G(C, P, 64)
         if (counters) {
             if (packed) RT_COOP(true, true); else RT_COOP(true, false);
         } else {
             if (packed) RT_COOP(false, true); else RT_COOP(false, false);
         }
 #undef RT_COOP
+#undef RT_COOP_G
         sched->coop_par ^= 1u;
     }
     return hipGetLastError();

@@ -1,13 +1,13 @@
 """Cooperative heavy rays (trace.coop_cap / trace.coop_cap_tiles, DESIGN.md
 "Cooperative heavy rays"): primary rays still traversing after the cap are
-queued and finished by k_trace_coop, one wave per ray, folding the leaves in
+queued and finished by k_trace_coop, a group of 16/32/64 lanes per ray, folding the leaves in
 §9.7 preorder.  Every frame must stay bit-identical to the CPU oracle (hits
 and RGBA) whatever the cap, the queue capacity (a full queue leaves rays to
 their own lane), the samples per pixel (a pixel resumes at its deferred
 sample with the colour sums of the earlier ones), the full-frame and the
 per-rank tiled kernels, successive frames (tile/pixel order on), and the
 frontier hand-off to the binary traversal (a scene of identical triangles,
-whose boxes all overlap, overflows the 256-entry frontier)."""
+whose boxes all overlap, overflows the frontier)."""
 import numpy as np
 import pytest
 
@@ -51,14 +51,16 @@ def _soup_view():
     return SOUP_VIEW
 
 
+@pytest.mark.parametrize("lanes", [16, 32, 64])
 @pytest.mark.parametrize("cap", [1, 2, 5, 16, 40])
 @pytest.mark.parametrize("spp", [1, 3])
-def test_coop_full_frame(R, oracle, cfg, cap, spp):
+def test_coop_full_frame(R, oracle, cfg, cap, spp, lanes):
     V = _soup_view()
     tris = oracle.soup(40000, 11).reshape(-1, 9)
     w, h = 200, 120
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("trace.coop_cap", cap, 0)
+    cfg("trace.coop_lanes", lanes, 64)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -103,9 +105,10 @@ def test_coop_queue_full(R, oracle, cfg, qmax):
             assert _same_hits(hits, eh), (qmax, frame)
 
 
+@pytest.mark.parametrize("lanes", [16, 64])
 @pytest.mark.parametrize("P", [2, 3, 8])
 @pytest.mark.parametrize("cap", [2, 24])
-def test_coop_tiles(R, oracle, cfg, P, cap):
+def test_coop_tiles(R, oracle, cfg, P, cap, lanes):
     """One rank's tiles (packed slabs, 64-thread blocks) through the queue:
     emulated P-rank frames == the oracle, three successive frames."""
     V = _soup_view()
@@ -114,6 +117,7 @@ def test_coop_tiles(R, oracle, cfg, P, cap):
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("render.emulate", 1, 0)
     cfg("trace.coop_cap_tiles", cap, 96)
+    cfg("trace.coop_lanes", lanes, 64)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -123,7 +127,8 @@ def test_coop_tiles(R, oracle, cfg, P, cap):
             assert _same_hits(hits, eh), (P, cap, frame)
 
 
-def test_coop_frontier_handoff(R, oracle, cfg):
+@pytest.mark.parametrize("lanes", [16, 32, 64])
+def test_coop_frontier_handoff(R, oracle, cfg, lanes):
     """All-overlapping boxes (600 copies of a few triangles, and a cluster):
     the frontier outgrows its 256 entries and hands over to the binary
     traversal from its head entry -- still the oracle's hits."""
@@ -134,6 +139,7 @@ def test_coop_frontier_handoff(R, oracle, cfg):
     w, h = 96, 64
     eh, er = _frame(oracle, tris, V, w, h, 1)
     cfg("trace.coop_cap", 1, 0)
+    cfg("trace.coop_lanes", lanes, 64)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
