@@ -299,6 +299,7 @@ def main():
     import torch
     import torch.distributed as dist
     import gpu_raytracer_amd as R
+    from gpu_raytracer_amd import _lib as L
     from gpu_raytracer_amd import dist as D
     from gpu_raytracer_amd import scenes as S
 
@@ -460,6 +461,39 @@ def main():
         except Exception as exc:  # a measurement only: never fail the bench line over it
             bvh_exchange = {"error": f"{type(exc).__name__}: {exc}"[:200]}
 
+    # the distributed build (rt_dbuild_* phases, Morton-
+    # prefix all-to-all, share gathers) timed next to the replicated build;
+    # its BVH must equal the replicated one bit for bit (checked on device).
+    dbuild = None
+    if world > 1:
+        try:
+            dms, info = [], None
+            for i in range(4):
+                barrier()
+                tb0 = time.perf_counter()
+                info = D.distributed_build(D.LibStages(scene, dev), D.Exchange(stage=args.dist_backend == "gloo"))
+                barrier()
+                if i:
+                    dms.append((time.perf_counter() - tb0) * 1e3)
+                if i == 0:  # the distributed build's sections (sorted keys/indices, nodes, wide records)
+                    st = D.LibStages(scene, dev)
+                    got = {k: st.buf(k).clone() for k in (L.RT_DB_KEYS, L.RT_DB_VALS, L.RT_DB_NODES, L.RT_DB_WIDE)}
+            scene.build()  # the replicated build again: must give the same bytes
+            st = D.LibStages(scene, dev)
+            same = all(torch.equal(st.buf(k), got[k]) for k in got)
+            rdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+            t = torch.tensor([float(np.median(dms)), 0.0 if same else 1.0, float(info["bytes_in"])],
+                             dtype=torch.float64, device=rdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dbuild = {"distributed_build_ms": round(float(t[0].item()), 4), "replicated_build_ms": round(build_ms, 4),
+                      "bit_identical": bool(t[1].item() == 0.0), "bytes_in_max_rank": int(t[2].item()),
+                      "crossing_nodes": info["crossing"],
+                      "exchange": "RCCL (all_to_all_single, broadcasts)" if args.dist_backend == "nccl"
+                      else "gloo staged through host (rehearsal)",
+                      "used": "replicated build (every rank builds; DESIGN.md 'Distributed build')"}
+        except Exception as exc:  # a measurement only: never fail the bench line over it
+            dbuild = {"error": f"{type(exc).__name__}: {exc}"[:200]}
+
     out = None
     if rank == 0:
         value = rays / ((trace_ms + gather_ms) * 1e-3) / 1e6
@@ -512,6 +546,7 @@ def main():
                            "trace_ms_static_ordered": round(static_ms, 4),
                            "gain_moving": round(cold_ms / trace_ms, 4)},
             "bvh_exchange": bvh_exchange,
+            "distributed_build": dbuild,
             "frame_mrays_per_s": round(rays / (wall / args.steps) / 1e6, 2),
             "build_stages_ms_last": {"bounds": round(stimes.bounds, 4), "morton": round(stimes.morton, 4),
                                      "sort": round(stimes.sort, 4), "topology": round(stimes.topology, 4),

@@ -45,7 +45,12 @@ EXPORTED = [
     "rt_stage_bounds", "rt_stage_morton", "rt_stage_sort", "rt_stage_topology", "rt_stage_refit", "rt_stage_trace",
     "rt_stage_intersect", "rt_stage_minmax", "rt_framebuffer_dump_ppm", "rt_hits_dump",
     "rt_config_set", "rt_last_error", "rt_device_count", "rt_version",
+    "rt_dbuild_shares", "rt_dbuild_bounds", "rt_dbuild_keys", "rt_dbuild_sort", "rt_dbuild_subtrees",
+    "rt_dbuild_merge", "rt_dbuild_buffer",
 ]
+# rt_dbuild_buffer selectors (include/gpu_raytracer_amd.h)
+(RT_DB_SEND_KEYS, RT_DB_SEND_VALS, RT_DB_RECV_KEYS, RT_DB_RECV_VALS, RT_DB_KEYS, RT_DB_VALS, RT_DB_NODES,
+ RT_DB_TRI_S, RT_DB_WIDE, RT_DB_TOPO, RT_DB_PRE, RT_DB_SUF, RT_DB_TOTALS, RT_DB_CROSS, RT_DB_CROSS_ALL) = range(15)
 
 
 class RtError(RuntimeError):
@@ -133,6 +138,13 @@ def lib() -> C.CDLL:
         "rt_framebuffer_dump_ppm": [P, u32, u32, C.c_char_p],
         "rt_hits_dump": [P, C.c_size_t, C.c_char_p],
         "rt_config_set": [C.c_char_p, C.c_int64],
+        "rt_dbuild_shares": [u32, u32, u32, P],
+        "rt_dbuild_bounds": [P, u32, u32, P],
+        "rt_dbuild_keys": [P, u32, u32, P, P],
+        "rt_dbuild_sort": [P, u32],
+        "rt_dbuild_subtrees": [P, u32, u32, C.POINTER(u32)],
+        "rt_dbuild_merge": [P, u32],
+        "rt_dbuild_buffer": [P, i32, PP, C.POINTER(u64)],
     }
     for name, args in sig.items():
         f = getattr(L, name)

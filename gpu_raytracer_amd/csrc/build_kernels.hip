@@ -182,7 +182,8 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
                                                          const float* __restrict__ partials, uint32_t nb,
                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                          uint32_t* __restrict__ ghist /* [4][256] */,
-                                                         uint32_t* __restrict__ counts0 /* [tile][256] */) {
+                                                         uint32_t* __restrict__ counts0 /* [tile][256] */,
+                                                         uint32_t vbase = 0 /* vals = vbase + index */) {
     __shared__ uint32_t hist[4 * 256];
     __shared__ float red[kSortThreads / 64][6];
     for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) hist[j] = 0u;
@@ -212,12 +213,13 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
         uint4* vp = reinterpret_cast<uint4*>(vals + first);
         kp[0] = make_uint4(k8[0], k8[1], k8[2], k8[3]);
         kp[1] = make_uint4(k8[4], k8[5], k8[6], k8[7]);
-        vp[0] = make_uint4(first, first + 1, first + 2, first + 3);
-        vp[1] = make_uint4(first + 4, first + 5, first + 6, first + 7);
+        const uint32_t v = vbase + first;
+        vp[0] = make_uint4(v, v + 1, v + 2, v + 3);
+        vp[1] = make_uint4(v + 4, v + 5, v + 6, v + 7);
     } else {
 #pragma unroll
         for (uint32_t q = 0; q < kTrisPerThread; ++q)
-            if (q < cnt) { keys[first + q] = k8[q]; vals[first + q] = first + q; }
+            if (q < cnt) { keys[first + q] = k8[q]; vals[first + q] = vbase + first + q; }
     }
     __syncthreads();
 #pragma unroll
@@ -311,8 +313,9 @@ __device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint3
 
 // Stage the sorted keys [B - KW, B + NT + KW) of a block of NT threads.
 template <int NT, int KW>
-__device__ __forceinline__ KeyWin stage_keys(const uint32_t* __restrict__ keys_g, uint32_t n, uint32_t* s_keys) {
-    const int64_t B = (int64_t)blockIdx.x * NT;
+__device__ __forceinline__ KeyWin stage_keys(const uint32_t* __restrict__ keys_g, uint32_t n, uint32_t* s_keys,
+                                             uint32_t block = blockIdx.x) {
+    const int64_t B = (int64_t)block * NT;
     const int64_t wlo = B - KW < 0 ? 0 : B - KW;
     const int64_t whi = B + NT + KW > (int64_t)n ? (int64_t)n : B + NT + KW;
     for (int64_t j = wlo + threadIdx.x; j < whi; j += NT) s_keys[j - wlo] = keys_g[j];
@@ -339,8 +342,10 @@ __device__ __forceinline__ uint4 karras_finish(const KeyWin& keys, int64_t N, in
     else esc = (uint32_t)(L0 + mx + 1);
     const uint4 tp = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
     topo[i] = tp;
-    parent[left] = (uint32_t)i;
-    parent[right] = (uint32_t)i;
+    if (parent) {
+        parent[left] = (uint32_t)i;
+        parent[right] = (uint32_t)i;
+    }
     return tp;
 }
 
@@ -370,7 +375,7 @@ __device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafT
                                                  Aabb& box, bool allow_defer, bool& deferred) {
     const int64_t i = i32, N = n;
     const uint32_t L0 = n - 1;
-    if (i32 == 0) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
+    if (i32 == 0 && parent) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
     uint32_t lesc;
     tp_out = make_uint4(0, 0, 0, 0);
     deferred = false;
@@ -711,7 +716,8 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         float* __restrict__ prebuf, float* __restrict__ sufbuf,
                                                         float* __restrict__ totals, uint32_t* __restrict__ cross,
                                                         uint32_t* cross_ctr, uint32_t cross_cap,
-                                                        uint4* __restrict__ wnodes, uint32_t collapse) {
+                                                        uint4* __restrict__ wnodes, uint32_t collapse,
+                                                        uint32_t block0 = 0) {
     constexpr int T = kRefitT, NW = T / 64, KW = 1024;
     static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
     static_assert(sizeof(uint4) <= sizeof(Aabb), "topology words must fit the table buffer");
@@ -722,7 +728,8 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
 
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t L0 = n - 1;
-    const uint32_t B0 = blockIdx.x * (uint32_t)T;
+    const uint32_t gb = blockIdx.x + block0;  // global refit block (a rank's share starts at block0)
+    const uint32_t B0 = gb * (uint32_t)T;
     const uint32_t B1 = (n - B0) < (uint32_t)T ? n : B0 + (uint32_t)T;
     const uint32_t k = B0 + tid;
     const bool valid = k < B1;
@@ -736,7 +743,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         // the gather is issued after the key staging: before it, the staging's
         // wait (vmcnt is in order) would also wait for the random gather
         const uint32_t prim = valid ? svals[k] : 0u;  // coalesced, with the window loads
-        const KeyWin keys = stage_keys<T, KW>(keys_g, n, reinterpret_cast<uint32_t*>(s_tab));
+        const KeyWin keys = stage_keys<T, KW>(keys_g, n, reinterpret_cast<uint32_t*>(s_tab), gb);
         RT_STAMP(1);
         LeafTri lt;
         if (valid) lt = gather_leaf(prim, tris);
@@ -764,7 +771,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         const bool need_pre = (has_int && tp.w == k && tp.z < B0) || (k == n - 1 && B0 > 0);
         if (need_suf) store_aabb(sufbuf, k, suf);
         if (need_pre) store_aabb(prebuf, k, pre);
-        if (k == B1 - 1) store_aabb(totals, blockIdx.x, pre);
+        if (k == B1 - 1) store_aabb(totals, gb, pre);
         if (has_int && (tp.z < B0 || tp.w >= B1)) cslot = atomicAdd(&s_ncross, 1u);  // LDS
     }
     __syncthreads();
@@ -774,7 +781,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
     // issued here, consumed after the sweep, so its latency overlaps it
     uint32_t cbase = 0;
     if (tid == 0 && s_ncross)
-        cbase = (blockIdx.x % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[blockIdx.x % kCrossShards], s_ncross);
+        cbase = (gb % kCrossShards) * cross_cap + atomicAdd(&cross_ctr[gb % kCrossShards], s_ncross);
     // ---- 3. sparse-table sweep: level kk holds T_kk[j] = U leaves [j, j + 2^kk),
     // odd levels in s_tab, even ones in s_box[T, 2T) (ping-pong: one barrier
     // per level); a node's box waits in registers until the sweep is over
@@ -1073,9 +1080,9 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
 static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, hipStream_t s) {
     if (!n) return hipSuccess;
     const uint32_t m = cdiv(n, kRefitT);
-    hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo, b.parent,
-                       b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr, cross_cap(m),
-                       b.wnodes, wide_collapse);
+    hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
+                       (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
+                       cross_cap(m), b.wnodes, wide_collapse, 0u);
     return hipGetLastError();
 }
 
@@ -1085,6 +1092,72 @@ hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
     if (e != hipSuccess) return e;
     if ((e = launch_topo_local(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
     return n ? launch_cross(b, n, cfg.wide_collapse, s) : hipSuccess;
+}
+
+// ------------------------------------------- distributed build
+// The per-rank device phases of rt_dbuild_* (DESIGN.md "Distributed build");
+// the exchanges between them are the caller's.  Every phase runs the build's
+// own kernels on a slice or a block range, so each value it produces is the
+// one the single-GPU build computes.
+
+// centroid bounds of tris[lo, lo + cnt) -> b.params (lo, hi; inv of the slice)
+hipError_t launch_dbuild_bounds(const BuildBufs& b, uint32_t lo, uint32_t cnt, hipStream_t s) {
+    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(cnt)), dim3(256), 0, s, b.tris + (uint64_t)lo * 9, cnt, b.partials,
+                       (uint32_t*)nullptr, 0u);
+    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, bounds_grid(cnt), b.params);
+    return hipGetLastError();
+}
+
+// Morton codes of tris[lo, lo + cnt) against the global bounds reduced from
+// every rank's box (boxes: nboxes x {lo[3], hi[3]}, device) into
+// keys[1]/vals[1] (vals = global indices), and the [1024] top-10-bit bucket
+// histogram into ghist (the caller then sorts the slice: launch_dbuild_sort).
+hipError_t launch_dbuild_keys(const BuildBufs& b, uint32_t lo, uint32_t cnt, const float* boxes, uint32_t nboxes,
+                              hipStream_t s) {
+    uint32_t* ghist = b.zero + kZHist;
+    hipError_t e = hipMemsetAsync(ghist, 0, 1024 * 4, s);
+    if (e != hipSuccess) return e;
+    // block 0 also stores the global lo/hi/inv into params (rt_bvh_read)
+    hipLaunchKernelGGL(k_morton<true>, dim3(std::max(1u, sort_tiles(cnt))), dim3(kSortThreads), 0, s,
+                       b.tris + (uint64_t)lo * 9, cnt, b.params, boxes, nboxes, b.keys[1], b.vals[1], ghist, b.counts,
+                       lo);
+    return hipGetLastError();
+}
+
+// stable LSB sort of keys[0]/vals[0][0, cnt) (scratch keys[1]/vals[1]); the
+// digit histograms go to ghist/counts (their previous contents are dead)
+hipError_t launch_dbuild_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t cnt, const BuildBufs& b, hipStream_t s) {
+    if (cnt <= 1) return hipSuccess;
+    uint32_t* ghist = b.zero + kZHist;
+    hipError_t e = hipMemsetAsync(ghist, 0, 1024 * 4, s);
+    if (e != hipSuccess) return e;
+    const uint64_t cs = (uint64_t)sort_tiles(b.cap_n ? b.cap_n : 1) * 256;
+    uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
+    if ((e = launch_digit_hist(keys[0], cnt, ghist, s)) != hipSuccess) return e;
+    if ((e = launch_tile_hist0(keys[0], cnt, counts[0], s)) != hipSuccess) return e;
+    return launch_sort(keys, vals, cnt, ghist, counts, s);
+}
+
+// K4 + K5 + K6-local + K7w-local over refit blocks [block0, block0 + nblocks)
+// of the full sorted keys/vals in keys[0]/vals[0]
+hipError_t launch_dbuild_subtrees(const BuildBufs& b, uint32_t n, uint32_t block0, uint32_t nblocks, hipStream_t s) {
+    const TraceConfig cfg = config_snapshot();
+    hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
+    if (e != hipSuccess || !n || !nblocks) return e;
+    const uint32_t m = cdiv(n, kRefitT);
+    hipLaunchKernelGGL(k_topo_refit, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
+                       (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
+                       cross_cap(m), b.wnodes, cfg.wide_collapse, block0);
+    return hipGetLastError();
+}
+
+uint32_t dbuild_cross_cap(uint32_t n) { return cross_cap(cdiv(n ? n : 1, kRefitT)); }
+uint32_t refit_blocks(uint32_t n) { return n ? cdiv(n, kRefitT) : 0u; }
+
+// K6t + K7w of every crossing node, with the crossing list and counters
+// (b.cross / zero + kZCrossCtr) and every share's blocks in place
+hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s) {
+    return n ? launch_cross(b, n, config_snapshot().wide_collapse, s) : hipSuccess;
 }
 
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages) {

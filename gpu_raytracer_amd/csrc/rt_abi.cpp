@@ -22,6 +22,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <limits>
 #include <vector>
 
 namespace rtio {
@@ -32,6 +33,9 @@ void soup_generate(uint32_t n, uint64_t seed, float* tris);
 }  // namespace rtio
 
 namespace {
+
+constexpr uint32_t kMaxDbuildRanks = 64;             // rt_dbuild_*: ranks of one distributed build
+constexpr uint32_t kRefitLeaves = (uint32_t)rt::kRefitT;  // leaves per refit block (a share is whole blocks)
 
 // One device's copy of a scene's BVH plus that device's render scratch.
 struct Replica {
@@ -71,6 +75,13 @@ struct Replica {
     // are written and read in launch order.
     hipEvent_t last = nullptr;
     hipStream_t last_stream = nullptr;  // stream `last` was recorded on (nullptr: none)
+    // distributed build (rt_dbuild_*): pair scratch and the crossing lists
+    uint32_t* dk[2] = {nullptr, nullptr};
+    uint32_t* dv[2] = {nullptr, nullptr};
+    uint32_t* dcross = nullptr;      // this rank's crossing nodes, compacted
+    uint32_t* dcross_all = nullptr;  // every rank's (gathered by the caller)
+    float* dboxes = nullptr;         // every rank's centroid box
+    uint32_t d_n = 0;                // n the scratch was sized for (0: none)
 };
 
 // RCCL communicators of one device list (rt_render(ngpus > 1)).
@@ -212,7 +223,8 @@ void replica_free(Replica& r) {
     rt::free_build(r.bufs);
     rt::free_path(r.path);
     for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.d_order, r.d_slab, r.d_slab_hits, r.d_recv,
-                    r.d_recv_hits})
+                    r.d_recv_hits, (void*)r.dk[0], (void*)r.dk[1], (void*)r.dv[0], (void*)r.dv[1], (void*)r.dcross,
+                    (void*)r.dcross_all, (void*)r.dboxes})
         if (p) (void)hipFree(p);
     for (auto& e : r.ev.e) (void)hipEventDestroy(e);
     (void)hipEventDestroy(r.r0);
@@ -636,7 +648,27 @@ rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* keys, uint32_
     if (nodes && tot) HIPR(hipMemcpy(nodes, r->bufs.nodes, tot * 32, hipMemcpyDeviceToHost));
     if (keys && n) HIPR(hipMemcpy(keys, r->bufs.keys[0], n * 4, hipMemcpyDeviceToHost));
     if (vals && n) HIPR(hipMemcpy(vals, r->bufs.vals[0], n * 4, hipMemcpyDeviceToHost));
-    if (parent && tot) HIPR(hipMemcpy(parent, r->bufs.parent, tot * 4, hipMemcpyDeviceToHost));
+    if (parent && tot) {
+        // derived here from the nodes (the build does not write parents:
+        // nothing on the trace path reads them): the children of internal
+        // node i are a = left and the left child's escape link (a left
+        // child's escape is its right sibling, §9.6)
+        std::vector<rt_node> nd;
+        const rt_node* np = nodes;
+        if (!np) {
+            nd.resize(tot);
+            HIPR(hipMemcpy(nd.data(), r->bufs.nodes, tot * 32, hipMemcpyDeviceToHost));
+            np = nd.data();
+        }
+        std::fill(parent, parent + tot, RT_SENTINEL);
+        for (size_t i = 0; i + 1 < n; ++i) {
+            const uint32_t a = np[i].a;
+            if (a >= tot) continue;  // malformed: leave the sentinel
+            const uint32_t b = np[a].esc;
+            parent[a] = (uint32_t)i;
+            if (b < tot) parent[b] = (uint32_t)i;
+        }
+    }
     if (bounds9) HIPR(hipMemcpy(bounds9, r->bufs.params, 9 * 4, hipMemcpyDeviceToHost));
     return RT_OK;
 }
@@ -667,14 +699,14 @@ rt_status rt_bvh_replicas(const rt_scene* s, uint32_t max, int* devices, uint32_
 // RTBVH1: "RTBVH1\0\0", u32 version, u32 n, u64 FNV-1a hash of the n*36
 // triangle bytes, u64 layout tag, then the device buffers the trace and
 // rt_bvh_read use, in order: BuildParams (64 B), sorted keys and vals (n x 4),
-// nodes ((2n-1) x 32), parent ((2n-1) x 4), tri_s (n x 48), wide records
-// ((n-1) x 64).  The tag changes whenever one of those layouts does.
+// nodes ((2n-1) x 32), tri_s (n x 48), wide records ((n-1) x 64).  The tag
+// changes whenever one of those layouts does (revision 2: no parent section).
 }  // extern "C"
 
 namespace {
 const char kBvhMagic[8] = {'R', 'T', 'B', 'V', 'H', '1', 0, 0};
 constexpr uint32_t kBvhVersion = 1;
-constexpr uint64_t kBvhLayout = 0x7274616d64000001ull;  // "rtamd" + layout revision 1
+constexpr uint64_t kBvhLayout = 0x7274616d64000002ull;  // "rtamd" + layout revision 2
 
 uint64_t fnv1a(const void* p, size_t bytes) {
     const unsigned char* b = static_cast<const unsigned char*>(p);
@@ -698,7 +730,6 @@ std::vector<BvhSection> bvh_sections(const rt_scene* s, const Replica& r) {
             {r.bufs.keys[0], n * 4},
             {r.bufs.vals[0], n * 4},
             {r.bufs.nodes, tot * 32},
-            {r.bufs.parent, tot * 4},
             {r.bufs.tri_s, n * 48},
             {r.bufs.wnodes, n >= 2 ? (n - 1) * 64 : 0}};
 }
@@ -1493,6 +1524,185 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path) {
     bool ok = std::fwrite(hits, sizeof(rt_hit), count, f) == count;
     if (std::fclose(f) != 0) ok = false;
     return ok ? RT_OK : fail(RT_EIO, std::string("write failed: ") + path);
+}
+
+// ------------------------------------------------------- distributed build
+// SURVEY.md §8(f) row 4; DESIGN.md "Distributed build".  SPMD over P ranks:
+// every rank holds the whole soup (a scene), runs these phases on its own
+// share and moves the bytes between them itself (gpu_raytracer_amd/dist.py:
+// torch.distributed over RCCL, or gloo).  Each phase runs the single-GPU
+// build's own kernels on a slice of triangles or a range of refit blocks, so
+// every rank ends with the BVH rt_bvh_build makes, bit for bit.
+
+rt_status rt_dbuild_shares(uint32_t n, uint32_t rank, uint32_t nranks, uint32_t out[6]) {
+    if (!out || !nranks || rank >= nranks) return fail(RT_EINVAL, "bad arguments");
+    const uint32_t m = rt::refit_blocks(n);
+    out[0] = (uint32_t)((uint64_t)n * rank / nranks);
+    out[1] = (uint32_t)((uint64_t)n * (rank + 1) / nranks);
+    out[2] = (uint32_t)((uint64_t)m * rank / nranks);
+    out[3] = (uint32_t)((uint64_t)m * (rank + 1) / nranks);
+    out[4] = std::min<uint64_t>((uint64_t)out[2] * kRefitLeaves, n);
+    out[5] = std::min<uint64_t>((uint64_t)out[3] * kRefitLeaves, n);
+    return RT_OK;
+}
+
+namespace {
+rt_status dbuild_replica(rt_scene* s, uint32_t rank, uint32_t nranks, Replica** out) {
+    if (!s || !nranks || rank >= nranks || nranks > kMaxDbuildRanks) return fail(RT_EINVAL, "bad rank / nranks");
+    Replica* r = nullptr;
+    RTR(primary(s, &r));
+    RTR(upload(s, *r));
+    HIPR(hipSetDevice(r->device));
+    RTR(join_caller_work(*r));
+    if (r->d_n != s->n || !r->dboxes) {
+        const size_t n4 = (size_t)(s->n ? s->n : 1) * 4;
+        const size_t cc = (size_t)rt::dbuild_cross_cap(s->n) * rt::kCrossShards * 4;
+        for (uint32_t** p : {&r->dk[0], &r->dk[1], &r->dv[0], &r->dv[1], &r->dcross, &r->dcross_all})
+            if (*p) { (void)hipFree(*p); *p = nullptr; }
+        if (r->dboxes) { (void)hipFree(r->dboxes); r->dboxes = nullptr; }
+        r->d_n = 0;
+        for (uint32_t** p : {&r->dk[0], &r->dk[1], &r->dv[0], &r->dv[1]}) {
+            hipError_t e = hipMalloc((void**)p, n4);
+            if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "hipMalloc");
+        }
+        for (uint32_t** p : {&r->dcross, &r->dcross_all}) {
+            hipError_t e = hipMalloc((void**)p, cc);
+            if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "hipMalloc");
+        }
+        hipError_t e = hipMalloc((void**)&r->dboxes, kMaxDbuildRanks * 6 * sizeof(float));
+        if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "hipMalloc");
+        r->d_n = s->n;
+    }
+    *out = r;
+    return RT_OK;
+}
+}  // namespace
+
+rt_status rt_dbuild_bounds(rt_scene* s, uint32_t rank, uint32_t nranks, float box_out[6]) {
+    if (!box_out) return fail(RT_EINVAL, "null argument");
+    Replica* r = nullptr;
+    RTR(dbuild_replica(s, rank, nranks, &r));
+    r->built = false;  // the BVH is rewritten from here on
+    uint32_t sh[6];
+    RTR(rt_dbuild_shares(s->n, rank, nranks, sh));
+    if (sh[1] > sh[0]) {
+        HIPR(rt::launch_dbuild_bounds(r->bufs, sh[0], sh[1] - sh[0], r->stream));
+        HIPR(hipMemcpyAsync(box_out, r->bufs.params, 6 * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+        HIPR(hipStreamSynchronize(r->stream));
+    } else {  // an empty slice: the identity of min/max
+        for (int c = 0; c < 3; ++c) {
+            box_out[c] = std::numeric_limits<float>::infinity();
+            box_out[3 + c] = -std::numeric_limits<float>::infinity();
+        }
+    }
+    return RT_OK;
+}
+
+rt_status rt_dbuild_keys(rt_scene* s, uint32_t rank, uint32_t nranks, const float* boxes, uint32_t hist_out[1024]) {
+    if (!boxes || !hist_out) return fail(RT_EINVAL, "null argument");
+    Replica* r = nullptr;
+    RTR(dbuild_replica(s, rank, nranks, &r));
+    uint32_t sh[6];
+    RTR(rt_dbuild_shares(s->n, rank, nranks, sh));
+    const uint32_t cnt = sh[1] - sh[0];
+    HIPR(hipMemcpyAsync(r->dboxes, boxes, (size_t)nranks * 6 * sizeof(float), hipMemcpyHostToDevice, r->stream));
+    HIPR(rt::launch_dbuild_keys(r->bufs, sh[0], cnt, r->dboxes, nranks, r->stream));
+    HIPR(hipMemcpyAsync(hist_out, r->bufs.zero + rt::kZHist, 1024 * 4, hipMemcpyDeviceToHost, r->stream));
+    HIPR(hipStreamSynchronize(r->stream));
+    // the slice sorted by (key, index): grouped by bucket, hence by destination
+    uint32_t* K[2] = {r->bufs.keys[1], r->dk[0]};
+    uint32_t* V[2] = {r->bufs.vals[1], r->dv[0]};
+    HIPR(rt::launch_dbuild_sort(K, V, cnt, r->bufs, r->stream));
+    HIPR(hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+rt_status rt_dbuild_sort(rt_scene* s, uint32_t count) {
+    if (!s || count > s->n) return fail(RT_EINVAL, "bad arguments");
+    if (s->reps.empty() || !s->reps[0]->d_n) return fail(RT_EINVAL, "rt_dbuild_keys first");
+    Replica* r = s->reps[0].get();
+    HIPR(hipSetDevice(r->device));
+    uint32_t* K[2] = {r->dk[1], r->dk[0]};
+    uint32_t* V[2] = {r->dv[1], r->dv[0]};
+    HIPR(rt::launch_dbuild_sort(K, V, count, r->bufs, r->stream));
+    HIPR(hipStreamSynchronize(r->stream));
+    return RT_OK;
+}
+
+rt_status rt_dbuild_subtrees(rt_scene* s, uint32_t rank, uint32_t nranks, uint32_t* ncross_out) {
+    if (!ncross_out) return fail(RT_EINVAL, "null argument");
+    Replica* r = nullptr;
+    RTR(dbuild_replica(s, rank, nranks, &r));
+    uint32_t sh[6];
+    RTR(rt_dbuild_shares(s->n, rank, nranks, sh));
+    HIPR(rt::launch_dbuild_subtrees(r->bufs, s->n, sh[2], sh[3] - sh[2], r->stream));
+    uint32_t ctr[rt::kCrossShards];
+    HIPR(hipMemcpyAsync(ctr, r->bufs.zero + rt::kZCrossCtr, sizeof(ctr), hipMemcpyDeviceToHost, r->stream));
+    HIPR(hipStreamSynchronize(r->stream));
+    // compact the sharded list into dcross
+    const uint32_t cap = rt::dbuild_cross_cap(s->n);
+    uint32_t tot = 0;
+    for (uint32_t j = 0; j < rt::kCrossShards; ++j) {
+        if (ctr[j] > cap) return fail(RT_EDEVICE, "crossing list overflow");
+        if (ctr[j])
+            HIPR(hipMemcpyAsync(r->dcross + tot, r->bufs.cross + (size_t)j * cap, ctr[j] * 4, hipMemcpyDeviceToDevice,
+                                r->stream));
+        tot += ctr[j];
+    }
+    HIPR(hipStreamSynchronize(r->stream));
+    *ncross_out = tot;
+    return RT_OK;
+}
+
+rt_status rt_dbuild_merge(rt_scene* s, uint32_t ncross_total) {
+    if (!s) return fail(RT_EINVAL, "null scene");
+    if (s->reps.empty() || !s->reps[0]->d_n) return fail(RT_EINVAL, "rt_dbuild_subtrees first");
+    Replica* r = s->reps[0].get();
+    HIPR(hipSetDevice(r->device));
+    const uint32_t cap = rt::dbuild_cross_cap(s->n);
+    if (ncross_total > cap * rt::kCrossShards) return fail(RT_EINVAL, "ncross_total exceeds the crossing-list capacity");
+    // the gathered list (dcross_all) dealt into the build's shards
+    uint32_t ctr[rt::kCrossShards] = {};
+    uint32_t done = 0;
+    for (uint32_t j = 0; j < rt::kCrossShards && done < ncross_total; ++j) {
+        ctr[j] = std::min(cap, ncross_total - done);
+        HIPR(hipMemcpyAsync(r->bufs.cross + (size_t)j * cap, r->dcross_all + done, ctr[j] * 4, hipMemcpyDeviceToDevice,
+                            r->stream));
+        done += ctr[j];
+    }
+    HIPR(hipMemcpyAsync(r->bufs.zero + rt::kZCrossCtr, ctr, sizeof(ctr), hipMemcpyHostToDevice, r->stream));
+    HIPR(rt::launch_dbuild_merge(r->bufs, s->n, r->stream));
+    HIPR(hipStreamSynchronize(r->stream));
+    r->times = rt_build_times{};
+    r->built = true;
+    return RT_OK;
+}
+
+rt_status rt_dbuild_buffer(rt_scene* s, int which, void** ptr, uint64_t* bytes) {
+    if (!s || !ptr || !bytes) return fail(RT_EINVAL, "null argument");
+    if (s->reps.empty() || !s->reps[0]->d_n) return fail(RT_EINVAL, "rt_dbuild_bounds first");
+    const Replica& r = *s->reps[0];
+    const uint64_t n = s->n, tot = n ? 2 * n - 1 : 0, ni = n ? n - 1 : 0;
+    const uint64_t cc = (uint64_t)rt::dbuild_cross_cap(s->n) * rt::kCrossShards * 4;
+    switch (which) {
+        case RT_DB_SEND_KEYS: *ptr = r.bufs.keys[1]; *bytes = n * 4; break;
+        case RT_DB_SEND_VALS: *ptr = r.bufs.vals[1]; *bytes = n * 4; break;
+        case RT_DB_RECV_KEYS: *ptr = r.dk[1]; *bytes = n * 4; break;
+        case RT_DB_RECV_VALS: *ptr = r.dv[1]; *bytes = n * 4; break;
+        case RT_DB_KEYS: *ptr = r.bufs.keys[0]; *bytes = n * 4; break;
+        case RT_DB_VALS: *ptr = r.bufs.vals[0]; *bytes = n * 4; break;
+        case RT_DB_NODES: *ptr = r.bufs.nodes; *bytes = tot * 32; break;
+        case RT_DB_TRI_S: *ptr = r.bufs.tri_s; *bytes = n * 48; break;
+        case RT_DB_WIDE: *ptr = r.bufs.wnodes; *bytes = ni * 64; break;
+        case RT_DB_TOPO: *ptr = r.bufs.topo; *bytes = ni * 16; break;
+        case RT_DB_PRE: *ptr = r.bufs.prebuf; *bytes = n * 24; break;
+        case RT_DB_SUF: *ptr = r.bufs.sufbuf; *bytes = n * 24; break;
+        case RT_DB_TOTALS: *ptr = r.bufs.table; *bytes = (uint64_t)rt::refit_blocks(s->n) * 24; break;
+        case RT_DB_CROSS: *ptr = r.dcross; *bytes = cc; break;
+        case RT_DB_CROSS_ALL: *ptr = r.dcross_all; *bytes = cc; break;
+        default: return fail(RT_EINVAL, "unknown rt_dbuild_buffer selector");
+    }
+    return RT_OK;
 }
 
 #ifdef RT_STAMPS

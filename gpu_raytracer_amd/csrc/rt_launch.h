@@ -59,6 +59,16 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, Buil
 // and the soup in tris.
 hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t stream);
 
+// Distributed build phases (rt_dbuild_*; DESIGN.md "Distributed build").
+hipError_t launch_dbuild_bounds(const BuildBufs& b, uint32_t lo, uint32_t cnt, hipStream_t s);
+hipError_t launch_dbuild_keys(const BuildBufs& b, uint32_t lo, uint32_t cnt, const float* boxes, uint32_t nboxes,
+                              hipStream_t s);
+hipError_t launch_dbuild_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t cnt, const BuildBufs& b, hipStream_t s);
+hipError_t launch_dbuild_subtrees(const BuildBufs& b, uint32_t n, uint32_t block0, uint32_t nblocks, hipStream_t s);
+hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s);
+uint32_t dbuild_cross_cap(uint32_t n);  // crossing-list entries per shard (kCrossShards shards)
+uint32_t refit_blocks(uint32_t n);      // kRefitT-leaf blocks of k_topo_refit
+
 // Stage launchers for parity entry points (buffers sized by the caller).
 hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, BuildParams* params, hipStream_t s);
 hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* params, uint32_t* keys,

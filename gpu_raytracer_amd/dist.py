@@ -86,3 +86,226 @@ def gather_slabs(slab: torch.Tensor, rank: int, world: int, gather_list=None, ou
         return out
     dist.gather(slab, None, dst=0)
     return None
+
+
+# ---------------------------------------------------------------- distributed build
+# SURVEY.md §8(f) row 4 (DESIGN.md "Distributed build"): the BVH built by P
+# ranks together instead of replicated, bit-identical to rt_bvh_build.  The
+# phases are librtamd's rt_dbuild_* (LibStages); this module only moves the
+# bytes between them.  The same driver runs over any stage backend with the
+# LibStages interface -- the CPU tests plug in a numpy restatement of the
+# phases (oracle/dbuild_np.py, test infrastructure) and run it with gloo.
+import numpy as _np  # noqa: E402
+
+from . import _lib as _L  # noqa: E402
+
+
+def split_buckets(total_hist, nranks: int) -> _np.ndarray:
+    """Rank d owns the top-10-bit key buckets [cut[d], cut[d + 1]): the
+    cumulative count split as evenly as whole buckets allow (a Morton-prefix
+    partition of the key space)."""
+    c = _np.concatenate([[0], _np.cumsum(_np.asarray(total_hist, _np.int64))])
+    n = int(c[-1])
+    cut = [0]
+    for d in range(1, nranks):
+        b = int(_np.searchsorted(c, -(-n * d // nranks), side="left"))
+        cut.append(min(max(b, cut[-1]), 1024))
+    cut.append(1024)
+    return _np.asarray(cut, _np.int64)
+
+
+class LibStages:
+    """librtamd's rt_dbuild_* phases on one rank's scene, with its exchange
+    buffers seen by torch without a copy (int32 views on `device`)."""
+
+    def __init__(self, scene, device):
+        self.s, self.dev = scene, device
+        self.n = scene.num_tris
+
+    def bounds(self, rank, P):
+        return self.s.dbuild_bounds(rank, P)
+
+    def keys(self, rank, P, boxes):
+        return self.s.dbuild_keys(rank, P, boxes)
+
+    def sort(self, count):
+        self.s.dbuild_sort(count)
+
+    def subtrees(self, rank, P):
+        return self.s.dbuild_subtrees(rank, P)
+
+    def merge(self, total):
+        self.s.dbuild_merge(total)
+
+    def buf(self, which) -> torch.Tensor:
+        p, nbytes = self.s.dbuild_buffer(which)
+        if not nbytes:
+            return torch.empty(0, dtype=torch.int32, device=self.dev)
+        return torch.as_tensor(_DeviceBytes(p, nbytes), device=self.dev).view(torch.int32)
+
+    def sync(self):
+        torch.cuda.synchronize(self.dev)
+
+
+class Exchange:
+    """The collectives the distributed build needs, over the default process
+    group.  stage=True (gloo with device buffers) moves the bytes through
+    host memory."""
+
+    def __init__(self, stage: bool = False):
+        self.stage = stage
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.bytes_in = 0  # bytes this rank received
+
+    def gather_small(self, arr) -> _np.ndarray:
+        a = torch.from_numpy(_np.ascontiguousarray(arr).copy())
+        out = [torch.empty_like(a) for _ in range(self.world)]
+        dist.all_gather(out, a)
+        return _np.stack([o.numpy() for o in out])
+
+    def alltoallv(self, send: torch.Tensor, scounts, recv: torch.Tensor, rcounts):
+        self.bytes_in += 4 * (sum(rcounts) - rcounts[self.rank])
+        if self.stage:
+            r = torch.empty(int(sum(rcounts)), dtype=send.dtype)
+            dist.all_to_all_single(r, send.cpu(), list(map(int, rcounts)), list(map(int, scounts)))
+            recv.copy_(r)
+        else:
+            dist.all_to_all_single(recv, send, list(map(int, rcounts)), list(map(int, scounts)))
+
+    def share(self, buf: torch.Tensor, ranges):
+        """Element range q of buf (written by rank q) broadcast from rank q
+        to every rank, in place."""
+        for q, (lo, hi) in enumerate(ranges):
+            if hi <= lo:
+                continue
+            view = buf[lo:hi]
+            if q != self.rank:
+                self.bytes_in += 4 * (hi - lo)
+            if self.stage:
+                h = view.cpu()
+                dist.broadcast(h, src=q)
+                if q != self.rank:
+                    view.copy_(h)
+            else:
+                dist.broadcast(view, src=q)
+
+
+def distributed_build(st, ex: Exchange) -> dict:
+    """SPMD distributed BVH build (include/gpu_raytracer_amd.h, rt_dbuild_*):
+    every rank calls this with its own stage backend `st` over the same soup;
+    afterwards every rank's scene holds the BVH rt_bvh_build would make.
+    Returns this rank's counts (bytes received, crossing nodes)."""
+    rank, P, n = ex.rank, ex.world, st.n
+    sync = getattr(st, "sync", lambda: None)
+    # 1. global centroid bounds from every rank's slice box
+    boxes = ex.gather_small(st.bounds(rank, P))
+    # 2. Morton codes; the Morton-prefix partition; all-to-all of (key, index)
+    hist = st.keys(rank, P, boxes).astype(_np.int64)
+    hists = ex.gather_small(hist)
+    cut = split_buckets(hists.sum(0), P)
+    scount = [int(hist[cut[d]:cut[d + 1]].sum()) for d in range(P)]
+    rcount = [int(hists[q, cut[rank]:cut[rank + 1]].sum()) for q in range(P)]
+    ns, nr = sum(scount), sum(rcount)
+    sync()
+    for a, b in ((_L.RT_DB_SEND_KEYS, _L.RT_DB_RECV_KEYS), (_L.RT_DB_SEND_VALS, _L.RT_DB_RECV_VALS)):
+        ex.alltoallv(st.buf(a)[:ns], scount, st.buf(b)[:nr], rcount)
+    sync()
+    # 3. sort the received runs -> this rank's run of the global order; gather
+    st.sort(nr)
+    seg = [int(hists[:, cut[d]:cut[d + 1]].sum()) for d in range(P)]
+    off = _np.concatenate([[0], _np.cumsum(seg)]).astype(_np.int64)
+    ranges = [(int(off[q]), int(off[q + 1])) for q in range(P)]
+    for src, dst in ((_L.RT_DB_RECV_KEYS, _L.RT_DB_KEYS), (_L.RT_DB_RECV_VALS, _L.RT_DB_VALS)):
+        full = st.buf(dst)
+        full[ranges[rank][0]:ranges[rank][1]].copy_(st.buf(src)[:nr])
+        sync()
+        ex.share(full, ranges)
+    sync()
+    # 4. this rank's refit blocks, then every section's shares
+    nc = st.subtrees(rank, P)
+    shares = [dbuild_shares_of(n, q, P) for q in range(P)]
+    ni = max(n - 1, 0)
+    secs = [  # (buffer, int32 words per element, [(lo, hi) element range per rank])
+        (_L.RT_DB_NODES, 8, [(s[4], min(s[5], ni)) for s in shares]),
+        (_L.RT_DB_NODES, 8, [(ni + s[4], ni + s[5]) for s in shares]),
+        (_L.RT_DB_TRI_S, 12, [(s[4], s[5]) for s in shares]),
+        (_L.RT_DB_WIDE, 16, [(s[4], min(s[5], ni)) for s in shares]),
+        (_L.RT_DB_TOPO, 4, [(s[4], min(s[5], ni)) for s in shares]),
+        (_L.RT_DB_PRE, 6, [(s[4], s[5]) for s in shares]),
+        (_L.RT_DB_SUF, 6, [(s[4], s[5]) for s in shares]),
+        (_L.RT_DB_TOTALS, 6, [(s[2], s[3]) for s in shares]),
+    ]
+    sync()
+    for which, wpe, rg in secs:
+        ex.share(st.buf(which), [(lo * wpe, hi * wpe) for lo, hi in rg])
+    ncs = ex.gather_small(_np.array([nc], _np.int64))[:, 0]
+    coff = _np.concatenate([[0], _np.cumsum(ncs)]).astype(_np.int64)
+    allc = st.buf(_L.RT_DB_CROSS_ALL)
+    allc[int(coff[rank]):int(coff[rank + 1])].copy_(st.buf(_L.RT_DB_CROSS)[:nc])
+    sync()
+    ex.share(allc, [(int(coff[q]), int(coff[q + 1])) for q in range(P)])
+    sync()
+    # 5. every crossing node
+    st.merge(int(coff[-1]))
+    return dict(bytes_in=ex.bytes_in, crossing=int(coff[-1]), cut=cut.tolist())
+
+
+def dbuild_shares_of(n: int, rank: int, nranks: int) -> tuple:
+    """rt_dbuild_shares (a host function: no device needed)."""
+    from .scene import dbuild_shares
+    return dbuild_shares(n, rank, nranks)
+
+
+class ThreadExchange:
+    """Exchange between P ranks that are threads of one process (one GPU
+    standing in for P: the multi-rank emulation of tests/test_dbuild_gpu.py
+    and tools/dbuild_emulate.py).  Bytes move by device copies; construct one
+    shared `ThreadExchange.Hub(P)` and one ThreadExchange(hub, rank) per
+    thread."""
+
+    class Hub:
+        def __init__(self, world: int):
+            import threading
+            self.world = world
+            self.bar = threading.Barrier(world)
+            self.slots = [None] * world
+
+    def __init__(self, hub: "ThreadExchange.Hub", rank: int):
+        self.hub, self.rank, self.world = hub, rank, hub.world
+        self.bytes_in = 0
+
+    def _post(self, x):
+        self.hub.slots[self.rank] = x
+        self.hub.bar.wait()
+        got = list(self.hub.slots)
+        return got
+
+    def _done(self):
+        torch.cuda.synchronize()
+        self.hub.bar.wait()
+
+    def gather_small(self, arr) -> _np.ndarray:
+        got = self._post(_np.ascontiguousarray(arr).copy())
+        self._done()
+        return _np.stack(got)
+
+    def alltoallv(self, send, scounts, recv, rcounts):
+        got = self._post((send, list(map(int, scounts))))
+        o = 0
+        for q in range(self.world):
+            sq, cq = got[q]
+            start = sum(cq[:self.rank])
+            n = cq[self.rank]
+            recv[o:o + n].copy_(sq[start:start + n])
+            if q != self.rank:
+                self.bytes_in += 4 * n
+            o += n
+        self._done()
+
+    def share(self, buf, ranges):
+        got = self._post(buf)
+        for q, (lo, hi) in enumerate(ranges):
+            if q != self.rank and hi > lo:
+                buf[lo:hi].copy_(got[q][lo:hi])
+                self.bytes_in += 4 * (hi - lo)
+        self._done()

@@ -246,6 +246,35 @@ class Scene:
     def mark_built(self):
         call("rt_bvh_mark_built", self._h)
 
+    # ---- distributed build phases (rt_dbuild_*; driven by dist.distributed_build)
+    def dbuild_bounds(self, rank: int, nranks: int) -> np.ndarray:
+        box = np.zeros(6, np.float32)
+        call("rt_dbuild_bounds", self._h, rank, nranks, _p(box))
+        return box
+
+    def dbuild_keys(self, rank: int, nranks: int, boxes: np.ndarray) -> np.ndarray:
+        boxes = np.ascontiguousarray(boxes, np.float32).reshape(nranks, 6)
+        hist = np.zeros(1024, np.uint32)
+        call("rt_dbuild_keys", self._h, rank, nranks, _p(boxes), _p(hist))
+        return hist
+
+    def dbuild_sort(self, count: int) -> None:
+        call("rt_dbuild_sort", self._h, int(count))
+
+    def dbuild_subtrees(self, rank: int, nranks: int) -> int:
+        nc = C.c_uint32()
+        call("rt_dbuild_subtrees", self._h, rank, nranks, C.byref(nc))
+        return nc.value
+
+    def dbuild_merge(self, ncross_total: int) -> None:
+        call("rt_dbuild_merge", self._h, int(ncross_total))
+
+    def dbuild_buffer(self, which: int):
+        """(device pointer, bytes) of an exchange buffer (RT_DB_*)."""
+        p, b = C.c_void_p(), C.c_uint64()
+        call("rt_dbuild_buffer", self._h, int(which), C.byref(p), C.byref(b))
+        return int(p.value or 0), int(b.value)
+
     def render_counters(self, cam: rt_camera, w: int, h: int, spp: int = 1) -> np.ndarray:
         """§9.7 binary-traversal counters (the oracle's): nodes fetched, tris tested."""
         c = np.zeros(2, np.uint64)
@@ -301,6 +330,14 @@ class Scene:
 
     def sync(self) -> None:
         call("rt_scene_sync", self._h)
+
+
+def dbuild_shares(n: int, rank: int, nranks: int) -> tuple:
+    """(tri_lo, tri_hi, block_lo, block_hi, leaf_lo, leaf_hi) of one rank
+    (rt_dbuild_shares)."""
+    out = np.zeros(6, np.uint32)
+    call("rt_dbuild_shares", int(n), int(rank), int(nranks), _p(out))
+    return tuple(int(x) for x in out)
 
 
 def tiles_for_rank(w: int, h: int, rank: int, nranks: int) -> int:

@@ -223,6 +223,47 @@ rt_status rt_unpack_tiles_device(const void* d_slabs, uint32_t tiles_per_slab, u
 rt_status rt_scene_stream(rt_scene* s, void** stream_out);
 rt_status rt_scene_sync(rt_scene* s);
 
+/* ---- distributed BVH build (SURVEY.md §8(f) row 4 "distributed BVH build
+ * (multi-GPU sort by Morton prefix with all-to-all)"; DESIGN.md "Distributed
+ * build").  SPMD over nranks ranks, one scene each (the whole soup on every
+ * rank); the caller moves the bytes between the phases (gpu_raytracer_amd/
+ * dist.py drives them over torch.distributed: RCCL on GPUs, gloo on CPU).
+ * Every rank ends with the BVH rt_bvh_build makes, bit for bit:
+ *   1. rt_dbuild_bounds: centroid box of the rank's triangle slice
+ *      -> all-gather the nranks boxes;
+ *   2. rt_dbuild_keys: Morton codes of the slice against the global bounds,
+ *      the slice sorted by (key, index) in RT_DB_SEND_*, and its 1024-bucket
+ *      histogram of the top 10 key bits -> all-gather the histograms; rank d
+ *      owns the bucket range dist.split_buckets gives it; all-to-all the
+ *      (key, index) runs into RT_DB_RECV_* (ordered by source rank);
+ *   3. rt_dbuild_sort: the received pairs sorted -> the rank's run of the
+ *      global order; all-gather the runs into RT_DB_KEYS / RT_DB_VALS;
+ *   4. rt_dbuild_subtrees: topology, leaves, local boxes and wide records of
+ *      the rank's refit blocks (rt_dbuild_shares) and its crossing-node list
+ *      (RT_DB_CROSS) -> all-gather every section's share (nodes, tri_s, wide
+ *      records, topology, block prefix/suffix boxes, block totals) and the
+ *      crossing lists into RT_DB_CROSS_ALL;
+ *   5. rt_dbuild_merge: boxes and wide records of every crossing node; the
+ *      scene is then built (rt_render, rt_bvh_read ...). */
+enum {
+    RT_DB_SEND_KEYS = 0, RT_DB_SEND_VALS, RT_DB_RECV_KEYS, RT_DB_RECV_VALS, RT_DB_KEYS, RT_DB_VALS,
+    RT_DB_NODES, RT_DB_TRI_S, RT_DB_WIDE, RT_DB_TOPO, RT_DB_PRE, RT_DB_SUF, RT_DB_TOTALS, RT_DB_CROSS,
+    RT_DB_CROSS_ALL
+};
+/* shares of rank `rank`: out = {tri_lo, tri_hi, block_lo, block_hi,
+ * leaf_lo, leaf_hi} (triangles [tri_lo, tri_hi) for phases 1-2; refit blocks
+ * of 512 leaves [block_lo, block_hi) = sorted leaves [leaf_lo, leaf_hi) and
+ * internal nodes [leaf_lo, min(leaf_hi, n - 1)) for phase 4). */
+rt_status rt_dbuild_shares(uint32_t n, uint32_t rank, uint32_t nranks, uint32_t out[6]);
+rt_status rt_dbuild_bounds(rt_scene* s, uint32_t rank, uint32_t nranks, float box_out[6]);
+rt_status rt_dbuild_keys(rt_scene* s, uint32_t rank, uint32_t nranks, const float* boxes /* nranks x 6 */,
+                         uint32_t hist_out[1024]);
+rt_status rt_dbuild_sort(rt_scene* s, uint32_t count);
+rt_status rt_dbuild_subtrees(rt_scene* s, uint32_t rank, uint32_t nranks, uint32_t* ncross_out);
+rt_status rt_dbuild_merge(rt_scene* s, uint32_t ncross_total);
+/* device pointer and size in bytes of an exchange buffer (RT_DB_*) */
+rt_status rt_dbuild_buffer(rt_scene* s, int which, void** ptr, uint64_t* bytes);
+
 /* ---- per-stage entry points for parity tests; host
  * buffers in/out, device compute on `device`. ---- */
 rt_status rt_stage_bounds(int device, const float* tris, uint32_t n, float bounds9[9]);

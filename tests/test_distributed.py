@@ -66,3 +66,70 @@ def test_partition_helpers():
     for (w, h, P) in [(1920, 1080, 8), (3840, 2160, 8), (17, 33, 3)]:
         assert sum(D.tiles_of_rank(w, h, r, P) for r in range(P)) == D.tiles_total(w, h)
         assert sum(D.rays_of_rank(w, h, 2, r, P) for r in range(P)) == w * h * 2
+
+
+def _dbuild_worker(rank, world, port, n, seed, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gpu_raytracer_amd import dist as D
+        from gpu_raytracer_amd import _lib as L
+        from oracle import oracle as O
+        from oracle.dbuild_np import NumpyStages
+        tris = O.soup(n, seed).reshape(-1, 9)
+        st = NumpyStages(tris)
+        info = D.distributed_build(st, D.Exchange())
+        exp = O.build(tris)
+        got_nodes = st.arr(L.RT_DB_NODES)
+        ok = {
+            "keys": np.array_equal(st.arr(L.RT_DB_KEYS), exp["keys"]),
+            "vals": np.array_equal(st.arr(L.RT_DB_VALS), exp["vals"]),
+            "nodes": np.array_equal(got_nodes.view(np.uint32), exp["nodes"].view(np.uint32)),
+            "tri_s": np.array_equal(st.arr(L.RT_DB_TRI_S)[:, :9], tris[exp["vals"]])
+            and np.array_equal(st.arr(L.RT_DB_TRI_S)[:, 9].view(np.uint32), exp["vals"]),
+            "crossing": info["crossing"] > 0 or n <= 512,
+            "exchanged": info["bytes_in"] > 0,
+        }
+        q.put((rank, ok))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,seed", [(2, 20000, 31), (3, 7001, 32), (2, 300, 33), (4, 5, 34)])
+def test_gloo_distributed_build(world, n, seed):
+    """the distributed-build driver (Morton-prefix
+    partition, all-to-all of (key, index), per-rank refit blocks, share
+    gathers, crossing-node merge) on world_size CPU ranks over gloo, with
+    the numpy restatement of the device phases: every rank ends with the
+    single-process oracle's BVH, bit for bit (sorted keys/indices, every
+    node's box, child and escape link, the leaf triangle records)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dbuild_worker, args=(r, world, port, n, seed, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = dict(q.get(timeout=10) for _ in range(world))
+    for r in range(world):
+        assert all(res[r].values()), (r, res[r])
+
+
+def test_split_buckets():
+    from gpu_raytracer_amd import dist as D
+    h = np.zeros(1024, np.int64)
+    h[[3, 500, 501, 1000]] = [10, 5, 5, 10]
+    for P in (1, 2, 3, 8):
+        cut = D.split_buckets(h, P)
+        assert cut[0] == 0 and cut[-1] == 1024 and np.all(np.diff(cut) >= 0)
+        assert sum(h[cut[d]:cut[d + 1]].sum() for d in range(P)) == h.sum()
+    assert list(D.split_buckets(np.ones(1024), 4)) == [0, 256, 512, 768, 1024]
+    for n, P in ((1_000_000, 8), (10, 3), (1, 2), (513, 2)):
+        sh = [D.dbuild_shares_of(n, r, P) for r in range(P)]
+        assert sh[0][0] == 0 and sh[-1][1] == n and all(sh[r][1] == sh[r + 1][0] for r in range(P - 1))
+        assert sh[0][4] == 0 and sh[-1][5] == n and all(sh[r][5] == sh[r + 1][4] for r in range(P - 1))
