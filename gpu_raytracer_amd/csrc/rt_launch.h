@@ -128,6 +128,8 @@ struct TileSched {
     uint32_t* coop_ctr = nullptr;   // [2] queue counters, alternating frames
     uint32_t coop_qcap = 0;
     uint32_t coop_par = 0;          // which counter this frame uses
+    CamF prev_cam{};                // camera of the previous frame of this shape (pixel order only if equal)
+    bool prev_cam_valid = false;
     bool coop_fresh = true;         // queue (re)allocated: zero both counters before the first launch
     bool have_prev = false;
     bool fresh = true;              // maps (re)allocated: clear both before the first launch

@@ -12,6 +12,7 @@
 #include "rt_launch.h"
 
 #include <atomic>
+#include <cstring>
 #include <mutex>
 
 namespace rt {
@@ -1763,10 +1764,22 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     // (more lanes in both branches of every step) only lengthens
     // (DESIGN.md "Pixel order").  256-thread blocks only (the ranking is per
     // block).
+    //
+    // The previous frame's per-pixel costs describe this frame's pixels only
+    // when the camera has not moved: with the bench's orbit (0.25 deg per
+    // frame, a few pixels of image motion) the stale order put lanes of
+    // different cost together and cost 3 % (0.372 vs 0.383 ms,
+    // profiles/ab_moving_r02.log), so after a camera change the frame keeps
+    // the quadrant layout and only records its costs for the next one.
     if (cost_out && !small && sched->px_cur &&
         (cfg.px_sort == 2 || (cfg.px_sort == 1 && nranks == 1))) {
-        if (sched->have_prev) px_prev = sched->px_prev;
+        const bool same_cam = sched->prev_cam_valid && std::memcmp(&sched->prev_cam, &c, sizeof(CamF)) == 0;
+        if (sched->have_prev && same_cam) px_prev = sched->px_prev;
         px_cost = sched->px_cur;
+    }
+    if (sched) {
+        sched->prev_cam = c;
+        sched->prev_cam_valid = true;
     }
     // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
     const uint32_t coop_cap = wide && sched && sched->coop_q ? (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) : 0u;

@@ -400,3 +400,27 @@ def _successive_frames(R, oracle, s_tris, exp):
                 assert np.array_equal(img.cpu().numpy().view(np.uint8), full), wg
             finally:
                 R.config_set("trace.wg_tiles", 64)
+
+
+def test_tile_order_moving_camera(R, oracle):
+    """A camera that moves every frame (the bench's orbit): the tile order
+    comes from the previous frame's map, the pixel order is skipped while
+    the camera moves and resumes when it stops -- every frame == the oracle."""
+    import math
+    from gpu_raytracer_amd.scenes import SOUP_VIEW as V
+    tris = soup(oracle, 40000, 14)
+    exp = oracle.build(tris)
+    w, h = 240, 136
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for i in (0, 1, 2, 3, 3, 3):
+            a = math.radians(2.0 * i)
+            ex, ez = V.eye[0] - V.at[0], V.eye[2] - V.at[2]
+            eye = (V.at[0] + ex * math.cos(a) - ez * math.sin(a), V.eye[1],
+                   V.at[2] + ex * math.sin(a) + ez * math.cos(a))
+            cam = R.camera_look_at(eye, V.at, V.up, V.vfov, w, h)
+            ocam = oracle.camera_look_at(eye, V.at, V.up, V.vfov, w, h)
+            eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, 1)
+            hits, rgba, _ = s.render(cam, w, h, 1)
+            assert np.array_equal(rgba, oracle.shade(eh, w, h, 1)), i
+            assert np.array_equal(bits(hits["t"]), bits(eh["t"])), i

@@ -1,0 +1,45 @@
+"""A/B of trace configurations on the bench's moving-camera sequence (the
+headline workload: soup-1M 1080p, eye orbiting 0.25 deg per frame), full
+frames on one GPU; each configuration renders the whole sequence in turn,
+interleaved over rounds; reports the mean event-timed trace per frame.
+usage: python tools/ab_moving.py [rounds] [frames] name:knob=v,knob=v ..."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import gpu_raytracer_amd as R  # noqa: E402
+from gpu_raytracer_amd import scenes as S  # noqa: E402
+import bench  # noqa: E402
+
+rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+frames = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+configs = [("base", {})]
+for a in sys.argv[3:]:
+    name, kv = a.split(":", 1)
+    configs.append((name, {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}))
+cfg = S.CONFIGS[3]
+view = S.VIEWS[cfg.scene]
+w, h, spp = cfg.w, cfg.h, cfg.spp
+scene = R.Scene.generate_soup(1_000_000, 1)
+scene.build()
+cams = [R.camera_look_at(bench.orbit_view(view, i), view.at, view.up, view.vfov, w, h) for i in range(frames + 2)]
+img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+defaults = {}
+res = {n: [] for n, _ in configs}
+for _ in range(rounds):
+    for name, kv in configs:
+        for k, v in kv.items():
+            R.config_set(k, v)
+        scene.render_device(cams[0], w, h, spp, d_rgba=img.data_ptr(), timed=True)  # this shape's first frame
+        scene.render_device(cams[1], w, h, spp, d_rgba=img.data_ptr(), timed=True)
+        t = [scene.render_device(cams[2 + i], w, h, spp, d_rgba=img.data_ptr(), timed=True) for i in range(frames)]
+        res[name].append(float(np.mean(t)))
+        for k in kv:  # back to the library defaults
+            R.config_set(k, {"trace.coop_cap": 0, "trace.tile_order": 1, "trace.px_sort": 1, "trace.wg": 256,
+                             "trace.order_dilate": 0, "trace.coop_lanes": 64}.get(k, 0))
+for name, _ in configs:
+    print(f"{name:<22s} mean trace {np.median(res[name]):.4f} ms  (rounds: {' '.join(f'{x:.4f}' for x in res[name])})",
+          flush=True)
