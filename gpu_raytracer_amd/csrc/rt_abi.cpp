@@ -353,7 +353,7 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
     const uint32_t qcap = (cfg.coop_cap || cfg.coop_cap_tiles) ? (cfg.coop_max + 63u) & ~63u : 0u;
     const size_t maps = 3ull * nb * 4 + 2ull * nb * 512;
     const size_t qoff = (maps + 255) & ~size_t(255);
-    const size_t need = qcap ? qoff + 512 + 32ull * qcap : maps;
+    const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
     if (!same || r.order_cap < need || r.sched.coop_qcap != qcap) {
         std::memset(r.sched_key, 0, sizeof(r.sched_key));  // invalid until the maps exist
         RTR(grow(&r.d_order, &r.order_cap, need));

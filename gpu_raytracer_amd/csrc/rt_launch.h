@@ -117,6 +117,8 @@ struct TraceConfig {
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };
 
+constexpr uint32_t kCoopEntryBytes = 176;  // heavy-ray queue entry (trace_kernels.hip kCoopEntry x 16 B)
+
 // Per-launch tile scheduling state (owned by the scene, one per frame shape).
 struct TileSched {
     uint32_t* order = nullptr;      // [nb] dispatch index -> tile slot
@@ -124,7 +126,7 @@ struct TileSched {
     uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
     uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
     uint16_t* px_cur = nullptr;     // [nb][256] this frame's
-    uint4* coop_q = nullptr;        // [coop_qcap][2] heavy-ray queue (trace.coop_cap)
+    uint4* coop_q = nullptr;        // [coop_qcap] x kCoopEntryBytes heavy-ray queue (trace.coop_cap)
     uint32_t* coop_ctr = nullptr;   // [2] queue counters, alternating frames
     uint32_t coop_qcap = 0;
     uint32_t coop_par = 0;          // which counter this frame uses

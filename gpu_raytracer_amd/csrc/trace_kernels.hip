@@ -514,13 +514,20 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
 // primary ray still traversing after coop_cap wide steps stops, and its
 // pixel -- from that sample on, with the colour sums of the samples before
 // it -- is queued for k_trace_coop, which traces it with a whole wave.
-// 32-B entries {x, y, first sample, output pixel index} {r, g, b, 0}, in
-// kCoopShards shards of `cap` entries, each with its own reservation counter
+// Entries of kCoopEntry x 16 B: {x, y, deferred sample, output pixel index}
+// {r, g, b sums of the earlier samples, best prim} {tb, hu, hv, nst} and
+// the deferred sample's traversal state -- its nst <= kWideStack + 1 pending
+// entries {ref, tn} bottom to top (the lane's stack, then its current entry):
+// k_trace_coop resumes the ray there instead of restarting it at the root.
+// They live in kCoopShards shards of `cap` entries, each with its own reservation counter
 // (wave gw reserves in shard gw mod kCoopShards): tens of thousands of
 // returning atomics on ONE device-scope counter serialise (~10 ns each, a
 // full-frame pass 1 went 0.33 -> 0.42 ms), spread over 64 they do not.  A
 // counter may pass `cap`: lanes that find their shard full go on tracing.
 constexpr uint32_t kCoopShards = 64;
+constexpr uint32_t kCoopFrontier = kWideStack + 1;           // pending entries a deferred ray can have
+constexpr uint32_t kCoopEntry = 3 + (kCoopFrontier + 1) / 2;  // uint4 per queue entry
+static_assert(kCoopEntry * 16 == kCoopEntryBytes, "rt_launch.h sizes the queue");
 struct CoopQ {
     uint4* q = nullptr;
     uint32_t* ctr = nullptr;       // [kCoopShards] this frame's reservation counters
@@ -531,6 +538,30 @@ struct CoopQ {
 // Called by the lanes that reach the step cap in this step (divergent): one
 // atomic per wave reserves their entries.  Returns 3 (deferred) with the
 // entry index, or 0 (shard full: keep tracing).
+// The deferring lane's entry: pixel, colour sums, best hit and its pending
+// subtrees in preorder from the bottom of its LDS stack (stack entries carry
+// their tn truncated to 16 bits: a lower bound, as in wide_step).
+template <int NT>
+__device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint32_t x, uint32_t y, uint32_t s,
+                                           uint32_t pi, float r, float g, float b, const WRay& R,
+                                           const uint32_t* sref, const uint16_t* stn) {
+    uint4* e = cq.q + (uint64_t)qslot * kCoopEntry;
+    const uint32_t nst = R.sp + (R.cur != RT_SENT ? 1u : 0u);
+    e[0] = make_uint4(x, y, s, pi);
+    e[1] = make_uint4(__float_as_uint(r), __float_as_uint(g), __float_as_uint(b), R.hp);
+    e[2] = make_uint4(__float_as_uint(R.tb), __float_as_uint(R.hu), __float_as_uint(R.hv), nst);
+    for (uint32_t j = 0; j < nst; j += 2) {
+        uint32_t rf[2], tn[2];
+#pragma unroll
+        for (uint32_t k = 0; k < 2; ++k) {
+            const uint32_t i = j + k;
+            rf[k] = i < R.sp ? sref[i * NT] : R.cur;
+            tn[k] = i < R.sp ? (uint32_t)stn[i * NT] << 16 : __float_as_uint(R.ctn);
+        }
+        e[3 + j / 2] = make_uint4(rf[0], tn[0], rf[1], tn[1]);
+    }
+}
+
 __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t& qslot) {
     const uint64_t mm = __ballot(1);
     const uint32_t leader = (uint32_t)__builtin_ctzll(mm);
@@ -621,7 +652,9 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                     if (!SHADOW && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
                 }
                 if (PX) steps += R.steps;
-                if (st == 3) {  // heavy: k_trace_coop finishes this pixel from sample s on
+                if (st == 3) {  // heavy: k_trace_coop finishes this pixel from here on
+                    coop_store<NT>(cq, qslot, x, y, s, PACKED ? slot * 256 + ly * 16 + lx : y * W + x, r, g, b, R,
+                                   s_ref + threadIdx.x, s_tn + threadIdx.x);
                     dsamp = s;
                     break;
                 }
@@ -661,10 +694,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             }
         }
         const uint32_t pi = PACKED ? slot * 256 + ly * 16 + lx : y * W + x;
-        if (dsamp != RT_SENT) {
-            cq.q[2 * (uint64_t)qslot] = make_uint4(x, y, dsamp, pi);
-            cq.q[2 * (uint64_t)qslot + 1] = make_uint4(__float_as_uint(r), __float_as_uint(g), __float_as_uint(b), 0u);
-        } else if (rgba) {
+        if (dsamp == RT_SENT && rgba) {
             const float sc = 1.0f / (float)spp;
             const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
             rgba[pi] = px;
@@ -776,25 +806,40 @@ __device__ __forceinline__ uint32_t gread_u(uint32_t x, uint32_t src) {
 
 // One group, one ray (o, d the same in all its lanes), 1/d finite on every
 // axis.  hp = prim.
+// resume (nullable): a queue entry -- start from its best hit and pending
+// entries (pass 1's state) instead of the root.
 template <bool COUNT, int G>
 __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                            const float4* __restrict__ tri_s, uint32_t n, const float* o,
-                                           const float* d, CoopLds<G>& L, float& tb_out, float& hu_out,
-                                           float& hv_out, uint32_t& hp_out, uint32_t& cn, uint32_t& ct) {
+                                           const float* d, CoopLds<G>& L, const uint4* __restrict__ resume,
+                                           float& tb_out, float& hu_out, float& hv_out, uint32_t& hp_out,
+                                           uint32_t& cn, uint32_t& ct) {
+    static_assert(G > kCoopFrontier, "a group loads a resumed frontier in one step");
     constexpr uint32_t CAP = CoopCfg<G>::cap;
     const uint32_t lane = __lane_id();
     const uint32_t gl = lane & (G - 1), gbase = lane & ~(uint32_t)(G - 1);
     WRay R;
     wray_init(o, d, R);
     float tb = __builtin_inff(), hu = 0.0f, hv = 0.0f;
-    uint32_t hk = RT_SENT;  // tri_s slot of the current best (its prim is read at the end)
-    if (gl == 0) {
+    uint32_t hk = RT_SENT;   // tri_s slot of a best hit found here (its prim is read at the end)
+    uint32_t hp0 = RT_SENT;  // the best hit's prim when resumed
+    uint32_t sp = 1;
+    if (resume) {
+        const uint4 h1 = resume[1], h2 = resume[2];
+        hp0 = h1.w;
+        tb = __uint_as_float(h2.x); hu = __uint_as_float(h2.y); hv = __uint_as_float(h2.z);
+        sp = h2.w;
+        if (gl < sp) {
+            const uint4 pr = resume[3 + gl / 2];
+            L.ref[gl] = (gl & 1) ? pr.z : pr.x;
+            L.tn[gl] = __uint_as_float((gl & 1) ? pr.w : pr.y);
+        }
+    } else if (gl == 0) {
         L.ref[0] = 0u;  // the root record
         L.tn[0] = 0.0f;
     }
     __builtin_amdgcn_wave_barrier();
     __asm__ volatile("" ::: "memory");
-    uint32_t sp = 1;
     const uint32_t limit = 4 * n + 16;
     bool handoff = false;
     for (uint32_t guard = 0; sp > 0; ++guard) {
@@ -889,7 +934,7 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
         __asm__ volatile("" ::: "memory");
         sp = spn;
     }
-    uint32_t hp = hk == RT_SENT ? RT_SENT : __float_as_uint(tri_s[(uint64_t)hk * 3 + 2].y);
+    uint32_t hp = hk == RT_SENT ? hp0 : __float_as_uint(tri_s[(uint64_t)hk * 3 + 2].y);
     if (handoff) {
         if (gl == 0) {
             const uint32_t head = sp ? L.ref[sp - 1] & ~kCoopRes : RT_SENT;
@@ -944,7 +989,8 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
             if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
         }
         const uint32_t slot = sh * cq.cap + (e - sbase);
-        const uint4 a = cq.q[2 * (uint64_t)slot], b = cq.q[2 * (uint64_t)slot + 1];
+        const uint4* ent = cq.q + (uint64_t)slot * kCoopEntry;
+        const uint4 a = ent[0], b = ent[1];
         const uint32_t x = a.x, y = a.y, pi = a.w;
         float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
         for (uint32_t s = a.z; s < spp; ++s) {
@@ -961,8 +1007,8 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
             for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
             float tb, hu, hv;
             uint32_t hp;
-            coop_trace<COUNT, G>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp], tb,
-                                 hu, hv, hp, cn, ct);
+            coop_trace<COUNT, G>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp],
+                                 s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
             if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
             if (hp != RT_SENT) {
                 r = r + hu;

@@ -11,7 +11,8 @@ import torch  # noqa: E402
 import gpu_raytracer_amd as R  # noqa: E402
 from gpu_raytracer_amd.scenes import SOUP_VIEW as V  # noqa: E402
 
-w, h, spp, P = 1920, 1080, 1, 8
+w, h, spp, P = 1920, 1080, 1, int(os.environ.get("COOP_P", "8"))
+R.config_set("trace.coop_lanes", int(os.environ.get("COOP_LANES", "64")))
 s = R.Scene.generate_soup(1_000_000, 1)
 s.build()
 cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)

@@ -29,16 +29,17 @@ for r in tr:
     cur["end"] = int(r["End_Timestamp"])
 if cur:
     frames.append(cur)
-per_cap = 8 * 4 + 4
+P = int(os.environ.get("COOP_P", "8"))
+per_cap = P * 4 + 4
 print(f"{len(frames)} frames parsed (expect {per_cap * len(caps)})")
 for i, c in enumerate(caps):
     fs = frames[i * per_cap:(i + 1) * per_cap]
     print(f"cap {c}:")
-    for r in range(9):
+    for r in range(P + 1):
         grp = fs[r * 4:(r + 1) * 4][1:]
         if not grp:
             continue
-        tag = f"rank {r}" if r < 8 else "full  "
+        tag = f"rank {r}" if r < P else "full  "
         span = [(f["end"] - f["start"]) / 1000.0 for f in grp]
         print(f"  {tag}: trace " + " ".join(f"{f.get('trace', 0):7.1f}" for f in grp) +
               " | coop " + " ".join(f"{f.get('coop', 0):6.1f}" for f in grp) +
