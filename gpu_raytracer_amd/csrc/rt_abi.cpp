@@ -435,6 +435,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "render.rccl1" && (value == 0 || value == 1)) c.render_rccl1 = (uint32_t)value;
     else if (k == "trace.coop_cap" && value >= 0 && value <= (1 << 20)) c.coop_cap = (uint32_t)value;
     else if (k == "trace.coop_cap_tiles" && value >= 0 && value <= (1 << 20)) c.coop_cap_tiles = (uint32_t)value;
+    else if (k == "trace.buf_loads" && (value == 0 || value == 1)) c.buf_loads = (uint32_t)value;
     else if (k == "trace.coop_lanes" && (value == 16 || value == 32 || value == 64)) c.coop_lanes = (uint32_t)value;
     else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
     else return false;
@@ -1583,7 +1584,8 @@ rt_status rt_dbuild_bounds(rt_scene* s, uint32_t rank, uint32_t nranks, float bo
     if (!box_out) return fail(RT_EINVAL, "null argument");
     Replica* r = nullptr;
     RTR(dbuild_replica(s, rank, nranks, &r));
-    r->built = false;  // the BVH is rewritten from here on
+    r->built = false;  // the BVH is rewritten from here on; other replicas are stale
+    for (size_t i = 1; i < s->reps.size(); ++i) s->reps[i]->built = false;
     uint32_t sh[6];
     RTR(rt_dbuild_shares(s->n, rank, nranks, sh));
     if (sh[1] > sh[0]) {

@@ -109,6 +109,7 @@ struct TraceConfig {
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
     uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
+    uint32_t buf_loads = 1;       // wide step loads through buffer descriptors (one round trip per step)
     uint32_t coop_cap = 0;        // primary full frames: rays past this many wide steps finish in k_trace_coop
                                   // (one wave per ray); 0 = off
     uint32_t coop_cap_tiles = 96; // the same for one rank's tiles of a multi-GPU frame (tools/coop_sweep.py)

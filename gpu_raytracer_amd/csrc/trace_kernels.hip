@@ -295,10 +295,40 @@ __device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const ui
 // 4-6 % faster); the full-frame primary kernel, issue-bound at high
 // occupancy, and path mode (3 % slower with it) keep the box test first
 // (profiles/ab_mtfirst_r01.log).
-template <bool COUNT, int NT, bool ANY = false, bool MTF = false>
+// Buffer views of the wide records and the leaf triangle records (BUF
+// steps): a step loads its record and its triangle with buffer loads whose
+// offset is out of range -- zero returned, no memory access -- for a lane
+// that needs neither, instead of branching around flat loads.  Without the
+// branches the compiler has no phi copies of half-arrived registers to make
+// and issues both loads before waiting for either: one round trip per step
+// where the flat form (a copy of the triangle's registers before the record
+// loads are issued) took two.  32-bit offsets: (n - 1) * 64 and n * 48 bytes
+// must fit (n <= 2^26; the launcher uses the flat form above that).
+struct WideMem {
+    __amdgpu_buffer_rsrc_t wr, tr;
+    uint32_t wbytes, tbytes;
+};
+constexpr uint32_t kBufMaxN = 1u << 26;
+
+__device__ __forceinline__ WideMem wide_mem(const uint4* wnodes, const float4* tri_s, uint32_t n) {
+    WideMem m;
+    m.wbytes = n >= 2 ? (n - 1) * 64u : 0u;
+    m.tbytes = n * 48u;
+    m.wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wnodes), 0, (int)m.wbytes, 0x00020000);
+    m.tr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tri_s), 0, (int)m.tbytes, 0x00020000);
+    return m;
+}
+__device__ __forceinline__ uint4 bload_u4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+__device__ __forceinline__ float4 bload_f4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+template <bool COUNT, int NT, bool ANY = false, bool MTF = false, bool BUF = false>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
-                                         uint32_t& cn, uint32_t& ct, bool any = ANY) {
+                                         uint32_t& cn, uint32_t& ct, bool any = ANY, const WideMem* M = nullptr) {
     if (++R.steps > limit) return 2;
     if (R.pend == RT_SENT) {
         if (R.cur == RT_SENT) wide_pop<NT>(R, sref, stn);
@@ -309,15 +339,26 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     }
     if (R.pend == RT_SENT && R.cur == RT_SENT) return 1;
     const bool node = R.cur != RT_SENT && !(R.cur & kWideLeaf);
+    const bool leaf = R.pend != RT_SENT;
+    // both addresses before any load: with a load in flight, a register
+    // the compiler reuses for the second address would force a wait for the
+    // first load, and the triangle and the record would cost two round trips
+    const uint4* wp = wnodes + (uint64_t)(node ? R.cur : 0u) * 4;
+    const float4* tp = tri_s + (uint64_t)(leaf ? (R.pend & ~kWideLeaf) : 0u) * 3;
+    const uint32_t to = BUF ? (leaf ? (R.pend & ~kWideLeaf) * 48u : M->tbytes) : 0u;
     uint4 w0, w1, w2, w3;
-    if (node) {
-        const uint4* wp = wnodes + (uint64_t)R.cur * 4;
-        w0 = wp[0]; w1 = wp[1]; w2 = wp[2]; w3 = wp[3];
+    float4 T0, T1, T2;
+    if (BUF) {
+        const uint32_t wo = node ? R.cur * 64u : M->wbytes;
+        T0 = bload_f4(M->tr, to); T1 = bload_f4(M->tr, to + 16); T2 = bload_f4(M->tr, to + 32);
+        w0 = bload_u4(M->wr, wo); w1 = bload_u4(M->wr, wo + 16); w2 = bload_u4(M->wr, wo + 32);
+        w3 = bload_u4(M->wr, wo + 48);
+    } else {
+        if (leaf) { T0 = tp[0]; T1 = tp[1]; T2 = tp[2]; }
+        if (node) { w0 = wp[0]; w1 = wp[1]; w2 = wp[2]; w3 = wp[3]; }
     }
-    if (R.pend != RT_SENT) {
+    if (leaf) {
         if (COUNT) ++ct;
-        const float4* tp = tri_s + (uint64_t)(R.pend & ~kWideLeaf) * 3;
-        const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
         const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
         if (MTF) {
             // §9.7 takes the triangle iff its exact leaf box passes the slab
@@ -328,7 +369,8 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
             float t, u, v;
             if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) {
                 __asm__ volatile("" ::: "memory");  // reload below instead of keeping tv live
-                const float4 U0 = tp[0], U1 = tp[1], U2 = tp[2];
+                const float4 U0 = BUF ? bload_f4(M->tr, to) : tp[0], U1 = BUF ? bload_f4(M->tr, to + 16) : tp[1],
+                             U2 = BUF ? bload_f4(M->tr, to + 32) : tp[2];
                 const float uv[9] = {U0.x, U0.y, U0.z, U0.w, U1.x, U1.y, U1.z, U1.w, U2.x};
                 float lo[3], hi[3], tn;
                 tri_bounds(uv, lo, hi);
@@ -577,7 +619,7 @@ __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t
     return 0;
 }
 
-template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false>
+template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false>
 __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,
@@ -646,9 +688,11 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                 wray_init(cam.eye, d, R);
                 int st = R.fin ? 0 : 2;
                 const char* nd = reinterpret_cast<const char*>(nodes);
+                const WideMem M = wide_mem(wnodes, tri_s, n);
                 while (st == 0) {
-                    st = wide_step<COUNT, NT, false, PACKED || SHADOW>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
-                                                                      s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct);
+                    st = wide_step<COUNT, NT, false, PACKED || SHADOW, BUF>(R, wnodes, tri_s, cam.eye, wcap,
+                                                                           4 * n + 16, s_ref + threadIdx.x,
+                                                                           s_tn + threadIdx.x, cn, ct, false, &M);
                     if (!SHADOW && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
                 }
                 if (PX) steps += R.steps;
@@ -1841,10 +1885,14 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         cq.ctr_next = sched->coop_ctr + (sched->coop_par ^ 1u) * kCoopShards;
         cq.cap = sched->coop_qcap / kCoopShards;
     }
-#define RT_TRACE_NT(C, P, WI, NT)                                                                                  \
-    hipLaunchKernelGGL((k_trace<C, P, WI, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes, cap, tris, n, \
-                       cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, cost_out, \
-                       px_prev, px_cost, coop_cap, cq)
+    // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
+    const bool buf = n <= kBufMaxN && cfg.buf_loads;
+#define RT_TRACE_NT_B(C, P, WI, NT, B)                                                                             \
+    hipLaunchKernelGGL((k_trace<C, P, WI, NT, false, B>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes,    \
+                       cap, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, \
+                       cost_out, px_prev, px_cost, coop_cap, cq)
+#define RT_TRACE_NT(C, P, WI, NT) \
+    if (buf) RT_TRACE_NT_B(C, P, WI, NT, WI); else RT_TRACE_NT_B(C, P, WI, NT, false)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \
@@ -1861,6 +1909,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
 #undef RT_TRACE_W
 #undef RT_TRACE
 #undef RT_TRACE_NT
+#undef RT_TRACE_NT_B
     if (coop_cap) {
         hipError_t le = hipGetLastError();
         if (le != hipSuccess) return le;

@@ -60,7 +60,7 @@ def main():
         lines.append(f"| {k} | {f:.1f} | {w:.1f} | {2*f*1024:.3e} | {w*1024:.3e} |")
     os.makedirs("profiles", exist_ok=True)
     open(f"profiles/rocprof_{tag}.md", "w").write("\n".join(lines) + "\n")
-    tk = "k_trace<false, false, true, 256, false>"  # the timed launch: no counters, full image, wide traversal
+    tk = "k_trace<false, false, true, 256, false, true>"  # the timed launch: no counters, full image, wide traversal, buffer loads
     if tk in pm["FETCH_SIZE"] and tk in pm["WRITE_SIZE"]:
         fetch = pm["FETCH_SIZE"][tk] * 1024
         write = pm["WRITE_SIZE"][tk] * 1024
