@@ -438,7 +438,15 @@ __device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const 
     R.tb = tmax;
     const bool wide = R.fin && wnodes && n >= 2;
     int st = wide ? 0 : 2;
-    while (st == 0) st = wide_step<COUNT, NT, false, MTF>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any);
+    if (n <= kBufMaxN) {  // buffer loads (WideMem): record and triangle in one round trip
+        const WideMem M = wide_mem(wnodes, tri_s, n);
+        while (st == 0)
+            st = wide_step<COUNT, NT, false, MTF, true>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any,
+                                                        &M);
+    } else {
+        while (st == 0)
+            st = wide_step<COUNT, NT, false, MTF>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any);
+    }
     if (st == 2) {
         const uint32_t start = !wide ? (n ? 0u : RT_SENT) : (R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1));
         trace_ray_from<COUNT>(nodes, tri_s, n, o, R.d, start, R.tb, R.hu, R.hv, R.hp, cn, ct, any);
