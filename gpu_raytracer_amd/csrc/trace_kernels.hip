@@ -872,6 +872,7 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
     const uint32_t gl = lane & (G - 1), gbase = lane & ~(uint32_t)(G - 1);
     WRay R;
     wray_init(o, d, R);
+    const WideMem M = wide_mem(wnodes, tri_s, n);  // n <= kBufMaxN (the launcher's condition)
     float tb = __builtin_inff(), hu = 0.0f, hv = 0.0f;
     uint32_t hk = RT_SENT;   // tri_s slot of a best hit found here (its prim is read at the end)
     uint32_t hp0 = RT_SENT;  // the best hit's prim when resumed
@@ -911,6 +912,18 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
         __builtin_amdgcn_wave_barrier();
         __asm__ volatile("" ::: "memory");
         const bool res = (ref & kCoopRes) != 0u;
+        // 0. every entry that may expand issues its loads now, before the
+        // fold (whose t_best only culls more): a triangle or a record, both
+        // as buffer loads with an out-of-range offset for the other one --
+        // no branches, so a step costs one memory round trip whatever mix
+        // of leaves and records the group holds
+        const bool pre_leaf = act && !res && (ref & kWideLeaf) && etn <= tb;
+        const bool pre_rec = act && !res && !(ref & kWideLeaf) && etn <= tb;
+        const uint32_t to = pre_leaf ? (ref & ~kWideLeaf) * 48u : M.tbytes;
+        const uint32_t wo = pre_rec ? ref * 64u : M.wbytes;
+        const float4 T0 = bload_f4(M.tr, to), T1 = bload_f4(M.tr, to + 16), T2 = bload_f4(M.tr, to + 32);
+        const uint4 w0 = bload_u4(M.wr, wo), w1 = bload_u4(M.wr, wo + 16), w2 = bload_u4(M.wr, wo + 32),
+                    w3 = bload_u4(M.wr, wo + 48);
         // 1. fold the head run of resolved leaves, in preorder
         const uint64_t nonres = gballot<G>(act && !res, gbase);
         const uint32_t j = nonres ? (uint32_t)__builtin_ctzll(nonres) : m;
@@ -935,8 +948,6 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
                 h[0] = true;  // not at the head yet: stays pending
             } else if (ref & kWideLeaf) {
                 if (COUNT) ++ct;
-                const float4* tp = tri_s + (uint64_t)(ref & ~kWideLeaf) * 3;
-                const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
                 const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
                 float lo[3], hi[3], tn;
                 tri_bounds(tv, lo, hi);
@@ -949,8 +960,6 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
                 }
             } else {
                 if (COUNT) ++cn;
-                const uint4* wp = wnodes + (uint64_t)ref * 4;
-                const uint4 w0 = wp[0], w1 = wp[1], w2 = wp[2], w3 = wp[3];
                 float tn[4];
                 const bool wild = record_test(R, o, w0, w1, w2, h, tn);
                 const uint32_t flags = w0.w >> 24;
@@ -1880,7 +1889,8 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
         sched->prev_cam_valid = true;
     }
     // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
-    const uint32_t coop_cap = wide && sched && sched->coop_q ? (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) : 0u;
+    const uint32_t coop_cap = wide && sched && sched->coop_q && n <= kBufMaxN
+                                  ? (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) : 0u;
     CoopQ cq;
     if (coop_cap) {
         if (sched->coop_fresh) {
