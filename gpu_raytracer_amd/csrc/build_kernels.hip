@@ -562,14 +562,19 @@ __device__ __forceinline__ void kids_of(const uint4& tp, uint32_t L0, uint32_t& 
 //    below hi <= ohi, which the per-axis check `top` rejects (wild).
 // A NaN/inf anywhere makes the slot sum non-finite (so does an overflowing
 // sum of finite values: wild, which is only conservative).
-__device__ __forceinline__ bool quant_axis(float olo, float ohi, const float (&clo)[4], const float (&chi)[4],
-                                           uint32_t valid, uint32_t& qlo_w, uint32_t& qhi_w, int& e_out) {
+template <int W>
+__device__ __forceinline__ bool quant_axis(float olo, float ohi, const float (&clo)[W], const float (&chi)[W],
+                                           uint32_t valid, uint32_t (&qlo_w)[W / 4], uint32_t (&qhi_w)[W / 4],
+                                           int& e_out) {
     const float ext = ohi - olo;
     // callers pass X's own box in unused slots (inside [olo, ohi]); their
     // bytes are written as 0
-    const float(&lo)[4] = clo;
-    const float(&hi)[4] = chi;
-    const float chk = (((lo[0] + lo[1]) + (lo[2] + lo[3])) + ((hi[0] + hi[1]) + (hi[2] + hi[3]))) + ext;
+    const float(&lo)[W] = clo;
+    const float(&hi)[W] = chi;
+    float chk = ext;
+#pragma unroll
+    for (int i = 0; i < W; i += 4)
+        chk = chk + (((lo[i] + lo[i + 1]) + (lo[i + 2] + lo[i + 3])) + ((hi[i] + hi[i + 1]) + (hi[i + 2] + hi[i + 3])));
     if (!isfinite(chk) || !(ext >= 0.0f)) return false;
     const uint32_t be = (__float_as_uint(ext) >> 23) & 0xFF;  // ext normal: 2^(be-127) <= ext
     int e = (ext > 0.0f && be) ? (int)be - 134 : -126;
@@ -578,59 +583,81 @@ __device__ __forceinline__ bool quant_axis(float olo, float ohi, const float (&c
     if (e > 119) return false;
     const float sc = wide_scale(e);
     const bool top = !(wide_plane(olo, 255u, sc) < ohi);
-    uint32_t lw = 0, hw = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        float fl = floorf(ldexpf(lo[i] - olo, -e));
-        fl = fmaf(fl, sc, olo) > lo[i] ? fl - 1.0f : fl;
-        float fh = ceilf(ldexpf(hi[i] - olo, -e));
-        fh = fmaf(fh, sc, olo) < hi[i] ? fh + 1.0f : fh;
-        const bool v = (valid >> i) & 1u;
-        lw = __builtin_amdgcn_cvt_pk_u8_f32(v ? fl : 0.0f, (uint32_t)i, lw);
-        hw = __builtin_amdgcn_cvt_pk_u8_f32(v ? fh : 0.0f, (uint32_t)i, hw);
+    for (int wd = 0; wd < W / 4; ++wd) {
+        uint32_t lw = 0, hw = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * wd + j;
+            float fl = floorf(ldexpf(lo[i] - olo, -e));
+            fl = fmaf(fl, sc, olo) > lo[i] ? fl - 1.0f : fl;
+            float fh = ceilf(ldexpf(hi[i] - olo, -e));
+            fh = fmaf(fh, sc, olo) < hi[i] ? fh + 1.0f : fh;
+            const bool v = (valid >> i) & 1u;
+            lw = __builtin_amdgcn_cvt_pk_u8_f32(v ? fl : 0.0f, (uint32_t)j, lw);
+            hw = __builtin_amdgcn_cvt_pk_u8_f32(v ? fh : 0.0f, (uint32_t)j, hw);
+        }
+        qlo_w[wd] = lw;
+        qhi_w[wd] = hw;
     }
-    qlo_w = lw; qhi_w = hw; e_out = e;
+    e_out = e;
     return top;
 }
 
 // Quantize and store the wide record of internal node X from its box and the
-// boxes of its 2-4 children-or-grandchildren (node[] binary indices in
-// preorder, RT_SENT in unused slots); box_of(slot) fetches a child box (LDS
-// in K6, global in k_wide_cross).
-template <typename BoxOf>
+// boxes of its 2-W cut entries (node[] binary indices in preorder, RT_SENT in
+// unused slots); box_of(slot) fetches an entry's box (LDS in K6, global in
+// k_wide_cross).  Layouts: rt_device.h (K7w for W = 4, K7w8 for W = 8).  A
+// wild record (a plane not representable) gets exponent bytes 255 and zero
+// planes: the trace then takes every valid child.
+template <int W, typename BoxOf>
 __device__ __forceinline__ void store_wide(uint4* __restrict__ wnodes, uint32_t X, const Aabb& bx,
-                                           const uint32_t (&node)[4], BoxOf box_of, uint32_t L0) {
+                                           const uint32_t (&node)[W], BoxOf box_of, uint32_t L0) {
+    constexpr int QW = W / 4;
     uint32_t valid = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) valid |= (node[i] != RT_SENT ? 1u : 0u) << i;
-    float bl[3][4], bh[3][4];  // static indices only: no scratch
+    for (int i = 0; i < W; ++i) valid |= (node[i] != RT_SENT ? 1u : 0u) << i;
+    float bl[3][W], bh[3][W];  // static indices only: no scratch
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < W; ++i) {
         const Aabb b = box_of(i);
 #pragma unroll
         for (int c = 0; c < 3; ++c) { bl[c][i] = b.lo[c]; bh[c][i] = b.hi[c]; }
     }
-    uint32_t q[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t ql[3][QW], qh[3][QW];
     int e[3] = {0, 0, 0};
     bool wild = false;
 #pragma unroll
     for (int c = 0; c < 3; ++c)
-        if (!quant_axis(bx.lo[c], bx.hi[c], bl[c], bh[c], valid, q[c], q[3 + c], e[c])) wild = true;
+        if (!quant_axis<W>(bx.lo[c], bx.hi[c], bl[c], bh[c], valid, ql[c], qh[c], e[c])) wild = true;
+    uint32_t eb = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16);
     if (wild) {
-        q[0] = q[1] = q[2] = q[3] = q[4] = q[5] = 0;
-        e[0] = e[1] = e[2] = 0;
-    }
-    uint32_t ref[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int k = 0; k < QW; ++k) ql[c][k] = qh[c][k] = 0u;
+        eb = kWideWildExp | (kWideWildExp << 8) | (kWideWildExp << 16);
+    }
+    uint32_t ref[W];
+#pragma unroll
+    for (int i = 0; i < W; ++i)
         ref[i] = node[i] == RT_SENT ? RT_SENT : node[i] < L0 ? node[i] : (kWideLeaf | (node[i] - L0));
-    const uint32_t meta = (uint32_t)(e[0] + 127) | ((uint32_t)(e[1] + 127) << 8) | ((uint32_t)(e[2] + 127) << 16) |
-                          ((valid << 4 | (wild ? kWideWild : 0u)) << 24);
-    uint4* o = wnodes + (uint64_t)X * 4;
-    o[0] = make_uint4(__float_as_uint(bx.lo[0]), __float_as_uint(bx.lo[1]), __float_as_uint(bx.lo[2]), meta);
-    o[1] = make_uint4(q[0], q[1], q[2], q[3]);
-    o[2] = make_uint4(q[4], q[5], ref[0], ref[1]);
-    o[3] = make_uint4(ref[2], ref[3], 0u, 0u);
+    uint4* o = wnodes + (uint64_t)X * WideFmt<W>::words;
+    if constexpr (W == 4) {
+        const uint32_t meta = eb | ((valid << 4 | (wild ? kWideWild : 0u)) << 24);
+        o[0] = make_uint4(__float_as_uint(bx.lo[0]), __float_as_uint(bx.lo[1]), __float_as_uint(bx.lo[2]), meta);
+        o[1] = make_uint4(ql[0][0], ql[1][0], ql[2][0], qh[0][0]);
+        o[2] = make_uint4(qh[1][0], qh[2][0], ref[0], ref[1]);
+        o[3] = make_uint4(ref[2], ref[3], 0u, 0u);
+    } else {
+        const uint32_t meta = eb | (valid << 24);
+        o[0] = make_uint4(__float_as_uint(bx.lo[0]), __float_as_uint(bx.lo[1]), __float_as_uint(bx.lo[2]), meta);
+        o[1] = make_uint4(ql[0][0], ql[0][QW - 1], ql[1][0], ql[1][QW - 1]);
+        o[2] = make_uint4(ql[2][0], ql[2][QW - 1], qh[0][0], qh[0][QW - 1]);
+        o[3] = make_uint4(qh[1][0], qh[1][QW - 1], qh[2][0], qh[2][QW - 1]);
+        o[4] = make_uint4(ref[0], ref[1], ref[2], ref[3]);
+        o[5] = make_uint4(ref[4], ref[5], ref[6], ref[7]);
+    }
 }
 
 // The record's entries (4 slots, RT_SENT-padded); topo_of(i) gives internal
@@ -649,36 +676,49 @@ __device__ __forceinline__ float half_area(const Aabb& b) {
     return (dx * dy + dy * dz) + dz * dx;
 }
 
-template <typename TopoOf, typename BoxOfNode>
+template <int W, typename TopoOf, typename BoxOfNode>
 __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoOf topo_of, BoxOfNode box_of_node,
-                                             uint32_t collapse, uint32_t (&node)[4]) {
+                                             uint32_t collapse, uint32_t (&node)[W]) {
     uint32_t l, r;
     kids_of(tx, L0, l, r);
-    if (collapse == 1) {
-        node[0] = l; node[1] = r; node[2] = RT_SENT; node[3] = RT_SENT;
+    if (collapse == 1 || W != 4) {
+        // W - 2 greedy replacements; ar[] caches the entries' surfaces
+        // (internal entries only; leaves and empty slots are never picked)
+        float ar[W];
+        node[0] = l; node[1] = r;
 #pragma unroll
-        for (int step = 0; step < 2; ++step) {
+        for (int i = 2; i < W; ++i) node[i] = RT_SENT;
+        ar[0] = l < L0 ? half_area(box_of_node(l)) : 0.0f;
+        ar[1] = r < L0 ? half_area(box_of_node(r)) : 0.0f;
+#pragma unroll
+        for (int i = 2; i < W; ++i) ar[i] = 0.0f;
+#pragma unroll
+        for (int step = 0; step < W - 2; ++step) {
             int best = -1;
             float ba = 0.0f;
 #pragma unroll
-            for (int i = 0; i < 3; ++i) {  // slot 3 is still empty
-                if (node[i] < L0) {       // internal (RT_SENT and leaves are >= L0)
-                    const float a = half_area(box_of_node(node[i]));
-                    if (best < 0 || a > ba) { best = i; ba = a; }
+            for (int i = 0; i < step + 2; ++i) {  // slots past step + 1 are still empty
+                if (node[i] < L0) {               // internal (RT_SENT and leaves are >= L0)
+                    if (best < 0 || ar[i] > ba) { best = i; ba = ar[i]; }
                 }
             }
             if (best < 0) break;
             uint32_t pick = node[0];
 #pragma unroll
-            for (int i = 1; i < 3; ++i) pick = best == i ? node[i] : pick;
+            for (int i = 1; i < step + 2; ++i) pick = best == i ? node[i] : pick;
             uint32_t c0, c1;
             kids_of(topo_of(pick), L0, c0, c1);
-            uint32_t nn[4];
+            const float a0 = c0 < L0 ? half_area(box_of_node(c0)) : 0.0f;
+            const float a1 = c1 < L0 ? half_area(box_of_node(c1)) : 0.0f;
+            uint32_t nn[W];
+            float na[W];
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                nn[i] = i < best ? node[i] : i == best ? c0 : i == best + 1 ? c1 : node[i - 1];
+            for (int i = 0; i < W; ++i) {
+                nn[i] = i < best ? node[i] : i == best ? c0 : i == best + 1 ? c1 : node[i - 1 < 0 ? 0 : i - 1];
+                na[i] = i < best ? ar[i] : i == best ? a0 : i == best + 1 ? a1 : ar[i - 1 < 0 ? 0 : i - 1];
+            }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) node[i] = nn[i];
+            for (int i = 0; i < W; ++i) { node[i] = nn[i]; ar[i] = na[i]; }
         }
         return;
     }
@@ -689,7 +729,7 @@ __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoO
     node[0] = a0;
     node[1] = a1 != RT_SENT ? a1 : b0;
     node[2] = a1 != RT_SENT ? b0 : b1;
-    node[3] = a1 != RT_SENT ? b1 : RT_SENT;
+    node[3 % W] = a1 != RT_SENT ? b1 : RT_SENT;
 }
 
 // K4 + K6 local + K7w local, fused.  One block = kRefitT consecutive sorted
@@ -708,6 +748,7 @@ __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoO
 //      block in its atomic-arrival loop) and without re-reading the
 //      topology and parent arrays K4 used to write for it;
 //   4. coalesced stores of the local internal nodes and their K7w records.
+template <int W>
 __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restrict__ keys_g,
                                                         const uint32_t* __restrict__ svals,
                                                         const float* __restrict__ tris, uint32_t n,
@@ -823,15 +864,15 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
     if (local) {
         const Aabb bx = s_box[T + tid];
         store_node(nodes, k, bx, tp.x, tp.y);
-        uint32_t node[4];
+        uint32_t node[W];
         // every descendant of a local node is local: topology and boxes in LDS
-        wide_entries(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; },
-                     [&](uint32_t i) { return s_box[T + i - B0]; }, collapse, node);
-        uint32_t slot[4];
+        wide_entries<W>(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; },
+                        [&](uint32_t i) { return s_box[T + i - B0]; }, collapse, node);
+        uint32_t slot[W];
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < W; ++i)
             slot[i] = node[i] == RT_SENT ? T + tid : node[i] >= L0 ? node[i] - L0 - B0 : T + node[i] - B0;
-        store_wide(wnodes, k, bx, node, [&](int i) { return s_box[slot[i]]; }, L0);
+        store_wide<W>(wnodes, k, bx, node, [&](int i) { return s_box[slot[i]]; }, L0);
     }
     RT_STAMP(5);
 }
@@ -909,6 +950,7 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
 
 // K7w records of the crossing internal nodes, once K6t has written their
 // boxes (every box such a record needs is then final in `nodes`).
+template <int W>
 __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ topo, const uint32_t* __restrict__ cross,
                                                     const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
                                                     const void* __restrict__ nodes, uint32_t n,
@@ -926,12 +968,12 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         const uint32_t X = cross[sh * cross_cap + (q - pre[sh])];
         if (X >= L0) continue;
         const uint4 tx = topo[X];
-        uint32_t node[4];
-        wide_entries(tx, L0, [&](uint32_t i) { return topo[i]; }, [&](uint32_t i) { return load_aabb_node(nodes, i); },
-                     collapse, node);
+        uint32_t node[W];
+        wide_entries<W>(tx, L0, [&](uint32_t i) { return topo[i]; },
+                        [&](uint32_t i) { return load_aabb_node(nodes, i); }, collapse, node);
         const Aabb bx = load_aabb_node(nodes, X);
-        store_wide(wnodes, X, bx, node, [&](int i) { return load_aabb_node(nodes, node[i] == RT_SENT ? X : node[i]); },
-                   L0);
+        store_wide<W>(wnodes, X, bx, node,
+                      [&](int i) { return load_aabb_node(nodes, node[i] == RT_SENT ? X : node[i]); }, L0);
     }
 }
 
@@ -972,7 +1014,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.tri_s, N * 48);
     RT_ALLOC(b.parent, (2 * N - 1) * 4);
     RT_ALLOC(b.topo, N * 16);
-    RT_ALLOC(b.wnodes, N * 64);
+    RT_ALLOC(b.wnodes, N * kWideRecMaxBytes);  // either arity (build.wide_arity)
     RT_ALLOC(b.prebuf, N * 24);
     RT_ALLOC(b.sufbuf, N * 24);
     RT_ALLOC(b.table, (uint64_t)b.levels * b.m_blocks * 24);
@@ -1050,7 +1092,8 @@ static hipError_t ensure_cross_attr() {
     return err[dev];
 }
 
-static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, hipStream_t s) {
+static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
+                                hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     if (m <= 1) return hipGetLastError();
     if (m <= (uint32_t)kLdsTreeMaxBlocks) {
@@ -1070,28 +1113,43 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
         hipLaunchKernelGGL(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
-    hipLaunchKernelGGL(k_wide_cross, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr, cross_cap(m),
-                       b.nodes, n, b.wnodes, wide_collapse);
+    if (arity == 8)
+        hipLaunchKernelGGL(k_wide_cross<8>, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+                           cross_cap(m), b.nodes, n, b.wnodes, wide_collapse);
+    else
+        hipLaunchKernelGGL(k_wide_cross<4>, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+                           cross_cap(m), b.nodes, n, b.wnodes, wide_collapse);
     return hipGetLastError();
 }
 
 // K4 + K5 + K6-local + K7w-local (k_topo_refit) over sorted keys/vals in
 // keys[0]/vals[0]; expects the crossing-list counters zeroed (K0 does it).
-static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, hipStream_t s) {
-    if (!n) return hipSuccess;
+static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
+                                     uint32_t block0, uint32_t nblocks, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
-    hipLaunchKernelGGL(k_topo_refit, dim3(m), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
-                       (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
-                       cross_cap(m), b.wnodes, wide_collapse, 0u);
+    if (arity == 8)
+        hipLaunchKernelGGL(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
+                           b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0);
+    else
+        hipLaunchKernelGGL(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
+                           b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0);
     return hipGetLastError();
+}
+
+static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
+                                    hipStream_t s) {
+    if (!n) return hipSuccess;
+    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s);
 }
 
 hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
     const TraceConfig cfg = config_snapshot();
     hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
     if (e != hipSuccess) return e;
-    if ((e = launch_topo_local(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
-    return n ? launch_cross(b, n, cfg.wide_collapse, s) : hipSuccess;
+    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
+    return n ? launch_cross(b, n, cfg.wide_collapse, b.warity, s) : hipSuccess;
 }
 
 // ------------------------------------------- distributed build
@@ -1144,11 +1202,7 @@ hipError_t launch_dbuild_subtrees(const BuildBufs& b, uint32_t n, uint32_t block
     const TraceConfig cfg = config_snapshot();
     hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
     if (e != hipSuccess || !n || !nblocks) return e;
-    const uint32_t m = cdiv(n, kRefitT);
-    hipLaunchKernelGGL(k_topo_refit, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n, b.topo,
-                       (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross, b.zero + kZCrossCtr,
-                       cross_cap(m), b.wnodes, cfg.wide_collapse, block0);
-    return hipGetLastError();
+    return launch_topo_blocks(b, n, cfg.wide_collapse, b.warity, block0, nblocks, s);
 }
 
 uint32_t dbuild_cross_cap(uint32_t n) { return cross_cap(cdiv(n ? n : 1, kRefitT)); }
@@ -1157,7 +1211,7 @@ uint32_t refit_blocks(uint32_t n) { return n ? cdiv(n, kRefitT) : 0u; }
 // K6t + K7w of every crossing node, with the crossing list and counters
 // (b.cross / zero + kZCrossCtr) and every share's blocks in place
 hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s) {
-    return n ? launch_cross(b, n, config_snapshot().wide_collapse, s) : hipSuccess;
+    return n ? launch_cross(b, n, config_snapshot().wide_collapse, b.warity, s) : hipSuccess;
 }
 
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages) {
@@ -1184,9 +1238,9 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     else e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
     if (e != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;
-    if ((e = launch_topo_local(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
+    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
-    if (n && (e = launch_cross(b, n, cfg.wide_collapse, s)) != hipSuccess) return e;
+    if (n && (e = launch_cross(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
     if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K4/K6 (records written with the boxes)
     return hipSuccess;

@@ -248,6 +248,11 @@ rt_status primary(rt_scene* s, Replica** out) {
     return RT_OK;
 }
 
+// record arity of the next build of an n-triangle scene (build.wide_arity;
+// the 8-ary records' 32-bit buffer offsets need n <= 2^26) and record size
+uint32_t build_arity(uint32_t n) { return (rt::config_snapshot().wide_arity == 8 && n <= rt::kWide8MaxN) ? 8u : 4u; }
+uint64_t wide_bytes(uint32_t arity) { return arity == 8 ? 96u : 64u; }
+
 Replica* primary_built(const rt_scene* s) {
     return (!s->reps.empty() && s->reps[0]->built) ? s->reps[0].get() : nullptr;
 }
@@ -299,6 +304,7 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         RTR(upload(s, *r));
         HIPR(hipSetDevice(r->device));
         RTR(join_caller_work(*r));
+        r->bufs.warity = build_arity(s->n);
         hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
     }
@@ -417,7 +423,7 @@ rt_status need_built(rt_scene* s, Replica** out) {
 bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "trace.variant" && value >= 0 && value <= 2) c.variant = (uint32_t)value;
-    else if (k == "trace.stack_cap" && value >= 1 && value <= 14) c.stack_cap = (uint32_t)value;
+    else if (k == "trace.stack_cap" && value >= 0 && value <= 18) c.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) c.wg = (uint32_t)value;
     else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) c.wg_tiles = (uint32_t)value;
     else if (k == "trace.tile_order" && (value == 0 || value == 1)) c.tile_order = (uint32_t)value;
@@ -425,6 +431,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && (value == 0 || value == 1)) c.sort_msb = (uint32_t)value;
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
+    else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;
     else if (k == "timing.event_fence" && (value == 0 || value == 1)) c.event_fence = (uint32_t)value;
     else if (k == "path.wavefront" && (value == 0 || value == 1)) c.path_wave = (uint32_t)value;
@@ -681,7 +688,17 @@ rt_status rt_bvh_read_wide(const rt_scene* s, void* records) {
     if (!r) return fail(RT_EINVAL, "scene not built");
     HIPR(hipSetDevice(r->device));
     HIPR(hipStreamSynchronize(r->stream));
-    if (s->n >= 2) HIPR(hipMemcpy(records, r->bufs.wnodes, (size_t)(s->n - 1) * 64, hipMemcpyDeviceToHost));
+    if (s->n >= 2)
+        HIPR(hipMemcpy(records, r->bufs.wnodes, (size_t)(s->n - 1) * wide_bytes(r->bufs.warity),
+                       hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+rt_status rt_bvh_wide_arity(const rt_scene* s, uint32_t* arity_out) {
+    if (!s || !arity_out) return fail(RT_EINVAL, "null argument");
+    const Replica* r = primary_built(s);
+    if (!r) return fail(RT_EINVAL, "scene not built");
+    *arity_out = r->bufs.warity;
     return RT_OK;
 }
 
@@ -708,7 +725,8 @@ rt_status rt_bvh_replicas(const rt_scene* s, uint32_t max, int* devices, uint32_
 namespace {
 const char kBvhMagic[8] = {'R', 'T', 'B', 'V', 'H', '1', 0, 0};
 constexpr uint32_t kBvhVersion = 1;
-constexpr uint64_t kBvhLayout = 0x7274616d64000002ull;  // "rtamd" + layout revision 2
+constexpr uint64_t kBvhLayout = 0x7274616d64000002ull;   // "rtamd" + layout revision 2 (4-ary records)
+constexpr uint64_t kBvhLayout8 = 0x7274616d64000082ull;  // the same with 8-ary (K7w8) records
 
 uint64_t fnv1a(const void* p, size_t bytes) {
     const unsigned char* b = static_cast<const unsigned char*>(p);
@@ -733,7 +751,7 @@ std::vector<BvhSection> bvh_sections(const rt_scene* s, const Replica& r) {
             {r.bufs.vals[0], n * 4},
             {r.bufs.nodes, tot * 32},
             {r.bufs.tri_s, n * 48},
-            {r.bufs.wnodes, n >= 2 ? (n - 1) * 64 : 0}};
+            {r.bufs.wnodes, n >= 2 ? (n - 1) * wide_bytes(r.bufs.warity) : 0}};
 }
 
 struct File {
@@ -755,7 +773,8 @@ rt_status rt_bvh_save(const rt_scene* s, const char* path) {
     FILE* f = std::fopen(path, "wb");
     if (!f) return fail(RT_EIO, std::string("cannot create ") + path);
     const uint32_t hv[2] = {kBvhVersion, s->n};
-    const uint64_t hh[2] = {fnv1a(s->tris.data(), s->tris.size() * sizeof(float)), kBvhLayout};
+    const uint64_t hh[2] = {fnv1a(s->tris.data(), s->tris.size() * sizeof(float)),
+                            r->bufs.warity == 8 ? kBvhLayout8 : kBvhLayout};
     bool ok = std::fwrite(kBvhMagic, 1, 8, f) == 8 && std::fwrite(hv, 4, 2, f) == 2 && std::fwrite(hh, 8, 2, f) == 2;
     std::vector<unsigned char> host;
     for (const BvhSection& sec : bvh_sections(s, *r)) {
@@ -782,7 +801,7 @@ rt_status rt_bvh_load(rt_scene* s, const char* path) {
     const bool hdr =
         std::fread(magic, 1, 8, f.f) == 8 && std::fread(hv, 4, 2, f.f) == 2 && std::fread(hh, 8, 2, f.f) == 2;
     if (!hdr || std::memcmp(magic, kBvhMagic, 8) != 0) return fail(RT_EIO, std::string(path) + ": not an RTBVH1 file");
-    if (hv[0] != kBvhVersion || hh[1] != kBvhLayout)
+    if (hv[0] != kBvhVersion || (hh[1] != kBvhLayout && hh[1] != kBvhLayout8))
         return fail(RT_EIO, std::string(path) + ": BVH cache from another library layout");
     if (hv[1] != s->n || hh[0] != fnv1a(s->tris.data(), s->tris.size() * sizeof(float)))
         return fail(RT_EINVAL, std::string(path) + ": BVH cache was built for different triangles");
@@ -796,6 +815,8 @@ rt_status rt_bvh_load(rt_scene* s, const char* path) {
     // leaves the scene unbuilt (and every other replica is now stale)
     r->built = false;
     for (size_t i = 1; i < s->reps.size(); ++i) s->reps[i]->built = false;
+    r->bufs.warity = hh[1] == kBvhLayout8 ? 8u : 4u;
+    if (r->bufs.warity == 8 && s->n > rt::kWide8MaxN) return fail(RT_EIO, std::string(path) + ": bad record arity");
     std::vector<unsigned char> host;
     for (const BvhSection& sec : bvh_sections(s, *r)) {
         if (!sec.bytes) continue;
@@ -816,7 +837,9 @@ rt_status rt_bvh_prepare(rt_scene* s) {
     if (!s) return fail(RT_EINVAL, "null scene");
     Replica* r = nullptr;
     RTR(primary(s, &r));
-    return upload(s, *r);
+    RTR(upload(s, *r));
+    r->bufs.warity = build_arity(s->n);  // the sender's (same configuration on every rank)
+    return RT_OK;
 }
 
 rt_status rt_bvh_device_sections(rt_scene* s, uint32_t max, void** ptrs, uint64_t* bytes, uint32_t* count_out) {
@@ -937,7 +960,8 @@ rt_status render_tiled(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h
         if (r) HIPR(hipStreamWaitEvent(R.stream, root.r0, 0));
         rt::TileSched* sched = nullptr;
         RTR(sched_for(R, w, h, spp, r, P, &sched));
-        hipError_t e = rt::launch_trace(R.bufs.nodes, R.bufs.wnodes, R.bufs.tri_s, s->n, camf(cam), w, h, spp, r, P,
+        hipError_t e = rt::launch_trace(R.bufs.nodes, R.bufs.wnodes, R.bufs.warity,
+                                        R.bufs.tri_s, s->n, camf(cam), w, h, spp, r, P,
                                         true, hits_out ? R.d_slab_hits : nullptr, R.d_slab, nullptr, false, R.d_work,
                                         sched, R.stream);
         if (e != hipSuccess) return hip_fail(e, "launch_trace");
@@ -1014,7 +1038,8 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     rt::TileSched* sched = nullptr;
     RTR(sched_for(*r, w, h, spp, 0, 1, &sched));
     HIPR(hipEventRecord(r->r0, r->stream));
-    hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
+    hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
+                                    r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
                                     false, hits_out ? r->d_hits : nullptr, r->d_rgba, nullptr, false, r->d_work, sched,
                                     r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
@@ -1065,7 +1090,8 @@ rt_status rt_render_shadow_device(rt_scene* s, const rt_camera* cam, const float
     Replica* r = nullptr;
     RTR(need_built(s, &r));
     return device_launch(*r, stream, ms_out, "launch_trace_shadow", [&](hipStream_t hs) {
-        return rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, r->bufs.tris, s->n, camf(cam), w,
+        return rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
+                                       r->bufs.tri_s, r->bufs.tris, s->n, camf(cam), w,
                                        h, spp, light, ambient, d_hits, d_rgba, nullptr, hs);
     });
 }
@@ -1096,7 +1122,8 @@ rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float l
     RTR(join_caller_work(*r));
     if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
     HIPR(hipMemsetAsync(r->d_ctr, 0, 16, r->stream));
-    hipError_t e = rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, r->bufs.tris, s->n, camf(cam),
+    hipError_t e = rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
+                                           r->bufs.tri_s, r->bufs.tris, s->n, camf(cam),
                                            w, h, spp, light, ambient, nullptr, nullptr, r->d_ctr, r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace_shadow");
     HIPR(hipStreamSynchronize(r->stream));
@@ -1130,11 +1157,13 @@ static hipError_t path_launch(rt_scene* s, Replica& r, const rt_camera* cam, con
                 return e;
             }
         }
-        return rt::launch_path_wavefront(r.bufs.nodes, r.bufs.wnodes, r.bufs.tri_s, r.bufs.tris, r.bufs.params, s->n,
+        return rt::launch_path_wavefront(r.bufs.nodes, r.bufs.wnodes, r.bufs.warity,
+                                         r.bufs.tri_s, r.bufs.tris, r.bufs.params, s->n,
                                          camf(cam), w, h, spp, light, sky, max_depth, d_hits, d_rgba, ctr, r.path,
                                          cfg.path_sort, hs);
     }
-    return rt::launch_trace_path(r.bufs.nodes, r.bufs.wnodes, r.bufs.tri_s, r.bufs.tris, s->n, camf(cam), w, h, spp,
+    return rt::launch_trace_path(r.bufs.nodes, r.bufs.wnodes, r.bufs.warity,
+                                 r.bufs.tri_s, r.bufs.tris, s->n, camf(cam), w, h, spp,
                                  light, sky, max_depth, d_hits, d_rgba, ctr, hs);
 }
 
@@ -1206,7 +1235,8 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     // it is on (trace.coop_cap*), which needs the frame shape's queue
     rt::TileSched* sched = nullptr;
     if (!binary) RTR(sched_for(*r, w, h, spp, rank, nranks, &sched));
-    hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
+    hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
+                                    r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
                                     nranks, packed, nullptr, nullptr, r->d_ctr, binary, r->d_work, sched, r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(r->stream));
@@ -1263,7 +1293,8 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     rt::TileSched* sched = nullptr;
     RTR(sched_for(*r, w, h, spp, 0, 1, &sched));
     RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
-        return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
+        return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
+                                r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
                                 d_hits, d_rgba, nullptr, false, r->d_work, sched, hs);
     }));
     sched_done(*r, cfg);
@@ -1285,7 +1316,8 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     rt::TileSched* sched = nullptr;
     RTR(sched_for(*r, w, h, spp, rank, nranks, &sched));
     RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
-        return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks,
+        return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
+                                r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks,
                                 true, d_packed_hits, d_packed_rgba, nullptr, false, r->d_work, sched, hs);
     }));
     sched_done(*r, cfg);
@@ -1423,6 +1455,7 @@ rt_status rt_stage_refit(int device, const uint32_t* sorted_keys, const uint32_t
         rt::BuildBufs& b;
         ~Guard() { rt::free_build(b); }
     } guard{b};
+    b.warity = build_arity(n);
     HIPR(hipMemcpy(b.tris, tris, (size_t)n * 36, hipMemcpyHostToDevice));
     HIPR(hipMemcpy(b.keys[0], sorted_keys, (size_t)n * 4, hipMemcpyHostToDevice));
     HIPR(hipMemcpy(b.vals[0], sorted_vals, (size_t)n * 4, hipMemcpyHostToDevice));
@@ -1453,7 +1486,7 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
     HIPR(dts.alloc((size_t)(n ? n : 1) * 48));
     HIPR(dw.alloc(4096));
     HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
-    HIPR(rt::launch_trace(dn.p, nullptr, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
+    HIPR(rt::launch_trace(dn.p, nullptr, 4u, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
                           counters ? dc.as<unsigned long long>() : nullptr, true, dw.as<uint32_t>(), nullptr, 0));
     HIPR(hipDeviceSynchronize());
     if (hits) HIPR(hipMemcpy(hits, dh.p, nh * 16, hipMemcpyDeviceToHost));
@@ -1638,6 +1671,7 @@ rt_status rt_dbuild_subtrees(rt_scene* s, uint32_t rank, uint32_t nranks, uint32
     RTR(dbuild_replica(s, rank, nranks, &r));
     uint32_t sh[6];
     RTR(rt_dbuild_shares(s->n, rank, nranks, sh));
+    r->bufs.warity = build_arity(s->n);
     HIPR(rt::launch_dbuild_subtrees(r->bufs, s->n, sh[2], sh[3] - sh[2], r->stream));
     uint32_t ctr[rt::kCrossShards];
     HIPR(hipMemcpyAsync(ctr, r->bufs.zero + rt::kZCrossCtr, sizeof(ctr), hipMemcpyDeviceToHost, r->stream));
@@ -1696,7 +1730,7 @@ rt_status rt_dbuild_buffer(rt_scene* s, int which, void** ptr, uint64_t* bytes) 
         case RT_DB_VALS: *ptr = r.bufs.vals[0]; *bytes = n * 4; break;
         case RT_DB_NODES: *ptr = r.bufs.nodes; *bytes = tot * 32; break;
         case RT_DB_TRI_S: *ptr = r.bufs.tri_s; *bytes = n * 48; break;
-        case RT_DB_WIDE: *ptr = r.bufs.wnodes; *bytes = ni * 64; break;
+        case RT_DB_WIDE: *ptr = r.bufs.wnodes; *bytes = ni * wide_bytes(r.bufs.warity); break;
         case RT_DB_TOPO: *ptr = r.bufs.topo; *bytes = ni * 16; break;
         case RT_DB_PRE: *ptr = r.bufs.prebuf; *bytes = n * 24; break;
         case RT_DB_SUF: *ptr = r.bufs.sufbuf; *bytes = n * 24; break;

@@ -92,10 +92,39 @@ constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree c
 //   w3 = {ref2, ref3, 0, 0}        ref = internal X, or kWideLeaf | k
 constexpr uint32_t kWideLeaf = 0x80000000u;
 constexpr uint32_t kWideWild = 1u;
+// A wild record (build.wide_arity 4 and 8) also carries exponent bytes 255:
+// its grid step is +inf, so the trace's slack is infinite and every valid
+// child counts as hit whatever the planes say (record_test).
+constexpr uint32_t kWideWildExp = 255u;
 // per-ray LDS stack entries (+1 spare slot, 6 B each, x 256 threads = 22.5 KB
 // per workgroup: the 7 workgroups per CU the kernel's registers allow);
 // overflow -> exact binary traversal from the overflowing record
 constexpr int kWideStack = 14;
+
+// ---- K7w8: the 8-ary form (build.wide_arity = 8, SURVEY.md §8(f) row 1's
+// "4/8-wide").  Record X holds up to 8 entries of X's greedy
+// largest-surface cut (2-8 entries in §9.7 preorder), 96 B:
+//   w0 = {origin.x, origin.y, origin.z, meta}  meta: e+127 per axis in bytes
+//        0..2 (255 on every axis: wild); byte 3 = valid-child mask
+//   w1 = {qlo.x[0..3], qlo.x[4..7], qlo.y[0..3], qlo.y[4..7]}
+//   w2 = {qlo.z[0..3], qlo.z[4..7], qhi.x[0..3], qhi.x[4..7]}
+//   w3 = {qhi.y[0..3], qhi.y[4..7], qhi.z[0..3], qhi.z[4..7]}
+//   w4 = {ref0..ref3}, w5 = {ref4..ref7}
+// A traversal step over it replaces up to three binary levels (two for the
+// 4-ary form): the heaviest rays' dependent fetch chains are ~25 % shorter
+// (tools/wide_sim.py).  Its per-ray stacks hold 18 entries (a record pushes
+// up to 7).
+template <int W> struct WideFmt;
+template <> struct WideFmt<4> {
+    static constexpr uint32_t words = 4, bytes = 64;
+    static constexpr int stack = kWideStack;
+};
+template <> struct WideFmt<8> {
+    static constexpr uint32_t words = 6, bytes = 96;
+    static constexpr int stack = 18;
+};
+constexpr int kWideStackMax = 18;
+constexpr uint32_t kWideRecMaxBytes = 96;  // wnodes is allocated for either arity
 constexpr uint32_t kPoolCounters = 32;  // pool-trace unit counters, 128 B apart (work buffer >= 4 KiB)
 
 // plane = origin + q * 2^e, rounded once: q * 2^e is exact (q < 2^8 and

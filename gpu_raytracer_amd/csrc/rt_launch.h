@@ -20,7 +20,8 @@ struct BuildBufs {
     float4* tri_s = nullptr;        // n x 48 B leaf-ordered {v0, e1, e2} for the trace
     uint32_t* parent = nullptr;     // 2n-1, unified index space
     uint4* topo = nullptr;          // n-1 x {left, esc, range_lo, range_hi}
-    uint4* wnodes = nullptr;        // n-1 x 64 B wide (4-ary) trace records, K7w
+    uint4* wnodes = nullptr;        // n-1 x 64 B (K7w, 4-ary) or 96 B (K7w8, 8-ary) wide trace records
+    uint32_t warity = 4;            // the arity wnodes was (or is being) built with: 4 or 8
     uint32_t* counts = nullptr;     // 4 x [tile][256] radix-sort tile digit counts (MSB: [tile][1024])
     uint32_t* bstart = nullptr;     // [1025] MSB bucket starts
     float* prebuf = nullptr;        // n x 6: block-prefix AABB at crossing ends
@@ -94,7 +95,8 @@ struct TraceConfig {
     uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
     uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
     uint32_t wg_tiles = 64;     // same, for one rank's tiles of a multi-GPU frame (nranks > 1)
-    uint32_t stack_cap = 14;    // wide stack entries used, <= kWideStack (tests force the overflow path)
+    uint32_t stack_cap = 0;     // wide stack entries used (tests force the overflow path); 0 = the arity's
+                                // whole stack (14 entries for 4-ary records, 18 for 8-ary)
     uint32_t path_wave = 1;     // path mode: 0 megakernel, 1 wavefront (default: faster on soup-1M and Sponza)
     uint32_t path_wg = 64;      // path megakernel: threads per block (64 = 8x8 quadrant, 256 = 16x16 tile)
     uint32_t path_sort = 0;     // wavefront: top key bytes the ray queue is sorted by (0 = unsorted, default)
@@ -105,6 +107,7 @@ struct TraceConfig {
     uint32_t px_sort = 1;       // with tile_order: each tile's pixels to lanes costliest first (previous
                                 // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
+    uint32_t wide_arity = 4;    // build.wide_arity: 4 = K7w 64-B records, 8 = K7w8 96-B records (greedy cut)
     uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbMaxN, 0 = 4-pass LSB always
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
@@ -118,7 +121,8 @@ struct TraceConfig {
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };
 
-constexpr uint32_t kCoopEntryBytes = 176;  // heavy-ray queue entry (trace_kernels.hip kCoopEntry x 16 B)
+constexpr uint32_t kCoopEntryBytes = 208;  // heavy-ray queue entry (trace_kernels.hip kCoopEntry x 16 B)
+constexpr uint32_t kWide8MaxN = 1u << 26;  // 8-ary records need 32-bit buffer offsets ((n-1) x 96 B)
 
 // Per-launch tile scheduling state (owned by the scene, one per frame shape).
 struct TileSched {
@@ -152,19 +156,23 @@ constexpr int kMaxDevices = 64;
 // binary_counts the kernel is the binary one, so `counters` are the §9.7
 // node/triangle counts the oracle reports; otherwise they count the running
 // kernel's own fetches (wide: records and triangle loads).
-hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tri_s, uint32_t n, const CamF& cam,
+// warity: the arity wnodes holds (BuildBufs::warity).
+hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s, uint32_t n,
+                        const CamF& cam,
                         uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
                         void* hits, void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
                         TileSched* sched, hipStream_t s);
 // Shadow mode: primary hits into `hits`, Lambert + shadow-ray
 // shaded image into `rgba`; tris = the scene's AoS triangles (normals).
-hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s,
+                               const float* tris,
                                uint32_t n, const CamF& cam, uint32_t w, uint32_t h, uint32_t spp,
                                const float light[3], float ambient, void* hits, void* rgba,
                                unsigned long long* counters, hipStream_t s);
 // Path mode: primary hits into `hits`, diffuse-path image into
 // `rgba`; counters (nullable): [0] node records, [1] tri records, [2] rays.
-hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s,
+                             const float* tris,
                              uint32_t n, const CamF& cam, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
                              float sky, uint32_t max_depth, void* hits, void* rgba, unsigned long long* counters,
                              hipStream_t s);
@@ -186,7 +194,8 @@ hipError_t alloc_path(PathBufs& b, uint32_t cap);
 void free_path(PathBufs& b);
 // sort_digits: 0 = trace the queue in emission order; 1..4 = stable LSB radix
 // sort of the queue by the top `sort_digits` bytes of the ray key first.
-hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
+hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s,
+                                 const float* tris,
                                  const BuildParams* params, uint32_t n, const CamF& cam, uint32_t w, uint32_t h,
                                  uint32_t spp, const float light[3], float sky, uint32_t max_depth, void* hits,
                                  void* rgba, unsigned long long* counters, PathBufs& pb, uint32_t sort_digits,

@@ -175,20 +175,47 @@ __device__ __forceinline__ bool slab_hit(const float* lo, const float* hi, const
 // truncation rounds down and the skip test stays conservative).  Slot `cap`
 // is the spare that takes the writes of children that are not pushed.
 struct WRay {
-    float d[3], invd[3], oslack[3];
+    float d[3], invd[3], kn[3], kf[3];  // kn/kf: the record test's per-ray offsets (record_test)
     float tb, hu, hv, ctn;
     uint32_t hp, cur, pend, sp, steps;
     bool fin;  // 1/d finite on every axis: the wide traversal applies
 };
 
-__device__ __forceinline__ void wray_init(const float* o, const float* d, WRay& R) {
+// The scene box (the binary root's, internal node 0, for n >= 2): every
+// record's origin and grid lie inside it, which bounds the record test's
+// rounding per ray instead of per record (record_test).
+struct SceneBox { float lo[3], hi[3]; };
+__device__ __forceinline__ float uniform_f(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ SceneBox scene_box(const void* nodes) {
+    const float4* p = reinterpret_cast<const float4*>(nodes);
+    const float4 a = p[0], b = p[1];  // the same address in every lane: kept in SGPRs
+    return SceneBox{{uniform_f(a.x), uniform_f(a.y), uniform_f(a.z)}, {uniform_f(a.w), uniform_f(b.x), uniform_f(b.y)}};
+}
+
+// R.fin: 1/d finite on every axis and the record-test slack finite and
+// small -- the wide traversal applies (else the binary one from the root).
+__device__ __forceinline__ void wray_init(const float* o, const float* d, WRay& R, const SceneBox& sb) {
+    bool ok = true;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         R.d[c] = d[c];
-        R.invd[c] = 1.0f / d[c];
-        R.oslack[c] = fmaf(fabsf(o[c] * R.invd[c]), 0x1p-20f, 0x1p-126f);  // record_test's |o/d| term
+        const float inv = 1.0f / d[c];
+        R.invd[c] = inv;
+        const float ai = fabsf(inv);
+        const float oi = o[c] * inv;
+        // |a| = |(org - o) / d| for any record origin org in the scene box,
+        // and 256 |B| = 256 * 2^e / |d| <= 4 * extent / |d| (quant_axis picks
+        // 2^e <= extent / 64 unless 2^e = 2^-126)
+        const float M = fmaxf(fabsf(sb.lo[c] - o[c]), fabsf(sb.hi[c] - o[c])) * ai;
+        const float B256 = fmaxf((sb.hi[c] - sb.lo[c]) * 4.0f, 0x1p-118f) * ai;
+        const float dl = fmaf((M + B256) + fabsf(oi), 0x1p-19f, 0x1p-125f);
+        ok = ok && isfinite(inv) && dl < 0x1p90f;  // false for NaN and infinities too
+        R.kn[c] = -oi - dl;
+        R.kf[c] = -oi + dl;
     }
-    R.fin = isfinite(R.invd[0]) && isfinite(R.invd[1]) && isfinite(R.invd[2]);
+    R.fin = ok;
     R.tb = __builtin_inff(); R.hu = 0.0f; R.hv = 0.0f; R.hp = RT_SENT;
     R.cur = 0; R.pend = RT_SENT; R.ctn = 0.0f; R.sp = 0; R.steps = 0;
 }
@@ -209,72 +236,103 @@ __device__ __forceinline__ void ray_dir(const Cam& cam, uint32_t x, uint32_t y, 
 }
 
 __device__ __forceinline__ void wray_setup(const Cam& cam, uint32_t x, uint32_t y, uint32_t W, uint32_t spp,
-                                           uint32_t s, WRay& R) {
+                                           uint32_t s, WRay& R, const SceneBox& sb) {
     float d[3];
     ray_dir(cam, x, y, W, spp, s, d);
-    wray_init(cam.eye, d, R);
+    wray_init(cam.eye, d, R, sb);
 }
 
 __device__ __forceinline__ uint32_t bin_of(uint32_t ref, uint32_t L0) {
     return (ref & kWideLeaf) ? L0 + (ref & ~kWideLeaf) : ref;
 }
 
-// Conservative slab test of a record's four quantized child boxes, in
-// about half the VALU of the §9.7 formula (this is the traversal's inner
-// loop, and the kernel is VALU-issue bound).  Child plane p = org + q*2^e, so
-// §9.7's (p - o)*invd is computed as fma(q, B, A) with the per-record
-// A = (org - o)*invd and B = 2^e*invd, and each axis's near/far plane is
-// picked once per record by the sign of invd (q_lo <= q_hi for every valid
-// child), replacing 6 sub + 6 mul + 6 min/max per child by 6 fma.
+// Conservative slab test of a record's quantized child boxes, in about a
+// third of the VALU of the §9.7 formula (this is the traversal's inner loop,
+// and the kernel is VALU-issue bound).  Child plane p = org + q*2^e, so §9.7's
+// (p - o)*invd is computed as fma(q, B, A') with B = 2^e*invd and, per record
+// and axis, A' = fma(org, invd, K) = (org - o)*invd -/+ dl (K = -o*invd -/+ dl
+// per ray, R.kn / R.kf); each axis's near/far plane is picked once per record
+// by the sign of invd (q_lo <= q_hi for every valid child).
 //
 // Exactness.  The internal-node tests only prune; the traversal stays exact
 // as long as a child is entered whenever §9.7's test of the child's EXACT box
-// b would hit (see the wide_step comment).  The fma form differs from §9.7 on
-// b by rounding: from A (2 roundings, <= 2u|A|), the fma (u|t|, |t| <=
-// |A| + 255|B|), §9.7's own two roundings (2u|t|), and the gap between the
-// real plane org + q*2^e and its rounded value, which the build compared with
-// b (<= u(|org| + 256*2^e)|invd| <= u(|A| + |o*invd| + 256|B|)); u = 2^-24.
-// In total less than u(6|A| + |o*invd| + 1021|B|) + denormal terms, so
-// widening each axis's interval by
-//     delta = 2^-20 (|A| + 256|B| + |o*invd|) + 2^-126
-// (16x that, R.oslack holds the ray's |o*invd| term) makes tn_fast <= tn_97
-// and tf_fast >= tf_97: a child §9.7 enters is always entered, and the stack
-// entry distance tn_fast stays a lower bound of §9.7's.  A record whose
-// delta is not small (huge 1/d, infinities) is treated as wild: every valid
-// child counts as hit with entry distance 0.  Returns that wild flag.
-__device__ __forceinline__ bool record_test(const WRay& R, const float* o, const uint4& w0, const uint4& w1,
-                                            const uint4& w2, bool (&hit)[4], float (&tn)[4]) {
+// b would hit (see the wide_step comment).  With a = (org - o)*invd (real),
+// u = 2^-24: A' differs from a -/+ dl by <= u(|a| + 2|o*invd| + 2dl) (the
+// roundings of o*invd, K and the fma); the child fma adds u|t| (|t| <= |a| +
+// 255|B| + dl); §9.7's own two roundings 2u|t|; and the real plane org + q*2^e
+// differs from its rounded value, which the build compared with b, by <=
+// u(|a| + |o*invd| + 256|B|).  In total less than u(5|a| + 3|o*invd| +
+// 1021|B| + 3dl) + denormal terms.  wray_init takes
+//     dl = 2^-19 (M + 256 Bmax + |o*invd|) + 2^-125
+// with M >= |a| and Bmax >= |B| for every record of the scene (its origin and
+// grid lie in the scene box), 32x the bound's |a|, |o*invd| and 8x its |B|
+// weight: tn_fast <= tn_97 and tf_fast >= tf_97, so a child §9.7 enters is
+// always entered and the stack entry distance stays a lower bound of §9.7's.
+// (The r01 form computed dl per record from the record's own A and B: 15
+// more VALU per record for a slack ~2^-19 of the scene size narrower.)  A
+// wild record (rt_device.h) has exponent bytes 255 and zero planes: B = +-inf,
+// fma(0, inf, A') = NaN on every axis, and the NaN-ignoring min/max give
+// tn = 0 <= tf = tb: every valid child is hit with entry distance 0.
+//
+// W = 8 (K7w8, rt_device.h): the same test over 8 children whose plane
+// bytes sit in two words per plane.
+template <int W>
+__device__ __forceinline__ void record_test(const WRay& R, const uint4 (&w)[WideFmt<W>::words], bool (&hit)[W],
+                                            float (&tn)[W]) {
+    constexpr int QW = W / 4;
+    const uint4 w0 = w[0];
     const float org[3] = {__uint_as_float(w0.x), __uint_as_float(w0.y), __uint_as_float(w0.z)};
-    const uint32_t qlo[3] = {w1.x, w1.y, w1.z}, qhi[3] = {w1.w, w2.x, w2.y};
+    uint32_t qlo[3][QW], qhi[3][QW];
+    if constexpr (W == 4) {
+        qlo[0][0] = w[1].x; qlo[1][0] = w[1].y; qlo[2][0] = w[1].z;
+        qhi[0][0] = w[1].w; qhi[1][0] = w[2].x; qhi[2][0] = w[2].y;
+    } else {
+        qlo[0][0] = w[1].x; qlo[0][QW - 1] = w[1].y; qlo[1][0] = w[1].z; qlo[1][QW - 1] = w[1].w;
+        qlo[2][0] = w[2].x; qlo[2][QW - 1] = w[2].y; qhi[0][0] = w[2].z; qhi[0][QW - 1] = w[2].w;
+        qhi[1][0] = w[3].x; qhi[1][QW - 1] = w[3].y; qhi[2][0] = w[3].z; qhi[2][QW - 1] = w[3].w;
+    }
     float An[3], Af[3], B[3];
-    uint32_t qn[3], qf[3];
-    float dmax = 0.0f;
+    uint32_t qn[3][QW], qf[3][QW];
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         const float scl = __uint_as_float(((w0.w >> (8 * c)) & 0xFFu) << 23);  // 2^e
         B[c] = scl * R.invd[c];
-        const float A = (org[c] - o[c]) * R.invd[c];
-        const float dl = fmaf(fabsf(A), 0x1p-20f, fmaf(fabsf(B[c]), 0x1p-12f, R.oslack[c]));
-        dmax = fmaxf(dmax, dl);
-        An[c] = A - dl;
-        Af[c] = A + dl;
+        An[c] = fmaf(org[c], R.invd[c], R.kn[c]);
+        Af[c] = fmaf(org[c], R.invd[c], R.kf[c]);
         const bool neg = R.invd[c] < 0.0f;
-        qn[c] = neg ? qhi[c] : qlo[c];
-        qf[c] = neg ? qlo[c] : qhi[c];
+#pragma unroll
+        for (int k = 0; k < QW; ++k) {
+            qn[c][k] = neg ? qhi[c][k] : qlo[c][k];
+            qf[c][k] = neg ? qlo[c][k] : qhi[c][k];
+        }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < W; ++i) {
         float tnear[3], tfar[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            tnear[c] = fmaf((float)((qn[c] >> (8 * i)) & 0xFFu), B[c], An[c]);
-            tfar[c] = fmaf((float)((qf[c] >> (8 * i)) & 0xFFu), B[c], Af[c]);
+            tnear[c] = fmaf((float)((qn[c][i >> 2] >> (8 * (i & 3))) & 0xFFu), B[c], An[c]);
+            tfar[c] = fmaf((float)((qf[c][i >> 2] >> (8 * (i & 3))) & 0xFFu), B[c], Af[c]);
         }
         tn[i] = fmaxf(fmaxf(fmaxf(tnear[0], tnear[1]), tnear[2]), 0.0f);
         const float tf = fminf(fminf(fminf(tfar[0], tfar[1]), tfar[2]), R.tb);
         hit[i] = tn[i] <= tf;
     }
-    return !(dmax < 0x1p90f);  // also true for NaN
+}
+
+// valid-child mask and child refs of a record (layouts: rt_device.h)
+template <int W>
+__device__ __forceinline__ uint32_t rec_mask(const uint4 (&w)[WideFmt<W>::words]) {
+    return W == 4 ? (w[0].w >> 28) & 0xFu : w[0].w >> 24;
+}
+template <int W>
+__device__ __forceinline__ uint32_t rec_ref(const uint4 (&w)[WideFmt<W>::words], int i) {
+    if constexpr (W == 4) {
+        return i == 0 ? w[2].z : i == 1 ? w[2].w : i == 2 ? w[3].x : w[3].y;
+    } else {
+        const uint4 v = w[4 + (i >> 2)];
+        return (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
+    }
 }
 
 template <int NT>
@@ -302,7 +360,7 @@ __device__ __forceinline__ void wide_pop(WRay& R, const uint32_t* sref, const ui
 // branches the compiler has no phi copies of half-arrived registers to make
 // and issues both loads before waiting for either: one round trip per step
 // where the flat form (a copy of the triangle's registers before the record
-// loads are issued) took two.  32-bit offsets: (n - 1) * 64 and n * 48 bytes
+// loads are issued) took two.  32-bit offsets: (n - 1) * 96 and n * 48 bytes
 // must fit (n <= 2^26; the launcher uses the flat form above that).
 struct WideMem {
     __amdgpu_buffer_rsrc_t wr, tr;
@@ -310,9 +368,10 @@ struct WideMem {
 };
 constexpr uint32_t kBufMaxN = 1u << 26;
 
+template <int W = 4>
 __device__ __forceinline__ WideMem wide_mem(const uint4* wnodes, const float4* tri_s, uint32_t n) {
     WideMem m;
-    m.wbytes = n >= 2 ? (n - 1) * 64u : 0u;
+    m.wbytes = n >= 2 ? (n - 1) * WideFmt<W>::bytes : 0u;
     m.tbytes = n * 48u;
     m.wr = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(wnodes), 0, (int)m.wbytes, 0x00020000);
     m.tr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float4*>(tri_s), 0, (int)m.tbytes, 0x00020000);
@@ -325,7 +384,7 @@ __device__ __forceinline__ float4 bload_f4(__amdgpu_buffer_rsrc_t r, uint32_t of
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
 
-template <bool COUNT, int NT, bool ANY = false, bool MTF = false, bool BUF = false>
+template <bool COUNT, int NT, bool ANY = false, bool MTF = false, bool BUF = false, int W = 4>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
                                          uint32_t& cn, uint32_t& ct, bool any = ANY, const WideMem* M = nullptr) {
@@ -343,19 +402,23 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     // both addresses before any load: with a load in flight, a register
     // the compiler reuses for the second address would force a wait for the
     // first load, and the triangle and the record would cost two round trips
-    const uint4* wp = wnodes + (uint64_t)(node ? R.cur : 0u) * 4;
+    constexpr uint32_t NW = WideFmt<W>::words;
+    const uint4* wp = wnodes + (uint64_t)(node ? R.cur : 0u) * NW;
     const float4* tp = tri_s + (uint64_t)(leaf ? (R.pend & ~kWideLeaf) : 0u) * 3;
     const uint32_t to = BUF ? (leaf ? (R.pend & ~kWideLeaf) * 48u : M->tbytes) : 0u;
-    uint4 w0, w1, w2, w3;
+    uint4 wr[NW];
     float4 T0, T1, T2;
     if (BUF) {
-        const uint32_t wo = node ? R.cur * 64u : M->wbytes;
+        const uint32_t wo = node ? R.cur * WideFmt<W>::bytes : M->wbytes;
         T0 = bload_f4(M->tr, to); T1 = bload_f4(M->tr, to + 16); T2 = bload_f4(M->tr, to + 32);
-        w0 = bload_u4(M->wr, wo); w1 = bload_u4(M->wr, wo + 16); w2 = bload_u4(M->wr, wo + 32);
-        w3 = bload_u4(M->wr, wo + 48);
+#pragma unroll
+        for (uint32_t k = 0; k < NW; ++k) wr[k] = bload_u4(M->wr, wo + 16 * k);
     } else {
         if (leaf) { T0 = tp[0]; T1 = tp[1]; T2 = tp[2]; }
-        if (node) { w0 = wp[0]; w1 = wp[1]; w2 = wp[2]; w3 = wp[3]; }
+        if (node) {
+#pragma unroll
+            for (uint32_t k = 0; k < NW; ++k) wr[k] = wp[k];
+        }
     }
     if (leaf) {
         if (COUNT) ++ct;
@@ -395,54 +458,57 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     if (!node) return 0;
     if (R.ctn > R.tb) { R.cur = RT_SENT; return 0; }
     if (COUNT) ++cn;
-    const uint32_t flags = w0.w >> 24;
-    const uint32_t ref[4] = {w2.z, w2.w, w3.x, w3.y};
-    bool hit[4];
-    float tn[4];
-    const bool wild = record_test(R, o, w0, w1, w2, hit, tn);
+    const uint32_t valid = rec_mask<W>(wr);
+    bool hit[W];
+    float tn[W];
+    record_test<W>(R, wr, hit, tn);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        hit[i] = ((flags >> (4 + i)) & 1u) && (hit[i] || wild);
-        if (wild) tn[i] = 0.0f;
-    }
-    bool earlier[4];
+    for (int i = 0; i < W; ++i) hit[i] = ((valid >> i) & 1u) && hit[i];
+    bool earlier[W];
     earlier[0] = false;
 #pragma unroll
-    for (int i = 1; i < 4; ++i) earlier[i] = earlier[i - 1] || hit[i - 1];
+    for (int i = 1; i < W; ++i) earlier[i] = earlier[i - 1] || hit[i - 1];
     bool over = false;
 #pragma unroll
-    for (int i = 3; i >= 1; --i) {
+    for (int i = W - 1; i >= 1; --i) {
         const bool push = hit[i] && earlier[i];
         const uint32_t slot = R.sp < cap ? R.sp : cap;
-        sref[slot * NT] = ref[i];
+        sref[slot * NT] = rec_ref<W>(wr, i);
         stn[slot * NT] = (uint16_t)(__float_as_uint(tn[i]) >> 16);
         over = over || (push && R.sp >= cap);
         R.sp += (push && R.sp < cap) ? 1u : 0u;
     }
     if (over) return 2;
-    R.cur = hit[0] ? ref[0] : hit[1] ? ref[1] : hit[2] ? ref[2] : hit[3] ? ref[3] : RT_SENT;
-    R.ctn = hit[0] ? tn[0] : hit[1] ? tn[1] : hit[2] ? tn[2] : tn[3];
+    uint32_t cur = RT_SENT;
+    float ctn = tn[W - 1];
+#pragma unroll
+    for (int i = W - 1; i >= 0; --i) {
+        cur = hit[i] ? rec_ref<W>(wr, i) : cur;
+        ctn = hit[i] ? tn[i] : ctn;
+    }
+    R.cur = cur;
+    R.ctn = ctn;
     return 0;
 }
 
 // One ray from o along d over (0, tmax): the wide traversal when it applies
 // (finite 1/d, K7w records present), with the binary hand-off on overflow;
 // the binary traversal from the root otherwise.  any: the first hit ends it.
-template <bool COUNT, int NT, bool MTF = false>
+template <bool COUNT, int NT, bool MTF = false, int W = 4>
 __device__ __forceinline__ void trace_gen(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                           uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n, const float* o,
                                           const float* d, float tmax, bool any, uint32_t* sref, uint16_t* stn,
                                           float& tb, float& hu, float& hv, uint32_t& hp, uint32_t& cn, uint32_t& ct) {
     WRay R;
-    wray_init(o, d, R);
+    wray_init(o, d, R, scene_box(nodes));
     R.tb = tmax;
     const bool wide = R.fin && wnodes && n >= 2;
     int st = wide ? 0 : 2;
-    if (n <= kBufMaxN) {  // buffer loads (WideMem): record and triangle in one round trip
-        const WideMem M = wide_mem(wnodes, tri_s, n);
+    if (W == 8 || n <= kBufMaxN) {  // buffer loads (WideMem): record and triangle in one round trip
+        const WideMem M = wide_mem<W>(wnodes, tri_s, n);
         while (st == 0)
-            st = wide_step<COUNT, NT, false, MTF, true>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any,
-                                                        &M);
+            st = wide_step<COUNT, NT, false, MTF, true, W>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct,
+                                                           any, &M);
     } else {
         while (st == 0)
             st = wide_step<COUNT, NT, false, MTF>(R, wnodes, tri_s, o, wcap, 4 * n + 16, sref, stn, cn, ct, any);
@@ -498,7 +564,7 @@ __device__ __forceinline__ void surface(const float* __restrict__ tris, uint32_t
 // Lambert term, ambient floor.  Operation order as orc_render_shadow.
 struct Light { float p[3]; float ambient; };
 
-template <bool COUNT, int NT>
+template <bool COUNT, int NT, int W = 4>
 __device__ __forceinline__ float shadow_factor(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s,
                                                const float* __restrict__ tris, uint32_t n, const float* o,
@@ -508,7 +574,8 @@ __device__ __forceinline__ float shadow_factor(const char* __restrict__ nodes, c
     surface(tris, prim, o, d, t, lt.p, f);
     float tb, hu, hv;
     uint32_t hp;
-    trace_gen<COUNT, NT, true>(nodes, wnodes, wcap, tri_s, n, f.S, f.D, 1.0f, true, sref, stn, tb, hu, hv, hp, cn, ct);
+    trace_gen<COUNT, NT, true, W>(nodes, wnodes, wcap, tri_s, n, f.S, f.D, 1.0f, true, sref, stn, tb, hu, hv, hp, cn,
+                                  ct);
     const float lit = hp != RT_SENT ? 0.0f : fmaxf(f.cosl, 0.0f);
     return lt.ambient + (1.0f - lt.ambient) * lit;
 }
@@ -574,8 +641,19 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
 // returning atomics on ONE device-scope counter serialise (~10 ns each, a
 // full-frame pass 1 went 0.33 -> 0.42 ms), spread over 64 they do not.  A
 // counter may pass `cap`: lanes that find their shard full go on tracing.
+// minimum waves per SIMD the trace kernels are compiled for (the register
+// budget): the shadow kernel (primary + shadow traversal in one loop nest)
+// at 5, whose 107 VGPRs would leave 4 (0.764 -> 0.72 ms per frame); the
+// primary kernels at the compiler's choice (forcing 6 waves spills and is
+// slower, profiles/ab_slack_r02.log)
+#ifndef RT_KTRACE_WAVES
+#define RT_KTRACE_WAVES 1
+#endif
+#ifndef RT_KSHADOW_WAVES
+#define RT_KSHADOW_WAVES 5
+#endif
 constexpr uint32_t kCoopShards = 64;
-constexpr uint32_t kCoopFrontier = kWideStack + 1;           // pending entries a deferred ray can have
+constexpr uint32_t kCoopFrontier = kWideStackMax + 1;        // pending entries a deferred ray can have (either arity)
 constexpr uint32_t kCoopEntry = 3 + (kCoopFrontier + 1) / 2;  // uint4 per queue entry
 static_assert(kCoopEntry * 16 == kCoopEntryBytes, "rt_launch.h sizes the queue");
 struct CoopQ {
@@ -627,8 +705,9 @@ __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t
     return 0;
 }
 
-template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false>
-__global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4>
+__global__ __launch_bounds__(NT, (SHADOW && WA == 4) ? RT_KSHADOW_WAVES : RT_KTRACE_WAVES)
+void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
@@ -640,8 +719,8 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
                                                const uint16_t* __restrict__ px_prev = nullptr,
                                                uint16_t* __restrict__ px_cost = nullptr,
                                                uint32_t coop_cap = 0, CoopQ cq = CoopQ{}) {
-    __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
-    __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (kWideStack + 1) * NT : 1];
+    __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
+    __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
     // tile slot from the block id: consecutive tiles go to different XCDs
     // under the round-robin dispatch, which balances the image's cheap and
     // costly bands over the 8 XCDs (an XCD-banded remap measured 1.2x
@@ -669,6 +748,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
     }
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
+    const SceneBox sb = scene_box(nodes);
     uint32_t cn = 0, ct = 0, steps = 0;
     uint32_t qslot = 0, dsamp = RT_SENT;  // heavy-ray queue entry, deferred sample
     const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -693,14 +773,14 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             uint32_t hp = RT_SENT;
             if (WIDE) {
                 WRay R;
-                wray_init(cam.eye, d, R);
+                wray_init(cam.eye, d, R, sb);
                 int st = R.fin ? 0 : 2;
                 const char* nd = reinterpret_cast<const char*>(nodes);
-                const WideMem M = wide_mem(wnodes, tri_s, n);
+                const WideMem M = wide_mem<WA>(wnodes, tri_s, n);
                 while (st == 0) {
-                    st = wide_step<COUNT, NT, false, PACKED || SHADOW, BUF>(R, wnodes, tri_s, cam.eye, wcap,
-                                                                           4 * n + 16, s_ref + threadIdx.x,
-                                                                           s_tn + threadIdx.x, cn, ct, false, &M);
+                    st = wide_step<COUNT, NT, false, PACKED || SHADOW, BUF, WA>(R, wnodes, tri_s, cam.eye, wcap,
+                                                                              4 * n + 16, s_ref + threadIdx.x,
+                                                                              s_tn + threadIdx.x, cn, ct, false, &M);
                     if (!SHADOW && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
                 }
                 if (PX) steps += R.steps;
@@ -727,7 +807,7 @@ __global__ __launch_bounds__(NT) void k_trace(const void* __restrict__ nodes, co
             if (SHADOW) {
                 float f = 0.0f;
                 if (hp != RT_SENT)
-                    f = shadow_factor<COUNT, NT>(reinterpret_cast<const char*>(nodes), WIDE ? wnodes : nullptr, wcap,
+                    f = shadow_factor<COUNT, NT, WA>(reinterpret_cast<const char*>(nodes), WIDE ? wnodes : nullptr, wcap,
                                                  tri_s, tris, n, cam.eye, d, tb, hp, lt, s_ref + threadIdx.x,
                                                  s_tn + threadIdx.x, cn, ct);
                 if (hp != RT_SENT) {
@@ -829,16 +909,16 @@ constexpr uint32_t kCoopGrid = 2048;        // persistent 256-thread blocks (rep
 
 // frontier entries per group: a step takes m <= G entries and a record
 // entry adds at most 3, so the list needs room for the growth of a few steps
-template <int G>
+template <int G, int W = 4>
 struct CoopCfg {
-    static constexpr uint32_t cap = G == 64 ? 256u : G == 32 ? 192u : 112u;
+    static constexpr uint32_t cap = (G == 64 ? 256u : G == 32 ? 192u : 112u) * (W == 8 ? 2u : 1u);
     static constexpr uint32_t groups = 256u / G;  // per 256-thread block
 };
 
-template <int G>
+template <int G, int W = 4>
 struct CoopLds {
-    uint32_t ref[CoopCfg<G>::cap];
-    float tn[CoopCfg<G>::cap], t[CoopCfg<G>::cap], u[CoopCfg<G>::cap], v[CoopCfg<G>::cap];
+    uint32_t ref[CoopCfg<G, W>::cap];
+    float tn[CoopCfg<G, W>::cap], t[CoopCfg<G, W>::cap], u[CoopCfg<G, W>::cap], v[CoopCfg<G, W>::cap];
 };
 
 // this group's bits of a wave-wide ballot, shifted to bit 0
@@ -860,19 +940,20 @@ __device__ __forceinline__ uint32_t gread_u(uint32_t x, uint32_t src) {
 // axis.  hp = prim.
 // resume (nullable): a queue entry -- start from its best hit and pending
 // entries (pass 1's state) instead of the root.
-template <bool COUNT, int G>
+template <bool COUNT, int G, int W = 4>
 __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                            const float4* __restrict__ tri_s, uint32_t n, const float* o,
-                                           const float* d, CoopLds<G>& L, const uint4* __restrict__ resume,
+                                           const float* d, CoopLds<G, W>& L, const uint4* __restrict__ resume,
                                            float& tb_out, float& hu_out, float& hv_out, uint32_t& hp_out,
                                            uint32_t& cn, uint32_t& ct) {
-    static_assert(G > kCoopFrontier, "a group loads a resumed frontier in one step");
-    constexpr uint32_t CAP = CoopCfg<G>::cap;
+    constexpr uint32_t CAP = CoopCfg<G, W>::cap;
+    constexpr uint32_t NW = WideFmt<W>::words;
+    static_assert(CAP >= kCoopFrontier + (W - 1), "room for a resumed frontier and one record's children");
     const uint32_t lane = __lane_id();
     const uint32_t gl = lane & (G - 1), gbase = lane & ~(uint32_t)(G - 1);
     WRay R;
-    wray_init(o, d, R);
-    const WideMem M = wide_mem(wnodes, tri_s, n);  // n <= kBufMaxN (the launcher's condition)
+    wray_init(o, d, R, scene_box(nodes));
+    const WideMem M = wide_mem<W>(wnodes, tri_s, n);  // n <= kBufMaxN (the launcher's condition)
     float tb = __builtin_inff(), hu = 0.0f, hv = 0.0f;
     uint32_t hk = RT_SENT;   // tri_s slot of a best hit found here (its prim is read at the end)
     uint32_t hp0 = RT_SENT;  // the best hit's prim when resumed
@@ -882,10 +963,10 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
         hp0 = h1.w;
         tb = __uint_as_float(h2.x); hu = __uint_as_float(h2.y); hv = __uint_as_float(h2.z);
         sp = h2.w;
-        if (gl < sp) {
-            const uint4 pr = resume[3 + gl / 2];
-            L.ref[gl] = (gl & 1) ? pr.z : pr.x;
-            L.tn[gl] = __uint_as_float((gl & 1) ? pr.w : pr.y);
+        for (uint32_t i = gl; i < sp; i += G) {
+            const uint4 pr = resume[3 + i / 2];
+            L.ref[i] = (i & 1) ? pr.z : pr.x;
+            L.tn[i] = __uint_as_float((i & 1) ? pr.w : pr.y);
         }
     } else if (gl == 0) {
         L.ref[0] = 0u;  // the root record
@@ -897,7 +978,7 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
     bool handoff = false;
     for (uint32_t guard = 0; sp > 0; ++guard) {
         uint32_t m = min((uint32_t)G, sp);
-        if (sp + 3 * m > CAP) m = (CAP - sp) / 3;  // a record adds at most 3 entries
+        if (sp + (W - 1) * m > CAP) m = (CAP - sp) / (W - 1);  // a record adds at most W - 1 entries
         if (m == 0 || guard > limit) {
             handoff = true;
             break;
@@ -920,10 +1001,11 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
         const bool pre_leaf = act && !res && (ref & kWideLeaf) && etn <= tb;
         const bool pre_rec = act && !res && !(ref & kWideLeaf) && etn <= tb;
         const uint32_t to = pre_leaf ? (ref & ~kWideLeaf) * 48u : M.tbytes;
-        const uint32_t wo = pre_rec ? ref * 64u : M.wbytes;
+        const uint32_t wo = pre_rec ? ref * WideFmt<W>::bytes : M.wbytes;
         const float4 T0 = bload_f4(M.tr, to), T1 = bload_f4(M.tr, to + 16), T2 = bload_f4(M.tr, to + 32);
-        const uint4 w0 = bload_u4(M.wr, wo), w1 = bload_u4(M.wr, wo + 16), w2 = bload_u4(M.wr, wo + 32),
-                    w3 = bload_u4(M.wr, wo + 48);
+        uint4 wr[NW];
+#pragma unroll
+        for (uint32_t k = 0; k < NW; ++k) wr[k] = bload_u4(M.wr, wo + 16 * k);
         // 1. fold the head run of resolved leaves, in preorder
         const uint64_t nonres = gballot<G>(act && !res, gbase);
         const uint32_t j = nonres ? (uint32_t)__builtin_ctzll(nonres) : m;
@@ -940,9 +1022,11 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
         }
         // 2. expand entries j..m-1 against the folded tb
         R.tb = tb;
-        bool h[4] = {false, false, false, false};
-        uint32_t cref[4] = {ref, 0u, 0u, 0u};
-        float ctn[4] = {etn, 0.0f, 0.0f, 0.0f};
+        bool h[W];
+        uint32_t cref[W];
+        float ctn[W];
+#pragma unroll
+        for (int i = 0; i < W; ++i) { h[i] = false; cref[i] = i == 0 ? ref : 0u; ctn[i] = i == 0 ? etn : 0.0f; }
         if (act && gl >= j && etn <= tb) {
             if (res) {
                 h[0] = true;  // not at the head yet: stays pending
@@ -960,29 +1044,36 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
                 }
             } else {
                 if (COUNT) ++cn;
-                float tn[4];
-                const bool wild = record_test(R, o, w0, w1, w2, h, tn);
-                const uint32_t flags = w0.w >> 24;
-                cref[0] = w2.z; cref[1] = w2.w; cref[2] = w3.x; cref[3] = w3.y;
+                float tn[W];
+                record_test<W>(R, wr, h, tn);
+                const uint32_t valid = rec_mask<W>(wr);
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    h[i] = ((flags >> (4 + i)) & 1u) && (h[i] || wild);
-                    ctn[i] = wild ? 0.0f : tn[i];
+                for (int i = 0; i < W; ++i) {
+                    cref[i] = rec_ref<W>(wr, i);
+                    h[i] = ((valid >> i) & 1u) && h[i];
+                    ctn[i] = tn[i];
                 }
             }
         }
         // 3. the outputs in preorder (lane order, then child order) replace
         // the m entries taken: output g lands at spn - 1 - g
-        const uint32_t c = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
-        const uint64_t b0 = gballot<G>(c & 1u, gbase), b1 = gballot<G>(c & 2u, gbase), b2 = gballot<G>(c & 4u, gbase);
+        uint32_t c = 0;
+#pragma unroll
+        for (int i = 0; i < W; ++i) c += (uint32_t)h[i];
+        // each lane's output count c <= W, summed over the group bit by bit
+        constexpr int CB = W == 8 ? 4 : 3;
         const uint64_t below = (1ull << gl) - 1ull;
-        const uint32_t pre = (uint32_t)__popcll(b0 & below) + 2u * (uint32_t)__popcll(b1 & below) +
-                             4u * (uint32_t)__popcll(b2 & below);
-        const uint32_t total = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+        uint32_t pre = 0, total = 0;
+#pragma unroll
+        for (int bit = 0; bit < CB; ++bit) {
+            const uint64_t bb = gballot<G>((c >> bit) & 1u, gbase);
+            pre += (uint32_t)__popcll(bb & below) << bit;
+            total += (uint32_t)__popcll(bb) << bit;
+        }
         const uint32_t spn = sp - m + total;
         uint32_t g = pre;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < W; ++i) {
             if (h[i]) {
                 const uint32_t p = spn - 1 - g;
                 L.ref[p] = cref[i];
@@ -1012,14 +1103,14 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // one group of G lanes each (a persistent grid striding over the queue), from
 // the queued sample on; writes their hits and RGBA exactly as k_trace would.
 // Block 0 zeroes the next frame's queue counters.
-template <bool COUNT, bool PACKED, int G>
+template <bool COUNT, bool PACKED, int G, int WA = 4>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
                                                     uint32_t W, uint32_t spp, CoopQ cq, float4* __restrict__ hits,
                                                     uint32_t* __restrict__ rgba,
                                                     unsigned long long* __restrict__ counters) {
-    constexpr uint32_t NG = CoopCfg<G>::groups;
-    __shared__ CoopLds<G> s_l[NG];
+    constexpr uint32_t NG = CoopCfg<G, WA>::groups;
+    __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
     if (blockIdx.x == 0 && threadIdx.x < kCoopShards) cq.ctr_next[threadIdx.x] = 0u;
     const uint32_t lane = threadIdx.x & 63, grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
@@ -1068,7 +1159,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
             for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
             float tb, hu, hv;
             uint32_t hp;
-            coop_trace<COUNT, G>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp],
+            coop_trace<COUNT, G, WA>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp],
                                  s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
             if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
             if (hp != RT_SENT) {
@@ -1115,15 +1206,15 @@ __device__ __forceinline__ float path_u01(uint32_t& st) { return (float)(path_ne
 
 struct PathCfg { float light[3]; float sky; uint32_t max_depth; };
 
-template <bool COUNT, int NT>
+template <bool COUNT, int NT, int WA = 4>
 __global__ __launch_bounds__(NT) void k_path(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                               uint32_t wcap, const float4* __restrict__ tri_s,
                                               const float* __restrict__ tris, uint32_t n, Cam cam, uint32_t W,
                                               uint32_t H, uint32_t spp, uint32_t tilesX, PathCfg pc,
                                               float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                               unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t s_ref[(kWideStack + 1) * NT];
-    __shared__ uint16_t s_tn[(kWideStack + 1) * NT];
+    __shared__ uint32_t s_ref[(WideFmt<WA>::stack + 1) * NT];
+    __shared__ uint16_t s_tn[(WideFmt<WA>::stack + 1) * NT];
     constexpr uint32_t WPB = NT / 64;
     const uint32_t gw = blockIdx.x * WPB + (threadIdx.x >> 6);
     const uint32_t t = gw >> 2;
@@ -1148,7 +1239,7 @@ __global__ __launch_bounds__(NT) void k_path(const void* __restrict__ nodes, con
         for (;;) {
             float tb, hu, hv;
             uint32_t hp;
-            trace_gen<COUNT, NT>(nd, wnodes, wcap, tri_s, n, o, d, tmax, shadow, s_ref + threadIdx.x,
+            trace_gen<COUNT, NT, false, WA>(nd, wnodes, wcap, tri_s, n, o, d, tmax, shadow, s_ref + threadIdx.x,
                                  s_tn + threadIdx.x, tb, hu, hv, hp, cn, ct);
             ++crays;
             bool bounce = false, done = false;
@@ -1270,15 +1361,15 @@ __device__ __forceinline__ uint32_t ray_key(const float* o, const float* d, bool
     return (shadow ? 1u << 30 : 0u) | (oct << 27) | m;
 }
 
-template <bool COUNT>
+template <bool COUNT, int WA = 4>
 __global__ __launch_bounds__(256) void k_pw_primary(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                      uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                      Cam cam, uint32_t W, uint32_t H, uint32_t spp, uint32_t tilesX,
                                                      uint32_t t0, float* __restrict__ pf, uint32_t* __restrict__ pu,
                                                      uint32_t cap, float4* __restrict__ hits,
                                                      unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
-    __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
+    __shared__ uint32_t s_ref[(WideFmt<WA>::stack + 1) * 256];
+    __shared__ uint16_t s_tn[(WideFmt<WA>::stack + 1) * 256];
     const uint32_t t = t0 + blockIdx.x;
     const uint32_t l = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t lx = (wv & 1) * 8 + (l & 7), ly = (wv >> 1) * 8 + (l >> 3);
@@ -1293,7 +1384,7 @@ __global__ __launch_bounds__(256) void k_pw_primary(const void* __restrict__ nod
         float d[3], tb, hu, hv;
         uint32_t hp;
         ray_dir(cam, x, y, W, spp, s, d);
-        trace_gen<COUNT, 256>(reinterpret_cast<const char*>(nodes), wnodes, wcap, tri_s, n, cam.eye, d,
+        trace_gen<COUNT, 256, false, WA>(reinterpret_cast<const char*>(nodes), wnodes, wcap, tri_s, n, cam.eye, d,
                               __builtin_inff(), false, s_ref + threadIdx.x, s_tn + threadIdx.x, tb, hu, hv, hp, cn, ct);
         if (hits) hits[sidx] = make_float4(tb, hu, hv, __uint_as_float(hp));
 #pragma unroll
@@ -1435,15 +1526,15 @@ __global__ __launch_bounds__(1024) void k_pw_shade(float* __restrict__ pf, uint3
     }
 }
 
-template <bool COUNT>
+template <bool COUNT, int WA = 4>
 __global__ __launch_bounds__(256) void k_pw_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                    uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                    const float4* __restrict__ rays, const uint32_t* __restrict__ order,
                                                    uint32_t count, const uint32_t* __restrict__ count_dev,
                                                    float* __restrict__ pf, uint32_t* __restrict__ pu,
                                                    uint32_t cap, unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
-    __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
+    __shared__ uint32_t s_ref[(WideFmt<WA>::stack + 1) * 256];
+    __shared__ uint16_t s_tn[(WideFmt<WA>::stack + 1) * 256];
     if (count_dev) count = *count_dev;  // grid sized for the bound, queue length read here
     if (blockIdx.x * 256 >= count) return;
     const uint32_t i = blockIdx.x * 256 + threadIdx.x;
@@ -1456,7 +1547,7 @@ __global__ __launch_bounds__(256) void k_pw_trace(const void* __restrict__ nodes
         const bool shadow = tag >> 31;
         float tb, hu, hv;
         uint32_t hp;
-        trace_gen<COUNT, 256>(reinterpret_cast<const char*>(nodes), wnodes, wcap, tri_s, n, o, d, A.w, shadow,
+        trace_gen<COUNT, 256, false, WA>(reinterpret_cast<const char*>(nodes), wnodes, wcap, tri_s, n, o, d, A.w, shadow,
                               s_ref + threadIdx.x, s_tn + threadIdx.x, tb, hu, hv, hp, cn, ct);
         if (shadow) {
             pu[kPuVis * cap + pid] = hp == RT_SENT ? 1u : 0u;
@@ -1523,6 +1614,7 @@ __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nod
     uint16_t* stn = s_tn + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const SceneBox sb = scene_box(nodes);
     const float o[3] = {cam.eye[0], cam.eye[1], cam.eye[2]};
     const uint32_t limit = 4 * n + 16;
 #ifdef RT_STAMPS
@@ -1564,7 +1656,7 @@ __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nod
                     have = true;
                     s = 0;
                     cr = cg = cb = 0.0f;
-                    wray_setup(cam, x, y, W, spp, 0, R);
+                    wray_setup(cam, x, y, W, spp, 0, R, sb);
                 }
             }
             next += take;
@@ -1600,7 +1692,7 @@ __global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nod
                     cr = cr + 0.0f; cg = cg + 0.0f; cb = cb + 0.0f;
                 }
                 if (++s < spp) {
-                    wray_setup(cam, x, y, W, spp, s, R);
+                    wray_setup(cam, x, y, W, spp, s, R, sb);
                 } else {
                     if (rgba) {
                         const float sc = 1.0f / (float)spp;
@@ -1790,10 +1882,34 @@ bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key
     return true;
 }
 
-hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tris, uint32_t n, const CamF& c,
-                        uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed, void* hits,
-                        void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
-                        TileSched* sched, hipStream_t s) {
+// the wide stack entries a launch uses: trace.stack_cap (tests force
+// overflows with small values), at most the arity's stack; 0 = all of it
+static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity) {
+    const uint32_t full = warity == 8 ? (uint32_t)WideFmt<8>::stack : (uint32_t)WideFmt<4>::stack;
+    return cfg.stack_cap ? min(cfg.stack_cap, full) : full;
+}
+
+// k_trace with the record arity and load form chosen at run time (the
+// binary kernel, WI = false, has one form)
+template <bool C, bool P, bool WI, int NT, typename... A>
+static void k_trace_go(bool buf, uint32_t warity, uint32_t grid, hipStream_t s, A... a) {
+    if constexpr (WI) {
+        if (warity == 8) {
+            hipLaunchKernelGGL((k_trace<C, P, true, NT, false, true, 8>), dim3(grid), dim3(NT), 0, s, a...);
+            return;
+        }
+        if (buf) {
+            hipLaunchKernelGGL((k_trace<C, P, true, NT, false, true, 4>), dim3(grid), dim3(NT), 0, s, a...);
+            return;
+        }
+    }
+    hipLaunchKernelGGL((k_trace<C, P, WI, NT, false, false, 4>), dim3(grid), dim3(NT), 0, s, a...);
+}
+
+hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tris, uint32_t n,
+                        const CamF& c, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
+                        bool packed, void* hits, void* rgba, unsigned long long* counters, bool binary_counts,
+                        uint32_t* work, TileSched* sched, hipStream_t s) {
     const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
     if (!nb) return hipSuccess;
@@ -1804,8 +1920,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     const uint32_t tilesX = (w + 15) / 16;
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
-    const uint32_t cap = cfg.stack_cap;
-    if (cfg.variant == 1 && wnodes && n >= 2 && !binary_counts && work) {
+    if (warity != 4 && warity != 8) return hipErrorInvalidValue;
+    if (warity == 8 && n > kBufMaxN) return hipErrorInvalidValue;  // the build keeps 8-ary records to n <= 2^26
+    const uint32_t cap = stack_cap_for(cfg, warity);
+    if (cfg.variant == 1 && wnodes && warity == 4 && n >= 2 && !binary_counts && work) {
         const uint32_t nunits = nb * 4;
         hipError_t me = hipMemsetAsync(work, 0, kPoolCounters * 128, s);
         if (me != hipSuccess) return me;
@@ -1905,12 +2023,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
-#define RT_TRACE_NT_B(C, P, WI, NT, B)                                                                             \
-    hipLaunchKernelGGL((k_trace<C, P, WI, NT, false, B>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wnodes,    \
-                       cap, tris, n, cam, w, h, spp, rank, nranks, tilesX, H, R, counters, nullptr, Light{}, order, \
-                       cost_out, px_prev, px_cost, coop_cap, cq)
-#define RT_TRACE_NT(C, P, WI, NT) \
-    if (buf) RT_TRACE_NT_B(C, P, WI, NT, WI); else RT_TRACE_NT_B(C, P, WI, NT, false)
+#define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
+    k_trace_go<C, P, WI, NT>(buf, warity, nb * (256 / NT), s, nodes, wnodes, cap, tris, n, cam, w, h, spp, rank,    \
+                             nranks, tilesX, H, R, counters, (const float*)nullptr, Light{}, order, cost_out, px_prev, \
+                             px_cost, coop_cap, cq)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \
@@ -1927,43 +2043,55 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
 #undef RT_TRACE_W
 #undef RT_TRACE
 #undef RT_TRACE_NT
-#undef RT_TRACE_NT_B
     if (coop_cap) {
         hipError_t le = hipGetLastError();
         if (le != hipSuccess) return le;
         uint32_t cgrid = kCoopGrid;
         {  // persistent grid = the resident capacity (per device and group width, computed once)
-            static std::atomic<uint32_t> resident[kMaxDevices][3];
+            static std::atomic<uint32_t> resident[kMaxDevices][3][2];
             int dev = 0;
             hipError_t e = hipGetDevice(&dev);
             if (e != hipSuccess) return e;
             if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
             const int gi = cfg.coop_lanes == 16 ? 0 : cfg.coop_lanes == 32 ? 1 : 2;
-            uint32_t r = resident[dev][gi].load(std::memory_order_relaxed);
+            const int ai = warity == 8 ? 1 : 0;
+            uint32_t r = resident[dev][gi][ai].load(std::memory_order_relaxed);
             if (!r) {
                 int per_cu = 0, cus = 0;
-                const void* kf = gi == 0 ? reinterpret_cast<const void*>(k_trace_coop<false, false, 16>)
-                               : gi == 1 ? reinterpret_cast<const void*>(k_trace_coop<false, false, 32>)
-                                         : reinterpret_cast<const void*>(k_trace_coop<false, false, 64>);
+                const void* kf =
+                    ai ? (gi == 0   ? reinterpret_cast<const void*>(k_trace_coop<false, false, 16, 8>)
+                          : gi == 1 ? reinterpret_cast<const void*>(k_trace_coop<false, false, 32, 8>)
+                                    : reinterpret_cast<const void*>(k_trace_coop<false, false, 64, 8>))
+                       : (gi == 0   ? reinterpret_cast<const void*>(k_trace_coop<false, false, 16>)
+                          : gi == 1 ? reinterpret_cast<const void*>(k_trace_coop<false, false, 32>)
+                                    : reinterpret_cast<const void*>(k_trace_coop<false, false, 64>));
                 if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, 256, 0)) != hipSuccess) return e;
                 if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
                     return e;
                 r = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
-                resident[dev][gi].store(r, std::memory_order_relaxed);
+                resident[dev][gi][ai].store(r, std::memory_order_relaxed);
             }
             cgrid = r;
         }
-#define RT_COOP_G(C, P, G)                                                                                         \
-    hipLaunchKernelGGL((k_trace_coop<C, P, G>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, spp, \
-                       cq, H, R, counters)
-#define RT_COOP(C, P)                                       \
-    if (cfg.coop_lanes == 16) RT_COOP_G(C, P, 16);          \
-    else if (cfg.coop_lanes == 32) RT_COOP_G(C, P, 32);     \
-    else RT_COOP_G(C, P, 64)
+#define RT_COOP_G(C, P, G)                                                                                        \
+    if (warity == 8)                                                                                               \
+        hipLaunchKernelGGL((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
+                           spp, cq, H, R, counters);                                                               \
+    else                                                                                                           \
+        hipLaunchKernelGGL((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
+                           spp, cq, H, R, counters)
+#define RT_COOP(C, P)                  \
+    if (cfg.coop_lanes == 16) {        \
+        RT_COOP_G(C, P, 16);           \
+    } else if (cfg.coop_lanes == 32) { \
+        RT_COOP_G(C, P, 32);           \
+    } else {                           \
+        RT_COOP_G(C, P, 64);           \
+    }
         if (counters) {
-            if (packed) RT_COOP(true, true); else RT_COOP(true, false);
+            if (packed) { RT_COOP(true, true); } else { RT_COOP(true, false); }
         } else {
-            if (packed) RT_COOP(false, true); else RT_COOP(false, false);
+            if (packed) { RT_COOP(false, true); } else { RT_COOP(false, false); }
         }
 #undef RT_COOP
 #undef RT_COOP_G
@@ -1972,9 +2100,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, const float4* tr
     return hipGetLastError();
 }
 
-hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
-                               uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
-                               float ambient, void* hits, void* rgba, unsigned long long* counters, hipStream_t s) {
+hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s,
+                               const float* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp,
+                               const float light[3], float ambient, void* hits, void* rgba,
+                               unsigned long long* counters, hipStream_t s) {
     const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, 0, 1);
     if (!nb) return hipSuccess;
@@ -1988,24 +2117,29 @@ hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, const flo
     const uint32_t tilesX = (w + 15) / 16;
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
+    if (warity != 4 && warity != 8) return hipErrorInvalidValue;
     const bool wide = wnodes && n >= 2 && cfg.variant != 2;
-    const uint32_t cap = cfg.stack_cap;
-#define RT_SHADOW(C, WI)                                                                                        \
-    hipLaunchKernelGGL((k_trace<C, false, WI, 256, true>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, tri_s, \
-                       n, cam, w, h, spp, 0u, 1u, tilesX, H, R, counters, tris, lt)
+    const uint32_t cap = stack_cap_for(cfg, warity);
+#define RT_SHADOW(C, WI, WW)                                                                                       \
+    hipLaunchKernelGGL((k_trace<C, false, WI, 256, true, false, WW>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, \
+                       tri_s, n, cam, w, h, spp, 0u, 1u, tilesX, H, R, counters, tris, lt)
     if (counters) {
-        if (wide) RT_SHADOW(true, true); else RT_SHADOW(true, false);
+        if (wide && warity == 8) RT_SHADOW(true, true, 8);
+        else if (wide) RT_SHADOW(true, true, 4);
+        else RT_SHADOW(true, false, 4);
     } else {
-        if (wide) RT_SHADOW(false, true); else RT_SHADOW(false, false);
+        if (wide && warity == 8) RT_SHADOW(false, true, 8);
+        else if (wide) RT_SHADOW(false, true, 4);
+        else RT_SHADOW(false, false, 4);
     }
 #undef RT_SHADOW
     return hipGetLastError();
 }
 
-hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
-                             uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp, const float light[3],
-                             float sky, uint32_t max_depth, void* hits, void* rgba, unsigned long long* counters,
-                             hipStream_t s) {
+hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s,
+                             const float* tris, uint32_t n, const CamF& c, uint32_t w, uint32_t h, uint32_t spp,
+                             const float light[3], float sky, uint32_t max_depth, void* hits, void* rgba,
+                             unsigned long long* counters, hipStream_t s) {
     const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, 0, 1);
     if (!nb) return hipSuccess;
@@ -2022,15 +2156,20 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, const float
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     // K7w records unless the binary traversal is asked for (variant 2)
     const uint4* wn = (cfg.variant != 2) ? wnodes : nullptr;
-    const uint32_t cap = cfg.stack_cap;
+    if (warity != 4 && warity != 8) return hipErrorInvalidValue;
+    const uint32_t cap = stack_cap_for(cfg, warity);
     const bool small = cfg.path_wg == 64;
-#define RT_PATH(C, NT)                                                                                            \
-    hipLaunchKernelGGL((k_path<C, NT>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, cam, \
-                       w, h, spp, tilesX, pc, H, R, counters)
+#define RT_PATH(C, NT)                                                                                                 \
+    if (warity == 8)                                                                                                 \
+        hipLaunchKernelGGL((k_path<C, NT, 8>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
+                           cam, w, h, spp, tilesX, pc, H, R, counters);                                              \
+    else                                                                                                             \
+        hipLaunchKernelGGL((k_path<C, NT, 4>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
+                           cam, w, h, spp, tilesX, pc, H, R, counters)
     if (counters) {
-        if (small) RT_PATH(true, 64); else RT_PATH(true, 256);
+        if (small) { RT_PATH(true, 64); } else { RT_PATH(true, 256); }
     } else {
-        if (small) RT_PATH(false, 64); else RT_PATH(false, 256);
+        if (small) { RT_PATH(false, 64); } else { RT_PATH(false, 256); }
     }
 #undef RT_PATH
     return hipGetLastError();
@@ -2066,8 +2205,9 @@ void free_path(PathBufs& b) {
     b = PathBufs{};
 }
 
-hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const float4* tri_s, const float* tris,
-                                 const BuildParams* params, uint32_t n, const CamF& c, uint32_t w, uint32_t h,
+hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s,
+                                 const float* tris, const BuildParams* params, uint32_t n, const CamF& c, uint32_t w,
+                                 uint32_t h,
                                  uint32_t spp, const float light[3], float sky, uint32_t max_depth, void* hits,
                                  void* rgba, unsigned long long* counters, PathBufs& pb, uint32_t sort_digits,
                                  hipStream_t s) {
@@ -2086,19 +2226,24 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const f
     pc.max_depth = max_depth;
     const uint32_t tilesX = (w + 15) / 16;
     const uint4* wn = (cfg.variant != 2) ? wnodes : nullptr;
-    const uint32_t wcap = cfg.stack_cap;
+    if (warity != 4 && warity != 8) return hipErrorInvalidValue;
+    const uint32_t wcap = stack_cap_for(cfg, warity);
+    const bool w8 = warity == 8;
     const uint32_t batch = pb.cap / per_tile;
     float4* H = reinterpret_cast<float4*>(hits);
     hipError_t e;
     for (uint32_t t0 = 0; t0 < nt; t0 += batch) {
         const uint32_t nb = min(batch, nt - t0);
         const uint32_t np = nb * per_tile;
-        if (counters)
-            hipLaunchKernelGGL(k_pw_primary<true>, dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h, spp,
-                               tilesX, t0, pb.f, pb.u, pb.cap, H, counters);
-        else
-            hipLaunchKernelGGL(k_pw_primary<false>, dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h,
-                               spp, tilesX, t0, pb.f, pb.u, pb.cap, H, counters);
+#define RT_PW_PRIMARY(C, WW)                                                                                  \
+    hipLaunchKernelGGL((k_pw_primary<C, WW>), dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h, spp, \
+                       tilesX, t0, pb.f, pb.u, pb.cap, H, counters)
+        if (counters) {
+            if (w8) RT_PW_PRIMARY(true, 8); else RT_PW_PRIMARY(true, 4);
+        } else {
+            if (w8) RT_PW_PRIMARY(false, 8); else RT_PW_PRIMARY(false, 4);
+        }
+#undef RT_PW_PRIMARY
         for (uint32_t depth = 0; depth <= max_depth + 1; ++depth) {
             if ((e = hipMemsetAsync(pb.qcount, 0, 4, s)) != hipSuccess) return e;
             hipLaunchKernelGGL(k_pw_shade, dim3((np + 1023) / 1024), dim3(1024), 0, s, pb.f, pb.u, pb.cap, np, depth,
@@ -2126,12 +2271,15 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, const f
                 count_dev = pb.qcount;
                 grid = (2 * np + 255) / 256;
             }
-            if (counters)
-                hipLaunchKernelGGL(k_pw_trace<true>, dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays,
-                                   order, count, count_dev, pb.f, pb.u, pb.cap, counters);
-            else
-                hipLaunchKernelGGL(k_pw_trace<false>, dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays,
-                                   order, count, count_dev, pb.f, pb.u, pb.cap, counters);
+#define RT_PW_TRACE(C, WW)                                                                                     \
+    hipLaunchKernelGGL((k_pw_trace<C, WW>), dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays, order, \
+                       count, count_dev, pb.f, pb.u, pb.cap, counters)
+            if (counters) {
+                if (w8) RT_PW_TRACE(true, 8); else RT_PW_TRACE(true, 4);
+            } else {
+                if (w8) RT_PW_TRACE(false, 8); else RT_PW_TRACE(false, 4);
+            }
+#undef RT_PW_TRACE
         }
         if (rgba)
             hipLaunchKernelGGL(k_pw_finish, dim3(nb), dim3(256), 0, s, pb.f, pb.cap, w, h, spp, tilesX, t0,

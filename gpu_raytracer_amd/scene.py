@@ -146,10 +146,19 @@ class Scene:
         call("rt_bvh_build_times", self._h, C.byref(t))
         return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total)
 
+    @property
+    def wide_arity(self) -> int:
+        """Arity of the built wide records: 4 (K7w) or 8 (K7w8)."""
+        a = C.c_uint32()
+        call("rt_bvh_wide_arity", self._h, C.byref(a))
+        return a.value
+
     def read_wide(self) -> np.ndarray:
-        """K7w wide records as uint32[(n-1), 16] (layout: csrc/rt_device.h)."""
+        """Wide records as uint32[(n-1), 16] (4-ary K7w) or uint32[(n-1), 24]
+        (8-ary K7w8); layouts: csrc/rt_device.h."""
         n = self.num_tris
-        rec = np.zeros((max(n - 1, 1), 16), np.uint32)
+        words = 24 if self.wide_arity == 8 else 16
+        rec = np.zeros((max(n - 1, 1), words), np.uint32)
         call("rt_bvh_read_wide", self._h, _p(rec))
         return rec[: max(n - 1, 0)]
 

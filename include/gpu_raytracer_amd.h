@@ -129,9 +129,13 @@ rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* sorted_keys,
  * for a bad file). */
 rt_status rt_bvh_save(const rt_scene* s, const char* path);
 rt_status rt_bvh_load(rt_scene* s, const char* path);
-/* Read back the K7w wide trace records: (n-1) x 64 B, one per binary internal
- * node (layout: gpu_raytracer_amd/csrc/rt_device.h); nothing for n < 2. */
+/* Read back the wide trace records, one per binary internal node: (n-1) x 64 B
+ * for 4-ary K7w records, (n-1) x 96 B for 8-ary K7w8 records (layouts:
+ * gpu_raytracer_amd/csrc/rt_device.h); nothing for n < 2.  The arity is the
+ * build's rt_config_set("build.wide_arity", 4 | 8) (8 only for n <= 2^26), as
+ * reported by rt_bvh_wide_arity.  SURVEY.md §8(f) row 1 ("4/8-wide"). */
 rt_status rt_bvh_read_wide(const rt_scene* s, void* records);
+rt_status rt_bvh_wide_arity(const rt_scene* s, uint32_t* arity_out);
 
 /* ---- render (SURVEY.md §8(b) rt_render(scene, cam, w, h, spp, ngpus, hits,
  * rgba)).  hits_out: w*h*spp records, rgba_out: w*h*4 bytes; either may be
@@ -296,9 +300,12 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * wide (4-ary) traversal over the K7w records (default), 1 = wide traversal
  * with per-lane refill from 8x8-pixel units dealt statically to a resident
  * grid, 2 = one thread per pixel, binary traversal; "trace.blocks" variant-1
- * grid (0 = resident capacity); "trace.stack_cap" (1..14) wide-traversal
- * stack entries -- rays that need more are re-traced by the binary
- * traversal; "trace.wg" 64/256 threads per block (8x8 quadrant / 16x16
+ * grid (0 = resident capacity); "trace.stack_cap" (1..18; 0 = all, the
+ * default: 14 for 4-ary records, 18 for 8-ary) wide-traversal stack
+ * entries -- rays that need more are re-traced by the binary traversal;
+ * "build.wide_arity" 4 (default) / 8: K7w 4-ary or K7w8 8-ary trace records
+ * (8-ary: about a quarter fewer dependent record fetches for the costliest
+ * rays, more instructions per step; n <= 2^26); "trace.wg" 64/256 threads per block (8x8 quadrant / 16x16
  * tile), default 256; "trace.wg_tiles" the same for one rank's tiles of a
  * multi-GPU frame (rt_render_tiles_device), default 64; "trace.tile_order"
  * 1 = dispatch a frame's tiles longest-first from the previous frame of the

@@ -227,7 +227,7 @@ def test_bvh_cache_rejects_without_device_work(rt, tmp_path):
 # restored afterwards (include/gpu_raytracer_amd.h; INTEGRATION.md "tuning").
 CONFIG_KEYS = {
     "trace.variant": ([0, 1, 2], [3, -1], 0),
-    "trace.stack_cap": ([1, 14], [0, 15], 14),
+    "trace.stack_cap": ([0, 1, 14, 18], [-1, 19], 0),
     "trace.wg": ([64, 256], [128], 256),
     "trace.wg_tiles": ([64, 256], [32], 64),
     "trace.tile_order": ([0, 1], [2], 1),
@@ -235,6 +235,7 @@ CONFIG_KEYS = {
     "trace.blocks": ([0, 4096], [-1], 0),
     "build.sort": ([0, 1], [2], 1),
     "build.wide_collapse": ([0, 1], [2, -1], 1),
+    "build.wide_arity": ([4, 8], [2, 6, 16, -1], 4),
     "build.stage_events": ([0, 1], [2], 0),
     "timing.event_fence": ([0, 1], [2], 0),
     "path.wavefront": ([0, 1], [2], 1),

@@ -18,7 +18,7 @@ def R(rt):
         pytest.fail("no GPU visible to librtamd")
     yield rt
     rt.config_set("trace.variant", 0)
-    rt.config_set("trace.stack_cap", 14)
+    rt.config_set("trace.stack_cap", 0)
     rt.config_set("trace.wg", 256)
     rt.config_set("path.wg", 64)
     rt.config_set("path.wavefront", 1)

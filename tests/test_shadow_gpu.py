@@ -17,7 +17,7 @@ def R(rt):
         pytest.fail("no GPU visible to librtamd")
     yield rt
     rt.config_set("trace.variant", 0)
-    rt.config_set("trace.stack_cap", 14)
+    rt.config_set("trace.stack_cap", 0)
 
 
 def _check(R, oracle, tris, view, light, w, h, spp, variant=0, cap=14, ambient=0.2):

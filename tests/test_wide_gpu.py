@@ -19,26 +19,44 @@ def R(rt):
         pytest.fail("no GPU visible to librtamd")
     yield rt
     rt.config_set("trace.variant", 0)
-    rt.config_set("trace.stack_cap", 14)
+    rt.config_set("trace.stack_cap", 0)
     rt.config_set("trace.blocks", 0)
 
 
 def _decode_planes(rec):
-    """Dequantized child planes of wide records, computed as the kernel does:
-    origin + q * 2^e rounded once (q * 2^e is exact, so the float32 add equals
-    the kernel's fma)."""
+    """Dequantized child planes of wide records (uint32[m, 16] 4-ary K7w or
+    uint32[m, 24] 8-ary K7w8), computed as the kernel does: origin + q * 2^e
+    rounded once (q * 2^e is exact, so the float32 add equals the kernel's
+    fma).  Returns lo, hi as float32[m, 3, arity]."""
+    W = 8 if rec.shape[1] == 24 else 4
     org = rec[:, 0:3].view(np.float32)
     meta = rec[:, 3]
     scale = ((meta[:, None] >> (8 * np.arange(3, dtype=np.uint32))) & 0xFF).astype(np.uint32) << 23
     scale = scale.view(np.float32)                              # [m, 3] = 2^e
-    qlo = np.stack([rec[:, 4], rec[:, 5], rec[:, 6]], 1)        # [m, 3] bytes = children
-    qhi = np.stack([rec[:, 7], rec[:, 8], rec[:, 9]], 1)
     sh = (8 * np.arange(4, dtype=np.uint32))
-    ql = ((qlo[:, :, None] >> sh) & 0xFF).astype(np.float32)    # [m, 3, 4]
-    qh = ((qhi[:, :, None] >> sh) & 0xFF).astype(np.float32)
-    lo = org[:, :, None] + ql * scale[:, :, None]
-    hi = org[:, :, None] + qh * scale[:, :, None]
+    if W == 4:
+        qlo = np.stack([rec[:, 4], rec[:, 5], rec[:, 6]], 1)[:, :, None]   # [m, 3, 1 word]
+        qhi = np.stack([rec[:, 7], rec[:, 8], rec[:, 9]], 1)[:, :, None]
+    else:  # two words per plane: qlo.x qlo.y qlo.z qhi.x qhi.y qhi.z at words 4..15
+        qlo = rec[:, 4:10].reshape(-1, 3, 2)
+        qhi = rec[:, 10:16].reshape(-1, 3, 2)
+    ql = ((qlo[:, :, :, None] >> sh) & 0xFF).reshape(len(rec), 3, W).astype(np.float32)  # [m, 3, W]
+    qh = ((qhi[:, :, :, None] >> sh) & 0xFF).reshape(len(rec), 3, W).astype(np.float32)
+    with np.errstate(invalid="ignore", over="ignore"):
+        lo = org[:, :, None] + ql * scale[:, :, None]
+        hi = org[:, :, None] + qh * scale[:, :, None]
     return lo.astype(np.float32), hi.astype(np.float32)
+
+
+def _layout(rec):
+    """(arity, wild[m], valid mask[m], refs[m, arity]) of wide records."""
+    meta = rec[:, 3]
+    if rec.shape[1] == 24:
+        wild = (meta & 0xFFFFFF) == 0xFFFFFF
+        return 8, wild, meta >> 24, rec[:, 16:24]
+    wild = ((meta >> 24) & 1).astype(bool)
+    assert np.all(((meta & 0xFFFFFF) == 0xFFFFFF) == wild)  # wild records carry exponent bytes 255
+    return 4, wild, (meta >> 28) & 0xF, rec[:, 10:14]
 
 
 def _half_area(lo, hi):
@@ -47,18 +65,18 @@ def _half_area(lo, hi):
     return np.float32(np.float32(d[0] * d[1]) + np.float32(d[1] * d[2])) + np.float32(d[2] * d[0])
 
 
-def _entries(X, a, esc, lo_e, hi_e, L0, collapse):
+def _entries(X, a, esc, lo_e, hi_e, L0, collapse, arity=4):
     """Restatement of wide_entries: the record's entries in preorder."""
     def kids(c):
         L = a[c]
         return [L, esc[L]]  # escape of a left child = its right sibling
-    if collapse == 0:
+    if collapse == 0 and arity == 4:
         out = []
         for c in kids(X):
             out += kids(c) if c < L0 else [c]
         return out
     ent = kids(X)
-    for _ in range(2):
+    for _ in range(arity - 2):
         best, ba = -1, None
         for i, c in enumerate(ent):
             if c < L0:
@@ -81,36 +99,37 @@ def _leaf_range(c, a, esc, L0, memo):
     return memo[c]
 
 
-def _check_wide(R, tris, collapse=1):
+def _check_wide(R, tris, collapse=1, arity=4):
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     n = len(tris)
     R.config_set("build.wide_collapse", collapse)
+    R.config_set("build.wide_arity", arity)
     try:
         with R.Scene.from_soup(tris) as s:
             s.build()
+            assert s.wide_arity == arity
             nodes = s.read_bvh()["nodes"]
             rec = s.read_wide()
     finally:
         R.config_set("build.wide_collapse", 1)
-    assert rec.shape == (n - 1, 16)
+        R.config_set("build.wide_arity", 4)
+    assert rec.shape == (n - 1, 24 if arity == 8 else 16)
     L0 = n - 1
     a, esc = nodes["a"].astype(np.int64), nodes["esc"].astype(np.int64)
     lo_e, hi_e = nodes["lo"], nodes["hi"]
     lo_q, hi_q = _decode_planes(rec)
-    meta = rec[:, 3]
-    wild = ((meta >> 24) & 1).astype(bool)
-    mask = (meta >> 28) & 0xF
-    refs = rec[:, 10:14]
+    W, wild, mask, refs = _layout(rec)
+    assert W == arity
     memo = {}
     for X in range(n - 1):
-        kids = _entries(X, a, esc, lo_e, hi_e, L0, collapse)
+        kids = _entries(X, a, esc, lo_e, hi_e, L0, collapse, arity)
         # a preorder cut of X's subtree: consecutive leaf ranges covering X's
         rng = [_leaf_range(c, a, esc, L0, memo) for c in kids]
         xl, xh = _leaf_range(X, a, esc, L0, memo)
         assert rng[0][0] == xl and rng[-1][1] == xh, X
         assert all(rng[i][1] + 1 == rng[i + 1][0] for i in range(len(rng) - 1)), X
-        if collapse == 1:
-            assert len(kids) == min(4, xh - xl + 1), X
+        if collapse == 1 or arity == 8:
+            assert len(kids) == min(arity, xh - xl + 1), X
         assert mask[X] == (1 << len(kids)) - 1, X
         for i, c in enumerate(kids):
             want = c if c < L0 else (LEAF | (c - L0))
@@ -142,12 +161,13 @@ def test_wide_records_small_and_degenerate(R, oracle, collapse):
     assert rec.shape[0] == 1
 
 
-def test_wide_records_nonfinite_are_wild(R, oracle):
+@pytest.mark.parametrize("arity", [4, 8])
+def test_wide_records_nonfinite_are_wild(R, oracle, arity):
     tris = oracle.soup(500, 6).reshape(-1, 9).copy()
     tris[17, 0] = np.inf
     tris[301, 4] = -np.inf
-    rec = _check_wide(R, tris)
-    assert ((rec[:, 3] >> 24) & 1).any()
+    rec = _check_wide(R, tris, 1, arity)
+    assert _layout(rec)[1].any()
 
 
 def _render_all(R, tris, cam, w, h, spp, variant, cap=14):
@@ -202,7 +222,7 @@ def test_collapse_rules_render_identically(R, oracle, collapse, cap):
         hits, rgba = _render_all(R, tris, cam, w, h, spp, 0, cap)
     finally:
         R.config_set("build.wide_collapse", 1)
-        R.config_set("trace.stack_cap", 14)
+        R.config_set("trace.stack_cap", 0)
     _same(hits, rgba, eh, er)
 
 
@@ -257,7 +277,7 @@ def test_wide_work_counters(R, oracle):
     w, h = 320, 180
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     R.config_set("trace.variant", 0)
-    R.config_set("trace.stack_cap", 14)
+    R.config_set("trace.stack_cap", 0)
     with R.Scene.from_soup(tris) as s:
         s.build()
         binary = s.render_counters(cam, w, h, 1)

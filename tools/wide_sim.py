@@ -1,0 +1,67 @@
+"""Step counts of the wide traversal for K-ary greedy cuts (CPU model,
+tools/wide_sim.c): how much an 8-wide record would shorten the heavy rays'
+dependent chains.  Design experiment; uses the oracle's build.
+
+    python tools/wide_sim.py [n] [K ...]
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from oracle import oracle as O  # noqa: E402
+from gpu_raytracer_amd import scenes as S  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    ks = [int(k) for k in sys.argv[2:]] or [4, 8]
+    so = "/tmp/libwsim.so"
+    O.lib()
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+                    "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
+                    "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
+    L = C.CDLL(so)
+    tris = O.soup(n, 1)
+    b = O.build(tris)
+    nodes = b["nodes"]
+    v = S.VIEWS["soup"]
+    W, H = 1920, 1080
+    cam = O.camera_look_at(v.eye, v.at, v.up, v.vfov, W, H)
+    ref, _ = O.trace(nodes, tris, cam, W, H)
+    P = C.c_void_p
+    for K in ks:
+        cut = np.empty((n - 1) * K, np.uint32)
+        L.wsim_cut(nodes.ctypes.data_as(P), n, K, cut.ctypes.data_as(P))
+        steps = np.zeros(W * H, np.uint16)
+        recs = np.zeros(W * H, np.uint16)
+        leaves = np.zeros(W * H, np.uint16)
+        hitp = np.zeros(W * H, np.uint32)
+        msp = np.zeros(W * H, np.uint8)
+
+        def band(y0):
+            L.wsim_trace(nodes.ctypes.data_as(P), n, tris.ctypes.data_as(P), cut.ctypes.data_as(P), K,
+                         C.byref(cam), W, H, y0, min(H, y0 + 36), steps.ctypes.data_as(P),
+                         recs.ctypes.data_as(P), leaves.ctypes.data_as(P), hitp.ctypes.data_as(P), msp.ctypes.data_as(P))
+
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(band, range(0, H, 36)))
+        assert np.array_equal(hitp, ref["prim"]), "model disagrees with the oracle"
+        s = steps.astype(np.int64)
+        # per 8x8 quadrant: the wave's steps = its slowest lane's
+        q = s.reshape(H // 8, 8, W // 8, 8).max(axis=(1, 3))
+        print(f"K={K}: records {int(recs.sum()):,} leaves {int(leaves.sum()):,} steps {int(s.sum()):,} | "
+              f"per ray mean {s.mean():.2f} p99 {np.percentile(s, 99):.0f} p99.9 {np.percentile(s, 99.9):.0f} "
+              f"max {s.max()} | wave(8x8) max-lane steps mean {q.mean():.1f} p99 {np.percentile(q, 99):.0f} "
+              f"max {q.max()} | rays > 96 steps {(s > 96).sum()}, > 64 {(s > 64).sum()}, > 48 {(s > 48).sum()}",
+              flush=True)
+        print("   stack depth: " + " ".join(f">{c}:{int((msp > c).sum())}" for c in (8, 10, 12, 14, 16, 20, 24, 28)) + f" max {msp.max()}", flush=True)
+
+
+if __name__ == "__main__":
+    main()
