@@ -749,6 +749,9 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
     const bool valid = x < W && y < H;
     const SceneBox sb = scene_box(nodes);
+    // uniform: with the queue off (full frames by default) the per-step cap
+    // test, and its kernel-argument reload, drop out of the loop
+    const bool coop_on = !SHADOW && coop_cap != 0;
     uint32_t cn = 0, ct = 0, steps = 0;
     uint32_t qslot = 0, dsamp = RT_SENT;  // heavy-ray queue entry, deferred sample
     const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -778,10 +781,10 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                 const char* nd = reinterpret_cast<const char*>(nodes);
                 const WideMem M = wide_mem<WA>(wnodes, tri_s, n);
                 while (st == 0) {
-                    st = wide_step<COUNT, NT, false, PACKED || SHADOW, BUF, WA>(R, wnodes, tri_s, cam.eye, wcap,
-                                                                              4 * n + 16, s_ref + threadIdx.x,
-                                                                              s_tn + threadIdx.x, cn, ct, false, &M);
-                    if (!SHADOW && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
+                    st = wide_step<COUNT, NT, false, PACKED || SHADOW, BUF, WA>(
+                        R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16, s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct,
+                        false, &M);
+                    if (coop_on && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
                 }
                 if (PX) steps += R.steps;
                 if (st == 3) {  // heavy: k_trace_coop finishes this pixel from here on

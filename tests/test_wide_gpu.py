@@ -285,3 +285,4 @@ def test_wide_work_counters(R, oracle):
     assert wide[0] * 2 < binary[0]
     assert wide[1] >= binary[1]
 
+

@@ -123,3 +123,213 @@ void wsim_trace(const node_t* nodes, uint32_t n, const float* tris, const uint32
             maxsp[p] = (uint8_t)(msp > 255 ? 255 : msp);
         }
 }
+
+/* ---- wave model: the 64 lanes of each 8x8 quadrant step together; a step
+ * runs the leaf block when any lane tests a leaf and the record block when
+ * any lane tests a record.  policy 0 = today's (a popped leaf is tested in
+ * the next step); policy F > 0 = a per-lane FIFO of up to F popped leaves,
+ * served (one per lane) only when some lane cannot go on without it (FIFO
+ * full, or no record left) or at least T lanes hold one.  Leaves are folded
+ * in preorder either way (exact); records are tested with the current tb.
+ * out[0] wave-steps, out[1] leaf blocks run, out[2] record blocks run,
+ * out[3] lane-leaf tests, out[4] lane-record tests, out[5] sum over waves of
+ * the VALU cost model (40 + 116*leafblock + 136*recblock per step). */
+typedef struct {
+    uint32_t stk[48]; float stn[48]; uint32_t sp, cur; float ctn, tb; uint32_t hp, pix;
+    uint32_t fifo[16]; uint32_t fc; int done; float d[3], invd[3];
+} lane_t;
+
+static int leaf_test(const node_t* nodes, const float* tris, const float* o, lane_t* L, uint32_t leaf) {
+    float tn, t, u, v;
+    const node_t* lf = &nodes[leaf];
+    if (slab(lf, o, L->invd, L->tb, &tn) && orc_intersect_tri(o, L->d, tris + (size_t)lf->a * 9, L->tb, &t, &u, &v)) {
+        L->tb = t;
+        L->hp = lf->a;
+        return 1;
+    }
+    return 0;
+}
+
+void wsim_waves(const node_t* nodes, uint32_t n, const float* tris, const uint32_t* cut, uint32_t K, const cam_t* c,
+                uint32_t w, uint32_t h, uint32_t qy0, uint32_t qy1, uint32_t F, uint32_t T, double* out,
+                uint32_t* hitp) {
+    const uint32_t L0 = n - 1;
+    static __thread lane_t lanes[64];
+    for (uint32_t qy = qy0; qy < qy1; ++qy)
+        for (uint32_t qx = 0; qx < w / 8; ++qx) {
+            for (int l = 0; l < 64; ++l) {
+                lane_t* L = &lanes[l];
+                const uint32_t x = qx * 8 + (l & 7), y = qy * 8 + (l >> 3);
+                const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+                for (int a = 0; a < 3; ++a) {
+                    L->d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
+                    L->invd[a] = 1.0f / L->d[a];
+                }
+                L->tb = INFINITY; L->hp = 0xFFFFFFFFu; L->sp = 0; L->cur = 0; L->ctn = 0.0f; L->fc = 0; L->done = 0;
+            }
+            uint32_t pend[64];
+            for (int l = 0; l < 64; ++l) pend[l] = 0xFFFFFFFFu;
+            for (;;) {
+                int any = 0;
+                /* gather phase: pops */
+                int want = 0, have = 0;
+                for (int l = 0; l < 64; ++l) {
+                    lane_t* L = &lanes[l];
+                    if (L->done) continue;
+                    if (F == 0) {
+                        if (pend[l] == 0xFFFFFFFFu) {
+                            if (L->cur == 0xFFFFFFFFu && L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+                            if (L->cur != 0xFFFFFFFFu && L->cur >= L0) {
+                                pend[l] = L->cur; L->cur = 0xFFFFFFFFu;
+                                if (L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+                            }
+                        }
+                        if (pend[l] == 0xFFFFFFFFu && L->cur == 0xFFFFFFFFu) { L->done = 1; continue; }
+                    } else {
+                        for (;;) {
+                            if (L->cur == 0xFFFFFFFFu && L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+                            if (L->cur != 0xFFFFFFFFu && L->cur >= L0 && L->fc < F) { L->fifo[L->fc++] = L->cur; L->cur = 0xFFFFFFFFu; continue; }
+                            break;
+                        }
+                        if (L->fc == 0 && L->cur == 0xFFFFFFFFu) { L->done = 1; continue; }
+                        if (L->fc && (L->fc == F || L->cur == 0xFFFFFFFFu || L->cur >= L0)) want = 1;
+                        if (L->fc) ++have;
+                    }
+                    any = 1;
+                }
+                if (!any) break;
+                const int serve = F == 0 ? 1 : (want || have >= (int)T);
+                int lb = 0, rb = 0;
+                for (int l = 0; l < 64; ++l) {
+                    lane_t* L = &lanes[l];
+                    if (L->done) continue;
+                    if (F == 0) {
+                        if (pend[l] != 0xFFFFFFFFu) { lb = 1; out[3] += 1; leaf_test(nodes, tris, c->eye, L, pend[l]); pend[l] = 0xFFFFFFFFu; }
+                    } else if (serve && L->fc) {
+                        lb = 1; out[3] += 1;
+                        leaf_test(nodes, tris, c->eye, L, L->fifo[0]);
+                        memmove(&L->fifo[0], &L->fifo[1], sizeof(uint32_t) * (L->fc - 1));
+                        --L->fc;
+                    }
+                    if (L->cur == 0xFFFFFFFFu || L->cur >= L0) continue;
+                    if (L->ctn > L->tb) { L->cur = 0xFFFFFFFFu; continue; }
+                    rb = 1; out[4] += 1;
+                    const uint32_t* e = cut + (size_t)L->cur * K;
+                    uint32_t hit[16], m = 0;
+                    float htn[16];
+                    for (uint32_t i = 0; i < K && e[i] != 0xFFFFFFFFu; ++i) {
+                        float tn;
+                        if (slab(&nodes[e[i]], c->eye, L->invd, L->tb, &tn)) { hit[m] = e[i]; htn[m] = tn; ++m; }
+                    }
+                    L->cur = 0xFFFFFFFFu;
+                    if (m) {
+                        for (uint32_t i = m - 1; i >= 1; --i) { L->stk[L->sp] = hit[i]; L->stn[L->sp] = htn[i]; ++L->sp; }
+                        L->cur = hit[0]; L->ctn = htn[0];
+                    }
+                }
+                out[0] += 1; out[1] += lb; out[2] += rb;
+                out[5] += 40.0 + 116.0 * lb + 136.0 * rb;
+            }
+            for (int l = 0; l < 64; ++l) hitp[(size_t)(qy * 8 + (l >> 3)) * w + qx * 8 + (l & 7)] = lanes[l].hp;
+        }
+}
+
+/* ---- wave compaction model: pass 1 runs each 8x8-quadrant wave (policy 0
+ * steps) until fewer than A of its lanes are still tracing (after at least
+ * S steps); those rays are queued with their state and pass 2 runs the queue
+ * packed 64 rays per wave, in queue order, to completion.  out as
+ * wsim_waves (pass 1 + pass 2), out[6] = rays queued. */
+static void run_wave(const node_t* nodes, uint32_t n, const float* tris, const uint32_t* cut, uint32_t K,
+                     const float* o, lane_t* lanes, int nl, uint32_t A, uint32_t S, double* out, lane_t* q,
+                     size_t* nq) {
+    const uint32_t L0 = n - 1;
+    uint32_t pend[64];
+    for (int l = 0; l < 64; ++l) pend[l] = 0xFFFFFFFFu;
+    for (uint32_t step = 0;; ++step) {
+        int act = 0;
+        for (int l = 0; l < nl; ++l) {
+            lane_t* L = &lanes[l];
+            if (L->done) continue;
+            if (pend[l] == 0xFFFFFFFFu) {
+                if (L->cur == 0xFFFFFFFFu && L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+                if (L->cur != 0xFFFFFFFFu && L->cur >= L0) {
+                    pend[l] = L->cur; L->cur = 0xFFFFFFFFu;
+                    if (L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+                }
+            }
+            if (pend[l] == 0xFFFFFFFFu && L->cur == 0xFFFFFFFFu) { L->done = 1; continue; }
+            ++act;
+        }
+        if (!act) break;
+        if (q && step >= S && (uint32_t)act < A) {  /* compact: queue the live rays (pending leaf back on top) */
+            for (int l = 0; l < nl; ++l) {
+                lane_t* L = &lanes[l];
+                if (L->done) continue;
+                if (pend[l] != 0xFFFFFFFFu) {  /* order: pend, cur, stack */
+                    if (L->cur != 0xFFFFFFFFu) { L->stk[L->sp] = L->cur; L->stn[L->sp] = L->ctn; ++L->sp; }
+                    L->cur = pend[l]; L->ctn = 0.0f;
+                }
+                q[(*nq)++] = *L;
+                L->done = 1;
+            }
+            out[6] += act;
+            break;
+        }
+        int lb = 0, rb = 0;
+        for (int l = 0; l < nl; ++l) {
+            lane_t* L = &lanes[l];
+            if (L->done) continue;
+            if (pend[l] != 0xFFFFFFFFu) { lb = 1; out[3] += 1; leaf_test(nodes, tris, o, L, pend[l]); pend[l] = 0xFFFFFFFFu; }
+            if (L->cur == 0xFFFFFFFFu || L->cur >= L0) continue;
+            if (L->ctn > L->tb) { L->cur = 0xFFFFFFFFu; continue; }
+            rb = 1; out[4] += 1;
+            const uint32_t* e = cut + (size_t)L->cur * K;
+            uint32_t hit[16], m = 0;
+            float htn[16];
+            for (uint32_t i = 0; i < K && e[i] != 0xFFFFFFFFu; ++i) {
+                float tn;
+                if (slab(&nodes[e[i]], o, L->invd, L->tb, &tn)) { hit[m] = e[i]; htn[m] = tn; ++m; }
+            }
+            L->cur = 0xFFFFFFFFu;
+            if (m) {
+                for (uint32_t i = m - 1; i >= 1; --i) { L->stk[L->sp] = hit[i]; L->stn[L->sp] = htn[i]; ++L->sp; }
+                L->cur = hit[0]; L->ctn = htn[0];
+            }
+        }
+        out[0] += 1; out[1] += lb; out[2] += rb;
+        out[5] += 40.0 + 116.0 * lb + 136.0 * rb;
+    }
+}
+
+void wsim_compact(const node_t* nodes, uint32_t n, const float* tris, const uint32_t* cut, uint32_t K, const cam_t* c,
+                  uint32_t w, uint32_t h, uint32_t qy0, uint32_t qy1, uint32_t A, uint32_t S, double* out,
+                  uint32_t* hitp) {
+    lane_t lanes[64];
+    const size_t cap = (size_t)(qy1 - qy0) * (w / 8) * 64;
+    lane_t* q = (lane_t*)malloc(sizeof(lane_t) * cap);
+    size_t nq = 0;
+    for (uint32_t qy = qy0; qy < qy1; ++qy)
+        for (uint32_t qx = 0; qx < w / 8; ++qx) {
+            for (int l = 0; l < 64; ++l) {
+                lane_t* L = &lanes[l];
+                const uint32_t x = qx * 8 + (l & 7), y = qy * 8 + (l >> 3);
+                const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+                for (int a = 0; a < 3; ++a) {
+                    L->d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
+                    L->invd[a] = 1.0f / L->d[a];
+                }
+                L->tb = INFINITY; L->hp = 0xFFFFFFFFu; L->sp = 0; L->cur = 0; L->ctn = 0.0f; L->fc = 0; L->done = 0;
+                L->pix = y * w + x;
+            }
+            run_wave(nodes, n, tris, cut, K, c->eye, lanes, 64, A, S, out, q, &nq);
+            for (int l = 0; l < 64; ++l) if (lanes[l].hp != 0xFFFFFFFFu || 1) hitp[lanes[l].pix] = lanes[l].hp;
+        }
+    /* pass 2: the queue, 64 rays per wave; a queued ray's hit is written at the end */
+    for (size_t b = 0; b < nq; b += 64) {
+        const int nl = (int)(nq - b < 64 ? nq - b : 64);
+        for (int l = 0; l < nl; ++l) { lanes[l] = q[b + l]; lanes[l].done = 0; }
+        run_wave(nodes, n, tris, cut, K, c->eye, lanes, nl, 0, 0, out, NULL, NULL);
+        for (int l = 0; l < nl; ++l) hitp[lanes[l].pix] = lanes[l].hp;
+    }
+    free(q);
+}

@@ -63,5 +63,89 @@ def main():
         print("   stack depth: " + " ".join(f">{c}:{int((msp > c).sum())}" for c in (8, 10, 12, 14, 16, 20, 24, 28)) + f" max {msp.max()}", flush=True)
 
 
+
+
+def waves(n=1_000_000, policies=((0, 0), (4, 16), (4, 24), (4, 32), (6, 24), (8, 24))):
+    """Wave model of leaf deferral (wsim_waves): steps, block counts, VALU."""
+    so = "/tmp/libwsim.so"
+    O.lib()
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+                    "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
+                    "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
+    L = C.CDLL(so)
+    tris = O.soup(n, 1)
+    b = O.build(tris)
+    nodes = b["nodes"]
+    v = S.VIEWS["soup"]
+    W, H = 1920, 1080
+    cam = O.camera_look_at(v.eye, v.at, v.up, v.vfov, W, H)
+    ref, _ = O.trace(nodes, tris, cam, W, H)
+    P = C.c_void_p
+    K = 4
+    cut = np.empty((n - 1) * K, np.uint32)
+    L.wsim_cut(nodes.ctypes.data_as(P), n, K, cut.ctypes.data_as(P))
+    for F, T in policies:
+        hitp = np.zeros(W * H, np.uint32)
+        outs = [np.zeros(6) for _ in range(8)]
+        bands = np.array_split(np.arange(H // 8), 8)
+
+        def run(i):
+            L.wsim_waves(nodes.ctypes.data_as(P), n, tris.ctypes.data_as(P), cut.ctypes.data_as(P), K, C.byref(cam),
+                         W, H, int(bands[i][0]), int(bands[i][-1] + 1), F, T, outs[i].ctypes.data_as(P),
+                         hitp.ctypes.data_as(P))
+
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(run, range(8)))
+        o = sum(outs)
+        assert np.array_equal(hitp, ref["prim"]), "model disagrees with the oracle"
+        print(f"F={F} T={T}: wave-steps {o[0]:,.0f} leaf blocks {o[1]:,.0f} ({o[3] / max(o[1], 1):.1f} lanes) "
+              f"record blocks {o[2]:,.0f} ({o[4] / max(o[2], 1):.1f} lanes) lane-records {o[4]:,.0f} "
+              f"VALU model {o[5]:,.0f}", flush=True)
+
+
+def compact(n=1_000_000, policies=((0, 0), (16, 8), (24, 8), (32, 8), (24, 16), (32, 16), (40, 16))):
+    """Wave-compaction model (wsim_compact): pass 1 until < A lanes live, pass 2 packed."""
+    so = "/tmp/libwsim.so"
+    O.lib()
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+                    "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
+                    "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
+    L = C.CDLL(so)
+    tris = O.soup(n, 1)
+    b = O.build(tris)
+    nodes = b["nodes"]
+    v = S.VIEWS["soup"]
+    W, H = 1920, 1080
+    cam = O.camera_look_at(v.eye, v.at, v.up, v.vfov, W, H)
+    ref, _ = O.trace(nodes, tris, cam, W, H)
+    P = C.c_void_p
+    K = 4
+    cut = np.empty((n - 1) * K, np.uint32)
+    L.wsim_cut(nodes.ctypes.data_as(P), n, K, cut.ctypes.data_as(P))
+    for A, Smin in policies:
+        hitp = np.zeros(W * H, np.uint32)
+        outs = [np.zeros(7) for _ in range(8)]
+        bands = np.array_split(np.arange(H // 8), 8)
+
+        def run(i):
+            L.wsim_compact(nodes.ctypes.data_as(P), n, tris.ctypes.data_as(P), cut.ctypes.data_as(P), K,
+                           C.byref(cam), W, H, int(bands[i][0]), int(bands[i][-1] + 1), A, Smin,
+                           outs[i].ctypes.data_as(P), hitp.ctypes.data_as(P))
+
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(run, range(8)))
+        o = sum(outs)
+        assert np.array_equal(hitp, ref["prim"]), "model disagrees with the oracle"
+        print(f"A={A} S={Smin}: wave-steps {o[0]:,.0f} leaf blocks {o[1]:,.0f} ({o[3] / max(o[1], 1):.1f} lanes) "
+              f"record blocks {o[2]:,.0f} ({o[4] / max(o[2], 1):.1f} lanes) queued {o[6]:,.0f} "
+              f"VALU model {o[5]:,.0f}", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "compact":
+        compact()
+        sys.exit(0)
+    if len(sys.argv) > 1 and sys.argv[1] == "waves":
+        waves()
+    else:
+        main()
