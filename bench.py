@@ -11,11 +11,14 @@ previous one):
 W untimed warm-up steps, then K timed steps between barrier+synchronize on
 both sides; the max over ranks is reported by rank 0 as ONE JSON line.
 
-  value      = W*H*spp / (mean over steps of max-rank trace time + gather time)
+  value      = W*H*spp / (mean over steps of the max-rank frame span)
                [Mrays/s, whole image, all ranks; SURVEY.md §8(e)].  At N>1 the
                trace, the RCCL gather and the unpack are queued back to back
-               on torch's stream and timed together with events on it
-               (gather time = that span minus the trace)
+               on torch's stream and timed together with events on it: the
+               frame span is trace start -> the gathered image unpacked (rank
+               0) or the slab sent (others); gather_ms = span - trace.  (Until
+               r02 value used max trace + max gather, which counted a slow
+               rank's lead twice: in its trace and in rank 0's wait.)
   value_cold = the same frame with row-major tile dispatch (a first frame: no
                previous frame's cost map); static_camera = the same camera
                every frame (the map replays an identical frame: best case)
@@ -334,9 +337,10 @@ def main():
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
     def frame(cam):
-        """trace (+ gather + unpack) of one frame; returns (trace_ms, gather_ms)."""
+        """trace (+ gather + unpack) of one frame; returns (trace_ms, frame_ms)."""
         if world == 1:
-            return scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True), 0.0
+            t = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+            return t, t
         cur = torch.cuda.current_stream(dev)
         if args.dist_backend == "nccl":
             # trace -> RCCL gather -> unpack queued back to back on torch's
@@ -352,8 +356,7 @@ def main():
                                       cur.cuda_stream)
             ev[2].record(cur)
             ev[2].synchronize()
-            trace_ms = ev[0].elapsed_time(ev[1])
-            return trace_ms, ev[0].elapsed_time(ev[2]) - trace_ms
+            return ev[0].elapsed_time(ev[1]), ev[0].elapsed_time(ev[2])
         # gloo rehearsal: stage through host memory, host-timed
         trace_ms = scene.render_tiles_device(cam, w, h, spp, rank, world, slab.data_ptr(), slab_hits.data_ptr(),
                                              timed=True)
@@ -364,7 +367,7 @@ def main():
             R.unpack_tiles_device(slabs_all.data_ptr(), max(tmax, 1), w, h, world, img.data_ptr(), local,
                                   torch.cuda.current_stream(dev).cuda_stream)
         torch.cuda.synchronize(dev)
-        return trace_ms, (time.perf_counter() - t0) * 1e3
+        return trace_ms, trace_ms + (time.perf_counter() - t0) * 1e3
 
     def step(i):
         build_ms = scene.build()
@@ -382,7 +385,7 @@ def main():
     rec = [step(args.warmup + i) for i in range(args.steps)]
     barrier()
     wall = time.perf_counter() - t0
-    per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, gather (ms)
+    per = np.array(rec, dtype=np.float64)  # [steps, 3] build, trace, frame span (ms)
     rank_trace_ms = float(per[:, 1].mean())
     if args.only_timed:  # profiler passes: the dispatches after the warm-up are the timed ones
         if rank == 0:
@@ -436,7 +439,8 @@ def main():
         t = torch.tensor(np.append(extra, wall), dtype=torch.float64, device=rdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         extra, wall = t.cpu().numpy()[:2], float(t[2].item())
-    build_ms, trace_ms, gather_ms = (float(x) for x in per.mean(axis=0))
+    build_ms, trace_ms, frame_ms = (float(x) for x in per.mean(axis=0))
+    gather_ms = max(frame_ms - trace_ms, 0.0)
     cold_ms, static_ms = (float(x) for x in extra)
 
     # "rank 0 builds and then broadcasts" measured next to the
@@ -496,7 +500,7 @@ def main():
 
     out = None
     if rank == 0:
-        value = rays / ((trace_ms + gather_ms) * 1e-3) / 1e6
+        value = rays / (frame_ms * 1e-3) / 1e6
         achieved = kernel_bytes / (rank_trace_ms * 1e-3) / 1e9
         frac = achieved / HBM_PEAK_GBS
         pmc = load_pmc(args.pmc_json, cfg.name, world)

@@ -304,11 +304,26 @@ __device__ __forceinline__ void store_node(void* nodes, uint32_t idx, const Aabb
 // three aligned 16-B words.  The trace recomputes the leaf box (tri_bounds)
 // and the Moller-Trumbore edges from the exact vertices, with the same fp32
 // operations K4 and §9.7 use.
-__device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint32_t k, const float* t, uint32_t prim) {
+// Leaf-ordered triangle record k (48 B): {v0, v1, v2, prim, esc, 0}.  esc is
+// leaf k's escape link: with the prim and the box (tri_bounds of the
+// vertices) the record holds the whole binary leaf node, so the build does
+// not write leaf nodes (rt_bvh_read derives them: k_leaf_nodes).
+__device__ __forceinline__ void store_leaf_tri(float4* __restrict__ tri_s, uint32_t k, const float* t, uint32_t prim,
+                                               uint32_t esc) {
     float4* o = tri_s + (uint64_t)k * 3;
     o[0] = make_float4(t[0], t[1], t[2], t[3]);
     o[1] = make_float4(t[4], t[5], t[6], t[7]);
-    o[2] = make_float4(t[8], __uint_as_float(prim), 0.0f, 0.0f);
+    o[2] = make_float4(t[8], __uint_as_float(prim), __uint_as_float(esc), 0.0f);
+}
+
+// leaf k's box from its triangle record (§9.2, as the leaf node holds it)
+__device__ __forceinline__ Aabb leaf_box(const float4* __restrict__ tri_s, uint32_t k) {
+    const float4* p = tri_s + (uint64_t)k * 3;
+    const float4 A = p[0], B = p[1], C = p[2];
+    const float t[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x};
+    Aabb b;
+    tri_bounds(t, b.lo, b.hi);
+    return b;
 }
 
 // Stage the sorted keys [B - KW, B + NT + KW) of a block of NT threads.
@@ -372,7 +387,7 @@ __device__ __forceinline__ LeafTri gather_leaf(uint32_t prim, const float* __res
 __device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafTri& lt, uint32_t n, uint32_t i32,
                                                  uint4* __restrict__ topo, uint32_t* __restrict__ parent,
                                                  void* __restrict__ nodes, float4* __restrict__ tri_s, uint4& tp_out,
-                                                 Aabb& box, bool allow_defer, bool& deferred) {
+                                                 Aabb& box, bool allow_defer, bool& deferred, bool leaf_node = false) {
     const int64_t i = i32, N = n;
     const uint32_t L0 = n - 1;
     if (i32 == 0 && parent) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
@@ -417,8 +432,8 @@ __device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafT
         lesc = RT_SENT;  // leaf n-1
     }
     tri_bounds(lt.v, box.lo, box.hi);
-    store_node(nodes, L0 + i32, box, lt.prim, lesc);
-    store_leaf_tri(tri_s, i32, lt.v, lt.prim);
+    if (leaf_node) store_node(nodes, L0 + i32, box, lt.prim, lesc);  // the stage entry point's full node array
+    store_leaf_tri(tri_s, i32, lt.v, lt.prim, lesc);
 }
 
 // Largest t in [0, R) with delta(i, i + t d) > thr, all 64 lanes probing at
@@ -480,7 +495,7 @@ __global__ __launch_bounds__(256) void k_karras_leaves(const uint32_t* __restric
     uint4 tp;
     Aabb box;
     bool deferred;
-    karras_node_leaf(keys, lt, n, i32, topo, parent, nodes, tri_s, tp, box, false, deferred);
+    karras_node_leaf(keys, lt, n, i32, topo, parent, nodes, tri_s, tp, box, false, deferred, true);
 }
 
 // Stand-alone leaf-triangle pass (rt_stage_trace on caller nodes).
@@ -488,11 +503,23 @@ __global__ __launch_bounds__(256) void k_leaf_tris(const void* __restrict__ node
                                                    uint32_t n, float4* __restrict__ tri_s) {
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     if (k >= n) return;
-    const uint32_t prim = reinterpret_cast<const uint32_t*>(nodes)[((uint64_t)(n - 1) + k) * 8 + 6];
+    const uint32_t* leaf = reinterpret_cast<const uint32_t*>(nodes) + ((uint64_t)(n - 1) + k) * 8;
+    const uint32_t prim = leaf[6];
     float t[9];
 #pragma unroll
     for (int c = 0; c < 9; ++c) t[c] = tris[(uint64_t)prim * 9 + c];
-    store_leaf_tri(tri_s, k, t, prim);
+    store_leaf_tri(tri_s, k, t, prim, leaf[7]);
+}
+
+// The binary leaf nodes L0 + k, derived from the triangle records
+// (rt_bvh_read / rt_bvh_save / rt_stage_refit: the build writes internal
+// nodes only).
+__global__ __launch_bounds__(256) void k_leaf_nodes(const float4* __restrict__ tri_s, uint32_t n,
+                                                    void* __restrict__ nodes) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k >= n) return;
+    const float4 C = tri_s[(uint64_t)k * 3 + 2];
+    store_node(nodes, n - 1 + k, leaf_box(tri_s, k), __float_as_uint(C.y), __float_as_uint(C.z));
 }
 
 // ---------------------------------------------------------------- K6 refit
@@ -953,8 +980,8 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
 template <int W>
 __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ topo, const uint32_t* __restrict__ cross,
                                                     const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
-                                                    const void* __restrict__ nodes, uint32_t n,
-                                                    uint4* __restrict__ wnodes, uint32_t collapse) {
+                                                    const void* __restrict__ nodes, const float4* __restrict__ tri_s,
+                                                    uint32_t n, uint4* __restrict__ wnodes, uint32_t collapse) {
     uint32_t pre[kCrossShards + 1];
     pre[0] = 0;
 #pragma unroll
@@ -969,11 +996,11 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         if (X >= L0) continue;
         const uint4 tx = topo[X];
         uint32_t node[W];
-        wide_entries<W>(tx, L0, [&](uint32_t i) { return topo[i]; },
-                        [&](uint32_t i) { return load_aabb_node(nodes, i); }, collapse, node);
+        // internal boxes from `nodes`, leaf boxes from the triangle records
+        const auto box_of = [&](uint32_t i) { return i >= L0 ? leaf_box(tri_s, i - L0) : load_aabb_node(nodes, i); };
+        wide_entries<W>(tx, L0, [&](uint32_t i) { return topo[i]; }, box_of, collapse, node);
         const Aabb bx = load_aabb_node(nodes, X);
-        store_wide<W>(wnodes, X, bx, node,
-                      [&](int i) { return load_aabb_node(nodes, node[i] == RT_SENT ? X : node[i]); }, L0);
+        store_wide<W>(wnodes, X, bx, node, [&](int i) { return box_of(node[i] == RT_SENT ? X : node[i]); }, L0);
     }
 }
 
@@ -1061,6 +1088,12 @@ hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* param
     return launch_morton_impl(tris, n, const_cast<BuildParams*>(params), nullptr, 0, keys, vals, ghist, counts0, s);
 }
 
+hipError_t launch_leaf_nodes(const float4* tri_s, uint32_t n, void* nodes, hipStream_t s) {
+    if (!n) return hipSuccess;
+    hipLaunchKernelGGL(k_leaf_nodes, dim3(cdiv(n, 256)), dim3(256), 0, s, tri_s, n, nodes);
+    return hipGetLastError();
+}
+
 hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, float4* tri_s, hipStream_t s) {
     if (!n) return hipSuccess;
     hipLaunchKernelGGL(k_leaf_tris, dim3(cdiv(n, 256)), dim3(256), 0, s, nodes, tris, n, tri_s);
@@ -1115,10 +1148,10 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
     }
     if (arity == 8)
         hipLaunchKernelGGL(k_wide_cross<8>, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.nodes, n, b.wnodes, wide_collapse);
+                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     else
         hipLaunchKernelGGL(k_wide_cross<4>, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.nodes, n, b.wnodes, wide_collapse);
+                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     return hipGetLastError();
 }
 

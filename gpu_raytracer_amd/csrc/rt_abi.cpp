@@ -253,6 +253,16 @@ rt_status primary(rt_scene* s, Replica** out) {
 uint32_t build_arity(uint32_t n) { return (rt::config_snapshot().wide_arity == 8 && n <= rt::kWide8MaxN) ? 8u : 4u; }
 uint64_t wide_bytes(uint32_t arity) { return arity == 8 ? 96u : 64u; }
 
+// Write the binary leaf nodes from the triangle records (the build writes
+// internal nodes only: store_leaf_tri) for readers of the whole node array
+// (rt_bvh_read, rt_bvh_save); the trace never reads them.
+rt_status materialize_leaves(Replica& r, uint32_t n) {
+    HIPR(hipSetDevice(r.device));
+    HIPR(rt::launch_leaf_nodes(r.bufs.tri_s, n, r.bufs.nodes, r.stream));
+    HIPR(hipStreamSynchronize(r.stream));
+    return RT_OK;
+}
+
 Replica* primary_built(const rt_scene* s) {
     return (!s->reps.empty() && s->reps[0]->built) ? s->reps[0].get() : nullptr;
 }
@@ -654,6 +664,7 @@ rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* keys, uint32_
     if (r->last_stream) HIPR(hipEventSynchronize(r->last));
     HIPR(hipStreamSynchronize(r->stream));
     const size_t n = s->n, tot = n ? 2 * n - 1 : 0;
+    RTR(materialize_leaves(*r, s->n));
     if (nodes && tot) HIPR(hipMemcpy(nodes, r->bufs.nodes, tot * 32, hipMemcpyDeviceToHost));
     if (keys && n) HIPR(hipMemcpy(keys, r->bufs.keys[0], n * 4, hipMemcpyDeviceToHost));
     if (vals && n) HIPR(hipMemcpy(vals, r->bufs.vals[0], n * 4, hipMemcpyDeviceToHost));
@@ -719,14 +730,15 @@ rt_status rt_bvh_replicas(const rt_scene* s, uint32_t max, int* devices, uint32_
 // triangle bytes, u64 layout tag, then the device buffers the trace and
 // rt_bvh_read use, in order: BuildParams (64 B), sorted keys and vals (n x 4),
 // nodes ((2n-1) x 32), tri_s (n x 48), wide records ((n-1) x 64).  The tag
-// changes whenever one of those layouts does (revision 2: no parent section).
+// changes whenever one of those layouts does (revision 2: no parent section;
+// 3: triangle records carry the leaf escape link).
 }  // extern "C"
 
 namespace {
 const char kBvhMagic[8] = {'R', 'T', 'B', 'V', 'H', '1', 0, 0};
 constexpr uint32_t kBvhVersion = 1;
-constexpr uint64_t kBvhLayout = 0x7274616d64000002ull;   // "rtamd" + layout revision 2 (4-ary records)
-constexpr uint64_t kBvhLayout8 = 0x7274616d64000082ull;  // the same with 8-ary (K7w8) records
+constexpr uint64_t kBvhLayout = 0x7274616d64000003ull;   // "rtamd" + layout revision 3 (4-ary records)
+constexpr uint64_t kBvhLayout8 = 0x7274616d64000083ull;  // the same with 8-ary (K7w8) records
 
 uint64_t fnv1a(const void* p, size_t bytes) {
     const unsigned char* b = static_cast<const unsigned char*>(p);
@@ -770,6 +782,7 @@ rt_status rt_bvh_save(const rt_scene* s, const char* path) {
     if (!r) return fail(RT_EINVAL, "scene not built");
     HIPR(hipSetDevice(r->device));
     HIPR(hipStreamSynchronize(r->stream));
+    RTR(materialize_leaves(*r, s->n));
     FILE* f = std::fopen(path, "wb");
     if (!f) return fail(RT_EIO, std::string("cannot create ") + path);
     const uint32_t hv[2] = {kBvhVersion, s->n};
@@ -1460,6 +1473,7 @@ rt_status rt_stage_refit(int device, const uint32_t* sorted_keys, const uint32_t
     HIPR(hipMemcpy(b.keys[0], sorted_keys, (size_t)n * 4, hipMemcpyHostToDevice));
     HIPR(hipMemcpy(b.vals[0], sorted_vals, (size_t)n * 4, hipMemcpyHostToDevice));
     HIPR(rt::launch_refit_stage(b, n, 0));
+    HIPR(rt::launch_leaf_nodes(b.tri_s, n, b.nodes, 0));
     HIPR(hipDeviceSynchronize());
     HIPR(hipMemcpy(nodes_out, b.nodes, (size_t)(2 * n - 1) * 32, hipMemcpyDeviceToHost));
     return RT_OK;

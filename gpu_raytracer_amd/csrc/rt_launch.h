@@ -16,8 +16,9 @@ struct BuildBufs {
     float* tris = nullptr;          // n*9 fp32, AoS (36 B/tri), 256-B aligned
     uint32_t* keys[2] = {nullptr, nullptr};
     uint32_t* vals[2] = {nullptr, nullptr};
-    void* nodes = nullptr;          // (2n-1) x 32 B {lo[3], hi[3], a, esc}
-    float4* tri_s = nullptr;        // n x 48 B leaf-ordered {v0, e1, e2} for the trace
+    void* nodes = nullptr;          // (2n-1) x 32 B {lo[3], hi[3], a, esc}; the build writes the internal
+                                    // n-1 (leaves: tri_s, launch_leaf_nodes)
+    float4* tri_s = nullptr;        // n x 48 B leaf-ordered {v0, v1, v2, prim, leaf escape, 0} for the trace
     uint32_t* parent = nullptr;     // 2n-1, unified index space
     uint4* topo = nullptr;          // n-1 x {left, esc, range_lo, range_hi}
     uint4* wnodes = nullptr;        // n-1 x 64 B (K7w, 4-ary) or 96 B (K7w8, 8-ary) wide trace records
@@ -85,6 +86,9 @@ hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const floa
 uint32_t sort_tiles(uint32_t n);
 uint32_t bounds_grid(uint32_t n);  // K0/K1 workgroups (8 tris per thread)
 hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, float4* tri_s, hipStream_t s);
+// binary leaf nodes (2n-1 node array, leaves L0 + k) from the triangle
+// records: the build writes internal nodes only (store_leaf_tri)
+hipError_t launch_leaf_nodes(const float4* tri_s, uint32_t n, void* nodes, hipStream_t s);
 
 struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 
@@ -115,8 +119,9 @@ struct TraceConfig {
     uint32_t buf_loads = 1;       // wide step loads through buffer descriptors (one round trip per step)
     uint32_t coop_cap = 0;        // primary full frames: rays past this many wide steps finish in k_trace_coop
                                   // (one wave per ray); 0 = off
-    uint32_t coop_cap_tiles = 96; // the same for one rank's tiles of a multi-GPU frame (tools/coop_sweep.py)
-    uint32_t coop_lanes = 64;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
+    uint32_t coop_cap_tiles = 80; // the same for one rank's tiles of a multi-GPU frame (tools/coop_sweep.py,
+                                  // profiles/coop_sweep_r02b.log)
+    uint32_t coop_lanes = 32;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
     uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
 };

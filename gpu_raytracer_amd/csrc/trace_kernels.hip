@@ -62,16 +62,15 @@ __device__ __forceinline__ bool intersect_tri(const float* o, const float* d, co
     return intersect_e(o, d, tri, e1, e2, tb, tout, uout, vout);
 }
 
-// §9.7 stackless escape-link traversal of one ray over the 32-B nodes (two
-// 16-B loads per node), with the leaf's triangle test deferred by one step:
-// after a leaf's box hits, the next node is always its escape, which the
-// leaf record already names, so the next step issues the escape node's
-// loads AND the leaf's triangle loads together, tests the triangle first (it
-// may shrink tb) and the node box second -- the §9.7 order, hence the same
-// tests with the same operands.  A wave step then costs one memory round
-// trip instead of two whenever some lane is at a leaf (+2-4 %,
-// profiles/ab_trace_r01_variants.log).  A well-formed tree visits each node
-// once; the guard and index checks only keep a malformed one from faulting.
+// §9.7 stackless escape-link traversal of one ray: an internal node is its
+// 32-B record (two 16-B loads), a leaf its 48-B triangle record (box from the
+// vertices, prim and escape link in the record's spare words), so a leaf
+// costs one memory round trip for the box test and the Moller-Trumbore test
+// together -- the §9.7 order, hence the same tests with the same operands.
+// (Until r02 the build also wrote 32-B leaf nodes and a leaf's triangle test
+// was deferred one step to share the escape node's round trip.)  A
+// well-formed tree visits each node once; the guard and index checks only
+// keep a malformed one from faulting.
 //
 // trace_ray_from resumes that loop at node `start` with the caller's
 // tb/hu/hv/hp: exact whenever every leaf before `start` in preorder has been
@@ -88,37 +87,44 @@ __device__ __forceinline__ void trace_ray_from(const char* __restrict__ nodes, c
     const uint32_t L0 = n ? n - 1 : 0;
     const uint32_t total = n ? 2 * n - 1 : 0;
     uint32_t idx = start;
-    uint32_t pend = RT_SENT, pprim = 0;  // leaf whose triangle test is due
-    for (uint32_t guard = 0; (idx < total || pend != RT_SENT) && guard <= total; ++guard) {
-        float4 A, B;
-        const bool node = idx < total;
-        if (node) {
-            const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)idx * 32);
-            A = np[0]; B = np[1];
-        }
-        if (pend != RT_SENT) {
-            if (COUNT) ++ct;
-            const float4* tp = tri_s + (uint64_t)pend * 3;
-            const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
-            const float tv[9] = {T0.x, T0.y, T0.z, T0.w, T1.x, T1.y, T1.z, T1.w, T2.x};
-            float t, u, v;
-            if (intersect_tri(o, d, tv, tb, t, u, v)) {
-                tb = t; hu = u; hv = v; hp = pprim;
-                if (any) return;  // any-hit (shadow ray): the first hit ends the search
-            }
-            pend = RT_SENT;
-        }
-        if (!node) break;
+    // A leaf is read from its triangle record {v0, v1, v2, prim, esc}: its box
+    // is tri_bounds of the vertices (the build writes no leaf nodes), and the
+    // Moller-Trumbore test uses the same loads.
+    for (uint32_t guard = 0; idx < total && guard <= total; ++guard) {
         if (COUNT) ++cn;
-        const float t0x = (A.x - o[0]) * invd[0], t1x = (A.w - o[0]) * invd[0];
-        const float t0y = (A.y - o[1]) * invd[1], t1y = (B.x - o[1]) * invd[1];
-        const float t0z = (A.z - o[2]) * invd[2], t1z = (B.y - o[2]) * invd[2];
+        float lo[3], hi[3], tv[9];
+        uint32_t na, esc;
+        const bool leaf = idx >= L0;
+        if (leaf) {
+            const float4* tp = tri_s + (uint64_t)(idx - L0) * 3;
+            const float4 T0 = tp[0], T1 = tp[1], T2 = tp[2];
+            tv[0] = T0.x; tv[1] = T0.y; tv[2] = T0.z; tv[3] = T0.w; tv[4] = T1.x;
+            tv[5] = T1.y; tv[6] = T1.z; tv[7] = T1.w; tv[8] = T2.x;
+            tri_bounds(tv, lo, hi);
+            na = __float_as_uint(T2.y);
+            esc = __float_as_uint(T2.z);
+        } else {
+            const float4* np = reinterpret_cast<const float4*>(nodes + (uint64_t)idx * 32);
+            const float4 A = np[0], B = np[1];
+            lo[0] = A.x; lo[1] = A.y; lo[2] = A.z; hi[0] = A.w; hi[1] = B.x; hi[2] = B.y;
+            na = __float_as_uint(B.z);
+            esc = __float_as_uint(B.w);
+        }
+        const float t0x = (lo[0] - o[0]) * invd[0], t1x = (hi[0] - o[0]) * invd[0];
+        const float t0y = (lo[1] - o[1]) * invd[1], t1y = (hi[1] - o[1]) * invd[1];
+        const float t0z = (lo[2] - o[2]) * invd[2], t1z = (hi[2] - o[2]) * invd[2];
         const float tn = fmaxf(fmaxf(fmaxf(fminf(t0x, t1x), fminf(t0y, t1y)), fminf(t0z, t1z)), 0.0f);
         const float tf = fminf(fminf(fminf(fmaxf(t0x, t1x), fmaxf(t0y, t1y)), fmaxf(t0z, t1z)), tb);
-        const uint32_t na = __float_as_uint(B.z), esc = __float_as_uint(B.w);
         const bool hit = tn <= tf;
-        if (hit && idx >= L0) { pend = idx - L0; pprim = na; }
-        idx = (hit && idx < L0) ? na : esc;
+        if (hit && leaf) {
+            if (COUNT) ++ct;
+            float t, u, v;
+            if (intersect_tri(o, d, tv, tb, t, u, v)) {
+                tb = t; hu = u; hv = v; hp = na;
+                if (any) return;  // any-hit (shadow ray): the first hit ends the search
+            }
+        }
+        idx = (hit && !leaf) ? na : esc;
     }
 }
 
@@ -652,6 +658,9 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
 #ifndef RT_KSHADOW_WAVES
 #define RT_KSHADOW_WAVES 5
 #endif
+#ifndef RT_KTILES_WAVES
+#define RT_KTILES_WAVES 5
+#endif
 constexpr uint32_t kCoopShards = 64;
 constexpr uint32_t kCoopFrontier = kWideStackMax + 1;        // pending entries a deferred ray can have (either arity)
 constexpr uint32_t kCoopEntry = 3 + (kCoopFrontier + 1) / 2;  // uint4 per queue entry
@@ -706,7 +715,7 @@ __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t
 }
 
 template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4>
-__global__ __launch_bounds__(NT, (SHADOW && WA == 4) ? RT_KSHADOW_WAVES : RT_KTRACE_WAVES)
+__global__ __launch_bounds__(NT, (SHADOW && WA == 4) ? RT_KSHADOW_WAVES : (PACKED && WA == 4) ? RT_KTILES_WAVES : RT_KTRACE_WAVES)
 void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
                                                Cam cam, uint32_t W, uint32_t H, uint32_t spp,

@@ -225,11 +225,12 @@ def distributed_build(st, ex: Exchange) -> dict:
     nc = st.subtrees(rank, P)
     shares = [dbuild_shares_of(n, q, P) for q in range(P)]
     ni = max(n - 1, 0)
+    # wide records: 16 words (4-ary) or 24 (8-ary, build.wide_arity)
+    wwpe = len(st.buf(_L.RT_DB_WIDE)) // ni if ni else 16
     secs = [  # (buffer, int32 words per element, [(lo, hi) element range per rank])
-        (_L.RT_DB_NODES, 8, [(s[4], min(s[5], ni)) for s in shares]),
-        (_L.RT_DB_NODES, 8, [(ni + s[4], ni + s[5]) for s in shares]),
+        (_L.RT_DB_NODES, 8, [(s[4], min(s[5], ni)) for s in shares]),  # internal nodes (leaves live in tri_s)
         (_L.RT_DB_TRI_S, 12, [(s[4], s[5]) for s in shares]),
-        (_L.RT_DB_WIDE, 16, [(s[4], min(s[5], ni)) for s in shares]),
+        (_L.RT_DB_WIDE, wwpe, [(s[4], min(s[5], ni)) for s in shares]),
         (_L.RT_DB_TOPO, 4, [(s[4], min(s[5], ni)) for s in shares]),
         (_L.RT_DB_PRE, 6, [(s[4], s[5]) for s in shares]),
         (_L.RT_DB_SUF, 6, [(s[4], s[5]) for s in shares]),

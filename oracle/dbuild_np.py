@@ -108,10 +108,11 @@ class NumpyStages:
         left, right, rlo, rhi, parent = O.karras(keys) if n > 1 else ([], [], [], [], np.zeros(1, np.uint32))
         esc = O.escape(n, left, right, parent) if n > 1 else np.array([0xFFFFFFFF], np.uint32)
         lmin, lmax = self.bmin[vals[k0:k1]], self.bmax[vals[k0:k1]]
-        leaves = nodes[L0 + k0:L0 + k1]  # leaf nodes and leaf-ordered triangle records
-        leaves["lo"], leaves["hi"], leaves["a"], leaves["esc"] = lmin, lmax, vals[k0:k1], esc[L0 + k0:L0 + k1]
+        # leaf-ordered triangle records {v0, v1, v2, prim, leaf escape, 0}: the
+        # device writes no leaf nodes (leaf_nodes() derives them)
         tri_s[k0:k1, :9] = self.tris[vals[k0:k1]]
         tri_s[k0:k1, 9] = vals[k0:k1].view(np.float32)
+        tri_s[k0:k1, 10] = esc[L0 + k0:L0 + k1].view(np.float32)
         cross = []
         for blk in range(b0, b1):
             B0, B1 = blk * T, min(blk * T + T, n)

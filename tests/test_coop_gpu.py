@@ -60,7 +60,7 @@ def test_coop_full_frame(R, oracle, cfg, cap, spp, lanes):
     w, h = 200, 120
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("trace.coop_cap", cap, 0)
-    cfg("trace.coop_lanes", lanes, 64)
+    cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -116,8 +116,8 @@ def test_coop_tiles(R, oracle, cfg, P, cap, lanes):
     w, h, spp = 170, 90, 2
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("render.emulate", 1, 0)
-    cfg("trace.coop_cap_tiles", cap, 96)
-    cfg("trace.coop_lanes", lanes, 64)
+    cfg("trace.coop_cap_tiles", cap, 80)
+    cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -139,7 +139,7 @@ def test_coop_frontier_handoff(R, oracle, cfg, lanes):
     w, h = 96, 64
     eh, er = _frame(oracle, tris, V, w, h, 1)
     cfg("trace.coop_cap", 1, 0)
-    cfg("trace.coop_lanes", lanes, 64)
+    cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()

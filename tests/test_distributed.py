@@ -82,7 +82,14 @@ def _dbuild_worker(rank, world, port, n, seed, q):
         st = NumpyStages(tris)
         info = D.distributed_build(st, D.Exchange())
         exp = O.build(tris)
-        got_nodes = st.arr(L.RT_DB_NODES)
+        # the device phases write internal nodes only; leaf L0 + k is derived
+        # from triangle record k {v0, v1, v2, prim, esc} (k_leaf_nodes)
+        got_nodes = st.arr(L.RT_DB_NODES).copy()
+        ts = st.arr(L.RT_DB_TRI_S)
+        lv, v = got_nodes[n - 1:], ts[:, :9].reshape(-1, 3, 3)
+        lv["lo"] = np.fmin(np.fmin(v[:, 0], v[:, 1]), v[:, 2])
+        lv["hi"] = np.fmax(np.fmax(v[:, 0], v[:, 1]), v[:, 2])
+        lv["a"], lv["esc"] = ts[:, 9].view(np.uint32), ts[:, 10].view(np.uint32)
         ok = {
             "keys": np.array_equal(st.arr(L.RT_DB_KEYS), exp["keys"]),
             "vals": np.array_equal(st.arr(L.RT_DB_VALS), exp["vals"]),

@@ -130,7 +130,7 @@ def test_wide8_coop_full_frame(R, oracle, cfg, lanes, cap):
     w, h, spp = 200, 120, 2
     eh, er = _oracle(oracle, tris, V, w, h, spp)
     cfg("trace.coop_cap", cap, 0)
-    cfg("trace.coop_lanes", lanes, 64)
+    cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -149,8 +149,8 @@ def test_wide8_tiles(R, oracle, cfg, P, lanes):
     w, h, spp = 170, 90, 2
     eh, er = _oracle(oracle, tris, V, w, h, spp)
     cfg("render.emulate", 1, 0)
-    cfg("trace.coop_cap_tiles", 6, 96)
-    cfg("trace.coop_lanes", lanes, 64)
+    cfg("trace.coop_cap_tiles", 6, 80)
+    cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -168,7 +168,7 @@ def test_wide8_coop_frontier_handoff(R, oracle, cfg, lanes):
     w, h = 96, 64
     eh, er = _oracle(oracle, tris, V, w, h, 1)
     cfg("trace.coop_cap", 1, 0)
-    cfg("trace.coop_lanes", lanes, 64)
+    cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
