@@ -775,6 +775,12 @@ __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoO
 //      block in its atomic-arrival loop) and without re-reading the
 //      topology and parent arrays K4 used to write for it;
 //   4. coalesced stores of the local internal nodes and their K7w records.
+// keys staged on each side of a refit block (its nodes' delta searches run in
+// LDS inside this window; a search that would leave it runs wave-wide in
+// global memory)
+#ifndef RT_REFIT_KEY_MARGIN
+#define RT_REFIT_KEY_MARGIN 1024
+#endif
 template <int W>
 __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restrict__ keys_g,
                                                         const uint32_t* __restrict__ svals,
@@ -786,7 +792,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         uint32_t* cross_ctr, uint32_t cross_cap,
                                                         uint4* __restrict__ wnodes, uint32_t collapse,
                                                         uint32_t block0 = 0) {
-    constexpr int T = kRefitT, NW = T / 64, KW = 1024;
+    constexpr int T = kRefitT, NW = T / 64, KW = RT_REFIT_KEY_MARGIN;
     static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
     static_assert(sizeof(uint4) <= sizeof(Aabb), "topology words must fit the table buffer");
     __shared__ Aabb s_tab[T];          // key window first (uint32), then the odd sparse-table levels
