@@ -387,6 +387,7 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
         r.sched.coop_fresh = true;
         r.sched.prev_cam_valid = false;
         r.sched.have_prev = false;
+        r.sched.order_ready = false;
         r.sched.fresh = true;
         std::memcpy(r.sched_key, key, sizeof(key));
     }

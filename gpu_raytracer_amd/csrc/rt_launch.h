@@ -144,6 +144,7 @@ struct TileSched {
     bool prev_cam_valid = false;
     bool coop_fresh = true;         // queue (re)allocated: zero both counters before the first launch
     bool have_prev = false;
+    bool order_ready = false;       // `order` for this frame already sorted by the previous frame's k_trace_coop
     bool fresh = true;              // maps (re)allocated: clear both before the first launch
 };
 // The process-wide knobs (rt_config_set).  Every launcher works on one

@@ -883,6 +883,88 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     }
 }
 
+// ---------------------------------------------------------------- tile order
+// DESIGN.md "Tile order".  A frame's time is set by its longest waves (~1 us
+// per dependent record fetch, up to ~200 fetches for rays grazing the soup):
+// dispatched in row-major order they start late and the GPU idles behind
+// them.  Each wave of k_trace records its duration into cost[slot]
+// (atomicMax over the tile's waves); the next frame of the same size
+// dispatches its tiles longest-first from that map.  The order only decides
+// which block renders which tile, never a pixel's result.
+//
+// Counting sort, costliest first, on a log-scale key: 8 buckets per octave
+// of the duration (10-ns clock ticks).  Order within a bucket is free.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t d) {
+    if (d < 8) return d;
+    const uint32_t e = 31u - (uint32_t)__clz((int)d);  // d in [2^e, 2^(e+1)), e >= 3
+    return min(255u, (e - 2) * 8 + ((d >> (e - 3)) & 7u));
+}
+
+constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per rank (4K frames)
+
+// It also clears the map it consumed: after the host's swap that buffer is
+// the one the next frame writes, so no memset is needed per frame.
+// The counting sort of one block of NTH threads, PER costs per thread (nb <=
+// NTH * PER): k_tile_order (1024 threads, its own launch) or block 0 of the
+// previous frame's k_trace_coop (256 threads, nb <= 4096: one rank's tiles),
+// whose order the next frame then finds ready (TileSched::order_ready).
+template <int NTH, int PER>
+__device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, uint32_t nb,
+                                                 uint32_t* __restrict__ order, uint32_t* s_hist, uint32_t* s_sum) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t j = tid; j < 256; j += NTH) s_hist[j] = 0u;
+    __syncthreads();
+    // each cost is read once: both passes see the same buckets, so `order`
+    // is a permutation even if the map were being rewritten meanwhile
+    uint8_t bk[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t i = tid + j * NTH;
+        bk[j] = i < nb ? (uint8_t)(255u - cost_bucket(cost[i])) : 0;
+        if (i < nb) {
+            atomicAdd(&s_hist[bk[j]], 1u);
+            cost[i] = 0u;
+        }
+    }
+    __syncthreads();
+    if (tid < 256) {  // exclusive scan of 256 buckets: 4 waves of 64
+        const uint32_t v = s_hist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_sum[wv] = x;
+    }
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
+        const uint32_t v = s_hist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        s_hist[tid] = pre + x - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t i = tid + j * NTH;
+        if (i < nb) order[atomicAdd(&s_hist[bk[j]], 1u)] = i;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_tile_order(uint32_t* __restrict__ cost, uint32_t nb,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_sum[16];
+    tile_order_block<1024, kOrderPerThread>(cost, nb, order, s_hist, s_sum);
+}
+
 // ------------------------------------------------------ cooperative heavy rays
 // DESIGN.md "Cooperative heavy rays".  A group of G lanes (16, 32 or 64:
 // trace.coop_lanes) traces one queued ray: a frame's (or one rank's
@@ -1114,17 +1196,32 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // Pass 2 of a primary frame with trace.coop_cap*: the queued heavy pixels,
 // one group of G lanes each (a persistent grid striding over the queue), from
 // the queued sample on; writes their hits and RGBA exactly as k_trace would.
-// Block 0 zeroes the next frame's queue counters.
+// Block 0 zeroes the next frame's queue counters.  With ord_out (one rank's
+// tiles, nb <= kOrderInCoop) block 0 instead sorts the cost map this frame's
+// k_trace just wrote into the next frame's tile order -- the k_tile_order
+// launch (8-11 us, all of it latency) leaves the next frame's critical path
+// -- and leaves the queue to the other blocks.
+constexpr uint32_t kOrderInCoop = 256 * 16;
 template <bool COUNT, bool PACKED, int G, int WA = 4>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
                                                     uint32_t W, uint32_t spp, CoopQ cq, float4* __restrict__ hits,
                                                     uint32_t* __restrict__ rgba,
-                                                    unsigned long long* __restrict__ counters) {
+                                                    unsigned long long* __restrict__ counters,
+                                                    uint32_t* __restrict__ ord_cost = nullptr, uint32_t ord_nb = 0,
+                                                    uint32_t* __restrict__ ord_out = nullptr) {
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
     if (blockIdx.x == 0 && threadIdx.x < kCoopShards) cq.ctr_next[threadIdx.x] = 0u;
+    static_assert(sizeof(CoopLds<G, WA>) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
+    const bool order_block = ord_out && gridDim.x > 1;  // uniform
+    if (order_block && blockIdx.x == 0) {
+        tile_order_block<256, 16>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
+                                  reinterpret_cast<uint32_t*>(&s_l[0]) + 256);
+        return;
+    }
+    const uint32_t b0 = order_block ? 1u : 0u;  // queue work over blocks [b0, gridDim.x)
     const uint32_t lane = threadIdx.x & 63, grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
     // the shards' filled lengths and their exclusive prefix, lane k = shard k
     const uint32_t len = min(cq.ctr[lane], cq.cap);
@@ -1145,7 +1242,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
     uint32_t cn = 0, ct = 0;
-    for (uint32_t e = blockIdx.x * NG + grp; e < cnt; e += gridDim.x * NG) {
+    for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
         // queued ray e lives in the last non-empty shard whose prefix is <= e
         uint32_t sh = 0, sbase = 0;
         for (uint32_t k = 0; k < 64; ++k) {
@@ -1797,78 +1894,6 @@ __global__ void k_minmax(uint32_t count, const float* __restrict__ a, const floa
 }
 
 
-// ---------------------------------------------------------------- tile order
-// DESIGN.md "Tile order".  A frame's time is set by its longest waves (~1 us
-// per dependent record fetch, up to ~200 fetches for rays grazing the soup):
-// dispatched in row-major order they start late and the GPU idles behind
-// them.  Each wave of k_trace records its duration into cost[slot]
-// (atomicMax over the tile's waves); the next frame of the same size
-// dispatches its tiles longest-first from that map.  The order only decides
-// which block renders which tile, never a pixel's result.
-//
-// Counting sort, costliest first, on a log-scale key: 8 buckets per octave
-// of the duration (10-ns clock ticks).  Order within a bucket is free.
-__device__ __forceinline__ uint32_t cost_bucket(uint32_t d) {
-    if (d < 8) return d;
-    const uint32_t e = 31u - (uint32_t)__clz((int)d);  // d in [2^e, 2^(e+1)), e >= 3
-    return min(255u, (e - 2) * 8 + ((d >> (e - 3)) & 7u));
-}
-
-constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per rank (4K frames)
-
-// It also clears the map it consumed: after the host's swap that buffer is
-// the one the next frame writes, so no memset is needed per frame.
-__global__ __launch_bounds__(1024) void k_tile_order(uint32_t* __restrict__ cost, uint32_t nb,
-                                                     uint32_t* __restrict__ order) {
-    __shared__ uint32_t s_hist[256];
-    __shared__ uint32_t s_sum[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid < 256) s_hist[tid] = 0u;
-    __syncthreads();
-    // each cost is read once: both passes see the same buckets, so `order`
-    // is a permutation even if the map were being rewritten meanwhile
-    uint8_t bk[kOrderPerThread];
-#pragma unroll
-    for (uint32_t j = 0; j < kOrderPerThread; ++j) {
-        const uint32_t i = tid + j * 1024;
-        bk[j] = i < nb ? (uint8_t)(255u - cost_bucket(cost[i])) : 0;
-        if (i < nb) {
-            atomicAdd(&s_hist[bk[j]], 1u);
-            cost[i] = 0u;
-        }
-    }
-    __syncthreads();
-    if (tid < 256) {  // exclusive scan of 256 buckets: 4 waves of 64
-        const uint32_t v = s_hist[tid];
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane == 63) s_sum[wv] = x;
-    }
-    __syncthreads();
-    if (tid < 256) {
-        uint32_t pre = 0;
-        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
-        const uint32_t v = s_hist[tid];
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        s_hist[tid] = pre + x - v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < kOrderPerThread; ++j) {
-        const uint32_t i = tid + j * 1024;
-        if (i < nb) order[atomicAdd(&s_hist[bk[j]], 1u)] = i;
-    }
-}
-
 // ================================================================ launchers
 uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) {
     const uint32_t nt = ((w + 15) / 16) * ((h + 15) / 16);
@@ -1987,9 +2012,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             sched->fresh = false;
         }
         if (sched->have_prev) {
-            hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order);
+            // computed already by the previous frame's k_trace_coop (one rank's tiles), else here
+            if (!sched->order_ready)
+                hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order);
             order = sched->order;
         }
+        sched->order_ready = false;
         cost_out = sched->cost_cur;
     }
     if (cfg.order_override) order = cfg.order_override;
@@ -2085,13 +2113,17 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             }
             cgrid = r;
         }
+        // block 0 sorts this frame's cost map into the next frame's tile order
+        const bool ord = cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
+        uint32_t* ord_cost = ord ? cost_out : nullptr;
+        uint32_t* ord_out = ord ? sched->order : nullptr;
 #define RT_COOP_G(C, P, G)                                                                                        \
     if (warity == 8)                                                                                               \
         hipLaunchKernelGGL((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters);                                                               \
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out);                                        \
     else                                                                                                           \
         hipLaunchKernelGGL((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters)
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out)
 #define RT_COOP(C, P)                  \
     if (cfg.coop_lanes == 16) {        \
         RT_COOP_G(C, P, 16);           \
@@ -2108,6 +2140,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
 #undef RT_COOP
 #undef RT_COOP_G
         sched->coop_par ^= 1u;
+        if (ord) sched->order_ready = true;
     }
     return hipGetLastError();
 }
