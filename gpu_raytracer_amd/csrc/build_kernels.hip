@@ -1131,6 +1131,15 @@ static hipError_t ensure_cross_attr() {
     return err[dev];
 }
 
+// grids of the crossing stage: a crossing node is a short chain of dependent
+// global loads, so more threads in flight beat each block's LDS segment-tree
+// setup (profiles/ab_cross_grid_r02.log: 64/64 blocks 28.3 us, 128/256 20.0 us)
+#ifndef RT_CROSS_GRID
+#define RT_CROSS_GRID 128
+#endif
+#ifndef RT_WCROSS_GRID
+#define RT_WCROSS_GRID 256
+#endif
 static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
                                 hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
@@ -1141,7 +1150,7 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
         const size_t lds = 2ull * P * sizeof(Aabb);
         const hipError_t e = ensure_cross_attr();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_refit_cross<true>, dim3(64), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
+        hipLaunchKernelGGL(k_refit_cross<true>, dim3(RT_CROSS_GRID), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
         const uint32_t L = sparse_levels(m);
@@ -1153,10 +1162,10 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     if (arity == 8)
-        hipLaunchKernelGGL(k_wide_cross<8>, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+        hipLaunchKernelGGL(k_wide_cross<8>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
                            cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     else
-        hipLaunchKernelGGL(k_wide_cross<4>, dim3(64), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+        hipLaunchKernelGGL(k_wide_cross<4>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
                            cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     return hipGetLastError();
 }
