@@ -356,7 +356,7 @@ __device__ __forceinline__ uint4 karras_finish(const KeyWin& keys, int64_t N, in
     else if (mx + 1 <= N - 2 && kdir(keys, N, mx + 1) > 0) esc = (uint32_t)(mx + 1);
     else esc = (uint32_t)(L0 + mx + 1);
     const uint4 tp = make_uint4(left, esc, (uint32_t)mn, (uint32_t)mx);
-    topo[i] = tp;
+    if (topo) topo[i] = tp;  // k_topo_refit stores the crossing nodes' words only
     if (parent) {
         parent[left] = (uint32_t)i;
         parent[right] = (uint32_t)i;
@@ -562,6 +562,17 @@ __device__ __forceinline__ Aabb load_aabb_node(const void* nodes, uint32_t i) {
 // Children of internal node X from its topology word {left, esc, lo, hi}:
 // the split g is the left child's index (internal g or leaf L0+g); the right
 // child is internal g+1, or leaf L0+g+1 when the range ends at g+1.
+// The topology word of internal node i rebuilt from its node record {box,
+// left, esc}: kids_of needs the left child and the range end mx, and the
+// escape link is §9.6's closed form of mx (SENT: mx = n-1; leaf L0+mx+1;
+// internal mx+1), so mx follows from it.  The range start is not needed.
+__device__ __forceinline__ uint4 topo_of_node(const void* nodes, uint32_t i, uint32_t L0) {
+    const float4 B = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)i * 32)[1];
+    const uint32_t left = __float_as_uint(B.z), esc = __float_as_uint(B.w);
+    const uint32_t mx = esc == RT_SENT ? L0 : esc >= L0 ? esc - L0 - 1 : esc - 1;
+    return make_uint4(left, esc, 0u, mx);
+}
+
 __device__ __forceinline__ void kids_of(const uint4& tp, uint32_t L0, uint32_t& l, uint32_t& r) {
     l = tp.x;
     const uint32_t g = l < L0 ? l : l - L0;
@@ -822,8 +833,10 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         LeafTri lt;
         if (valid) lt = gather_leaf(prim, tris);
         bool deferred = false;
-        if (valid) karras_node_leaf(keys, lt, n, k, topo, parent, nodes, tri_s, tp, box, true, deferred);
-        karras_wave_search(keys, n, k, deferred, topo, parent, tp);
+        // topology words stay in registers/LDS: only the crossing nodes' go to
+        // global memory (step 2), for k_refit_cross / k_wide_cross
+        if (valid) karras_node_leaf(keys, lt, n, k, nullptr, parent, nodes, tri_s, tp, box, true, deferred);
+        karras_wave_search(keys, n, k, deferred, nullptr, parent, tp);
     }
     s_box[tid] = box;
     RT_STAMP(2);
@@ -846,7 +859,10 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         if (need_suf) store_aabb(sufbuf, k, suf);
         if (need_pre) store_aabb(prebuf, k, pre);
         if (k == B1 - 1) store_aabb(totals, gb, pre);
-        if (has_int && (tp.z < B0 || tp.w >= B1)) cslot = atomicAdd(&s_ncross, 1u);  // LDS
+        if (has_int && (tp.z < B0 || tp.w >= B1)) {
+            cslot = atomicAdd(&s_ncross, 1u);  // LDS
+            topo[k] = tp;
+        }
     }
     __syncthreads();
     RT_STAMP(3);
@@ -1002,9 +1018,11 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         if (X >= L0) continue;
         const uint4 tx = topo[X];
         uint32_t node[W];
-        // internal boxes from `nodes`, leaf boxes from the triangle records
+        // internal boxes from `nodes`, leaf boxes from the triangle records;
+        // a descendant's children from its node record (k_topo_refit writes
+        // topology words for crossing nodes only)
         const auto box_of = [&](uint32_t i) { return i >= L0 ? leaf_box(tri_s, i - L0) : load_aabb_node(nodes, i); };
-        wide_entries<W>(tx, L0, [&](uint32_t i) { return topo[i]; }, box_of, collapse, node);
+        wide_entries<W>(tx, L0, [&](uint32_t i) { return topo_of_node(nodes, i, L0); }, box_of, collapse, node);
         const Aabb bx = load_aabb_node(nodes, X);
         store_wide<W>(wnodes, X, bx, node, [&](int i) { return box_of(node[i] == RT_SENT ? X : node[i]); }, L0);
     }
