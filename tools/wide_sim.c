@@ -333,3 +333,90 @@ void wsim_compact(const node_t* nodes, uint32_t n, const float* tris, const uint
     }
     free(q);
 }
+
+/* Top-of-stack prefetch model (design experiment): the lane keeps the record
+ * (or leaf) on top of its stack loaded, re-issuing the load whenever the top
+ * changes.  A step needs no memory wait when everything it processes came off
+ * the stack as a top established at least two steps earlier (its load was in
+ * flight for a whole step); entries reached by descent, or a second entry
+ * popped in one step, still wait.  ready[pixel] = such steps. */
+void wsim_chain(const node_t* nodes, uint32_t n, const float* tris, const uint32_t* cut, uint32_t K,
+                const cam_t* c, uint32_t w, uint32_t h, uint32_t y0, uint32_t y1, uint16_t* steps, uint16_t* ready,
+                uint32_t* hitp) {
+    const uint32_t L0 = n - 1;
+    uint32_t stk[512];
+    float stn[512];
+    for (uint32_t y = y0; y < y1; ++y)
+        for (uint32_t x = 0; x < w; ++x) {
+            const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+            float d[3], invd[3];
+            for (int a = 0; a < 3; ++a) {
+                d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
+                invd[a] = 1.0f / d[a];
+            }
+            float tb = INFINITY;
+            uint32_t hp = 0xFFFFFFFFu, sp = 0, cur = 0, pend = 0xFFFFFFFFu, ns = 0, nready = 0;
+            int top_step = -1000;            /* step whose end established the current top */
+            int cur_ok = 0, pend_ok = 0;     /* data already present for cur / pend */
+            float ctn = 0.0f;
+            for (;;) {
+                const int s = (int)ns;
+                if (pend == 0xFFFFFFFFu) {
+                    int popped = 0;
+                    if (cur == 0xFFFFFFFFu && sp) {
+                        --sp; cur = stk[sp]; ctn = stn[sp];
+                        cur_ok = (s - top_step >= 2);
+                        top_step = s - 1;
+                        popped = 1;
+                    }
+                    if (cur != 0xFFFFFFFFu && cur >= L0) {
+                        pend = cur;
+                        pend_ok = cur_ok;
+                        cur = 0xFFFFFFFFu;
+                        if (sp) {
+                            --sp; cur = stk[sp]; ctn = stn[sp];
+                            cur_ok = popped ? 0 : (s - top_step >= 2);  /* a second pop in one step waits */
+                            top_step = s - 1;
+                        }
+                    }
+                }
+                if (pend == 0xFFFFFFFFu && cur == 0xFFFFFFFFu) break;
+                ++ns;
+                int ok = 1;
+                if (pend != 0xFFFFFFFFu) {
+                    ok &= pend_ok;
+                    float tn, t, u, v;
+                    const node_t* lf = &nodes[pend];
+                    if (slab(lf, c->eye, invd, tb, &tn) &&
+                        orc_intersect_tri(c->eye, d, tris + (size_t)lf->a * 9, tb, &t, &u, &v)) {
+                        tb = t;
+                        hp = lf->a;
+                    }
+                    pend = 0xFFFFFFFFu;
+                }
+                if (cur == 0xFFFFFFFFu || cur >= L0) { nready += ok; continue; }
+                if (ctn > tb) { nready += ok; cur = 0xFFFFFFFFu; continue; }
+                ok &= cur_ok;
+                nready += ok;
+                const uint32_t* e = cut + (size_t)cur * K;
+                uint32_t hit[16], m = 0;
+                float htn[16];
+                for (uint32_t i = 0; i < K && e[i] != 0xFFFFFFFFu; ++i) {
+                    float tn;
+                    if (slab(&nodes[e[i]], c->eye, invd, tb, &tn)) { hit[m] = e[i]; htn[m] = tn; ++m; }
+                }
+                cur = 0xFFFFFFFFu;
+                if (m) {
+                    for (uint32_t i = m - 1; i >= 1; --i) { stk[sp] = hit[i]; stn[sp] = htn[i]; ++sp; }
+                    if (m > 1) top_step = s;  /* pushed at the end of this step */
+                    cur = hit[0];
+                    ctn = htn[0];
+                    cur_ok = 0;              /* reached by descent: fetched next step */
+                }
+            }
+            const size_t p = (size_t)y * w + x;
+            steps[p] = (uint16_t)(ns > 65535 ? 65535 : ns);
+            ready[p] = (uint16_t)(nready > 65535 ? 65535 : nready);
+            hitp[p] = hp;
+        }
+}

@@ -141,7 +141,48 @@ def compact(n=1_000_000, policies=((0, 0), (16, 8), (24, 8), (32, 8), (24, 16), 
               f"VALU model {o[5]:,.0f}", flush=True)
 
 
+def chain(n=1_000_000, K=4):
+    """Top-of-stack prefetch model (wsim_chain): steps whose data would already be there."""
+    so = "/tmp/libwsim.so"
+    O.lib()
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+                    "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
+                    "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
+    L = C.CDLL(so)
+    tris = O.soup(n, 1)
+    nodes = O.build(tris)["nodes"]
+    v = S.VIEWS["soup"]
+    W, H = 1920, 1080
+    cam = O.camera_look_at(v.eye, v.at, v.up, v.vfov, W, H)
+    ref, _ = O.trace(nodes, tris, cam, W, H)
+    P = C.c_void_p
+    cut = np.empty((n - 1) * K, np.uint32)
+    L.wsim_cut(nodes.ctypes.data_as(P), n, K, cut.ctypes.data_as(P))
+    steps = np.zeros(W * H, np.uint16)
+    ready = np.zeros(W * H, np.uint16)
+    hitp = np.zeros(W * H, np.uint32)
+
+    def band(y0):
+        L.wsim_chain(nodes.ctypes.data_as(P), n, tris.ctypes.data_as(P), cut.ctypes.data_as(P), K, C.byref(cam),
+                     W, H, y0, min(H, y0 + 36), steps.ctypes.data_as(P), ready.ctypes.data_as(P),
+                     hitp.ctypes.data_as(P))
+
+    with ThreadPoolExecutor(8) as ex:
+        list(ex.map(band, range(0, H, 36)))
+    assert np.array_equal(hitp, ref["prim"]), "model disagrees with the oracle"
+    s, r = steps.astype(np.int64), ready.astype(np.int64)
+    print(f"K={K}: steps {s.sum():,} ready {r.sum():,} ({r.sum() / s.sum():.3f})", flush=True)
+    for lo in (32, 64, 96, 128, 192):
+        m = s >= lo
+        if m.any():
+            print(f"  rays >= {lo} steps: {int(m.sum())}, ready fraction {r[m].sum() / s[m].sum():.3f}, "
+                  f"max steps {s[m].max()}, waits of the costliest {int(s[m].max() - r[m][s[m].argmax()])}", flush=True)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "chain":
+        chain()
+        sys.exit(0)
     if len(sys.argv) > 1 and sys.argv[1] == "compact":
         compact()
         sys.exit(0)
