@@ -246,7 +246,9 @@ rt_status rt_scene_sync(rt_scene* s);
  *      the rank's refit blocks (rt_dbuild_shares) and its crossing-node list
  *      (RT_DB_CROSS) -> all-gather every section's share (nodes, tri_s, wide
  *      records, topology, block prefix/suffix boxes, block totals) and the
- *      crossing lists into RT_DB_CROSS_ALL;
+ *      crossing lists into RT_DB_CROSS_ALL.  RT_DB_TOPO holds {left, esc,
+ *      range lo, range hi} for the crossing nodes only (the merge reads no
+ *      other entry; their contents are unspecified);
  *   5. rt_dbuild_merge: boxes and wide records of every crossing node; the
  *      scene is then built (rt_render, rt_bvh_read ...). */
 enum {
