@@ -92,6 +92,16 @@ hipError_t launch_leaf_nodes(const float4* tri_s, uint32_t n, void* nodes, hipSt
 
 struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 
+// trace.coop_cap_tiles = -1 (the default): the step cap one rank's tiles use,
+// by rank count.  A rank of a two-way split holds twice the tiles of P = 4
+// and is partly throughput-bound, so it gains from queueing fewer rays:
+// P=2 0.213 -> 0.206 ms at 88 against 80, while P=4/8 are best at 80.
+constexpr uint32_t kCoopCapAuto = 0xFFFFFFFFu;
+inline uint32_t coop_cap_for_tiles(uint32_t knob, uint32_t nranks) {
+    if (knob != kCoopCapAuto) return knob;
+    return nranks <= 2 ? 88u : 80u;
+}
+
 // Trace kernel selection / tuning (rt_config_set); every setting gives
 // bit-identical hits and images.
 struct TraceConfig {
@@ -119,8 +129,9 @@ struct TraceConfig {
     uint32_t buf_loads = 1;       // wide step loads through buffer descriptors (one round trip per step)
     uint32_t coop_cap = 0;        // primary full frames: rays past this many wide steps finish in k_trace_coop
                                   // (one wave per ray); 0 = off
-    uint32_t coop_cap_tiles = 80; // the same for one rank's tiles of a multi-GPU frame (tools/coop_sweep.py,
-                                  // profiles/coop_sweep_r02b.log)
+    uint32_t coop_cap_tiles = kCoopCapAuto;  // the same for one rank's tiles of a multi-GPU frame;
+                                  // auto (default): coop_cap_for_tiles (tools/coop_sweep.py,
+                                  // profiles/coop_sweep_r02b.log, profiles/coop_sweep_hi_r02.log)
     uint32_t coop_lanes = 32;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
     uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order

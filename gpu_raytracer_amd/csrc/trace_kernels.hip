@@ -2048,7 +2048,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     }
     // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
     const uint32_t coop_cap = wide && sched && sched->coop_q && n <= kBufMaxN
-                                  ? (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) : 0u;
+                                  ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : cfg.coop_cap) : 0u;
     CoopQ cq;
     if (coop_cap) {
         if (sched->coop_fresh) {

@@ -116,7 +116,7 @@ def test_coop_tiles(R, oracle, cfg, P, cap, lanes):
     w, h, spp = 170, 90, 2
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("render.emulate", 1, 0)
-    cfg("trace.coop_cap_tiles", cap, 80)
+    cfg("trace.coop_cap_tiles", cap, -1)
     cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:

@@ -149,7 +149,7 @@ def test_wide8_tiles(R, oracle, cfg, P, lanes):
     w, h, spp = 170, 90, 2
     eh, er = _oracle(oracle, tris, V, w, h, spp)
     cfg("render.emulate", 1, 0)
-    cfg("trace.coop_cap_tiles", 6, 80)
+    cfg("trace.coop_cap_tiles", 6, -1)
     cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
