@@ -319,6 +319,23 @@ __device__ __forceinline__ void wave_prefix(uint32_t (*s_wc)[kMsbBuckets], uint3
     }
 }
 
+// The same with 16-B LDS accesses (4 digits per thread and wave row);
+// s_wc rows and s_cnt 16-B aligned.
+template <int NW, int NT>
+__device__ __forceinline__ void wave_prefix4(uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt) {
+    for (uint32_t q = threadIdx.x; q < kMsbBuckets / 4; q += NT) {
+        uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+            uint4* row = reinterpret_cast<uint4*>(s_wc[w]);
+            const uint4 c = row[q];
+            row[q] = acc;
+            acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
+        }
+        reinterpret_cast<uint4*>(s_cnt)[q] = acc;
+    }
+}
+
 // In-place exclusive scan of a[1024] in LDS by NT threads (a written before a
 // barrier); ends with a barrier.
 template <int NT>
@@ -456,13 +473,16 @@ __global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __
 __device__ __forceinline__ void bucket_rank(const uint32_t (&k)[kSortItems], const bool (&ok)[kSortItems],
                                             uint32_t shift, uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt,
                                             uint32_t (&dg)[kSortItems], uint32_t (&r)[kSortItems]) {
-    for (uint32_t j = threadIdx.x; j < kBucketWaves * kMsbBuckets; j += kBucketThreads) (&s_wc[0][0])[j] = 0u;
+    {  // 16-B stores: 4 per thread instead of 16
+        uint4* z = reinterpret_cast<uint4*>(&s_wc[0][0]);
+        for (uint32_t j = threadIdx.x; j < kBucketWaves * kMsbBuckets / 4; j += kBucketThreads) z[j] = make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < kSortItems; ++i) dg[i] = (k[i] >> shift) & (kMsbBuckets - 1);
     rank10(dg, ok, s_wc, r);
     __syncthreads();
-    wave_prefix<kBucketWaves, kBucketThreads>(s_wc, s_cnt);
+    wave_prefix4<kBucketWaves, kBucketThreads>(s_wc, s_cnt);
     __syncthreads();
     const uint32_t w = threadIdx.x >> 6;
 #pragma unroll
@@ -475,8 +495,9 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
                                                                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                                 const uint32_t* __restrict__ bstart) {
     static_assert(kBucketWaves * kMsbBuckets == 2 * kBucketCap, "counters and sorted chunk share one buffer");
-    __shared__ uint32_t s_wc[kBucketWaves][kMsbBuckets];  // ranking counters; fast path: then the sorted chunk
-    __shared__ uint32_t s_cnt[kMsbBuckets], s_run[kMsbBuckets];
+    __shared__ __attribute__((aligned(16))) uint32_t s_wc[kBucketWaves][kMsbBuckets];  // ranking counters; fast path: then the sorted chunk
+    __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kMsbBuckets];
+    __shared__ uint32_t s_run[kMsbBuckets];
     __shared__ uint32_t s_sw[kBucketWaves];
     const uint32_t s = bstart[blockIdx.x], m = bstart[blockIdx.x + 1] - s;
     if (m == 0) return;
@@ -486,15 +507,22 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
     if (m <= kBucketCap) {
         uint32_t* s_key = &s_wc[0][0];
         uint32_t* s_val = s_key + kBucketCap;
+        // per items per lane (<= kSortItems): wave w holds [64 per w, 64 per (w+1)),
+        // so all four waves rank a partly filled bucket (index order is
+        // wave-major, then item, then lane, as the ranking counts it)
+        const uint32_t per = (m + kBucketThreads - 1) / kBucketThreads;
+        RT_STAMP(0);
 #pragma unroll
         for (int i = 0; i < kSortItems; ++i) {
-            const uint32_t j = w * (64u * kSortItems) + i * 64u + l;
-            ok[i] = j < m;
+            const uint32_t j = w * (64u * per) + i * 64u + l;
+            ok[i] = (uint32_t)i < per && j < m;
             k[i] = ok[i] ? kin[s + j] : 0u;
             v[i] = ok[i] ? vin[s + j] : 0u;
         }
         for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+            RT_STAMP(1 + shift / 5);  // 1, 3: before the ranking
             bucket_rank(k, ok, shift, s_wc, s_cnt, dg, r);
+            RT_STAMP(2 + shift / 5);  // 2, 4: ranked
             scan1024<kBucketThreads>(s_cnt, s_sw);  // its barriers also end every counter read
 #pragma unroll
             for (int i = 0; i < kSortItems; ++i)
@@ -506,7 +534,7 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < kSortItems; ++i) {
-                const uint32_t j = w * (64u * kSortItems) + i * 64u + l;
+                const uint32_t j = w * (64u * per) + i * 64u + l;
                 if (ok[i]) {
                     k[i] = s_key[j];
                     v[i] = s_val[j];
@@ -514,14 +542,16 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
             }
             __syncthreads();
         }
+        RT_STAMP(5);
 #pragma unroll
         for (int i = 0; i < kSortItems; ++i) {
-            const uint32_t j = w * (64u * kSortItems) + i * 64u + l;
+            const uint32_t j = w * (64u * per) + i * 64u + l;
             if (ok[i]) {
                 kout[s + j] = k[i];
                 vout[s + j] = v[i];
             }
         }
+        RT_STAMP(6);
         return;
     }
     // A bucket beyond one LDS sort (clustered or degenerate scenes): the same
