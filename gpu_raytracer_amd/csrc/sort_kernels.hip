@@ -414,15 +414,16 @@ __global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __
                                                               uint32_t n, const uint32_t* __restrict__ offs) {
     constexpr int W = kSortThreads / 64;
     static_assert(W * kMsbBuckets == 2 * kSortTile, "counters and bucketed tile share one buffer");
-    __shared__ uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
-    __shared__ uint32_t s_start[kMsbBuckets], s_gofs[kMsbBuckets];
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
+    __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
+    __shared__ uint32_t s_gofs[kMsbBuckets];
     __shared__ uint32_t s_sw[W];
     uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_buf);
     uint32_t* s_key = s_buf;
     uint32_t* s_val = s_buf + kSortTile;
     const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x, base = tile * (uint32_t)kSortTile;
-    for (uint32_t j = tid; j < 2 * kSortTile; j += kSortThreads) s_buf[j] = 0u;
+    for (uint32_t j = tid; j < 2 * kSortTile / 4; j += kSortThreads) reinterpret_cast<uint4*>(s_buf)[j] = make_uint4(0, 0, 0, 0);
     for (uint32_t j = tid; j < kMsbBuckets; j += kSortThreads) s_gofs[j] = offs[(uint64_t)tile * kMsbBuckets + j];
     uint32_t k[kSortItems], v[kSortItems], dg[kSortItems], r[kSortItems];
     bool ok[kSortItems];
@@ -437,7 +438,7 @@ __global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __
     __syncthreads();
     rank10(dg, ok, s_wc, r);
     __syncthreads();
-    wave_prefix<W, kSortThreads>(s_wc, s_start);
+    wave_prefix4<W, kSortThreads>(s_wc, s_start);
     __syncthreads();
     scan1024<kSortThreads>(s_start, s_sw);
     uint32_t pos[kSortItems];
@@ -466,8 +467,8 @@ __global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __
     }
 }
 
-// Ranks one chunk (<= kBucketCap items in registers, item j = w*512 + i*64 +
-// lane) by the 10-bit digit at `shift`: r[i] = the item's position among its
+// Ranks one chunk (<= kBucketCap items in registers, item j = w*64*per +
+// i*64 + lane, wave-major) by the 10-bit digit at `shift`: r[i] = the item's position among its
 // digit's items of the chunk (earlier waves first, then item order); s_cnt =
 // the chunk's digit counts.  Callers barrier before reusing s_wc.
 __device__ __forceinline__ void bucket_rank(const uint32_t (&k)[kSortItems], const bool (&ok)[kSortItems],
