@@ -145,6 +145,7 @@ struct TileSched {
     uint32_t* order = nullptr;      // [nb] dispatch index -> tile slot
     uint32_t* cost_prev = nullptr;  // [nb] previous frame's per-tile wave time
     uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
+    uint32_t* cost_ema = nullptr;   // [nb] running mean of the frames' tile costs: the order's key
     uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
     uint16_t* px_cur = nullptr;     // [nb][256] this frame's
     uint4* coop_q = nullptr;        // [coop_qcap] x kCoopEntryBytes heavy-ray queue (trace.coop_cap)

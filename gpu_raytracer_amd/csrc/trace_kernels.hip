@@ -908,9 +908,15 @@ constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per
 // NTH * PER): k_tile_order (1024 threads, its own launch) or block 0 of the
 // previous frame's k_trace_coop (256 threads, nb <= 4096: one rank's tiles),
 // whose order the next frame then finds ready (TileSched::order_ready).
+// The sort key is not the last frame's cost but a running mean m = (m + c)/2
+// over the frames of this shape (`ema`, kept beside the maps): a tile's cost
+// is its slowest wave, set by one costly ray that a small camera move makes
+// or breaks, and the mean ranks the tiles that keep holding such rays (the
+// bench's orbit: 0.363 -> 0.353 ms, profiles/ab_order_ema_r02.log).
 template <int NTH, int PER>
 __device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, uint32_t nb,
-                                                 uint32_t* __restrict__ order, uint32_t* s_hist, uint32_t* s_sum) {
+                                                 uint32_t* __restrict__ order, uint32_t* s_hist, uint32_t* s_sum,
+                                                 uint32_t* __restrict__ ema) {
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     for (uint32_t j = tid; j < 256; j += NTH) s_hist[j] = 0u;
     __syncthreads();
@@ -920,8 +926,14 @@ __device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, ui
 #pragma unroll
     for (uint32_t j = 0; j < PER; ++j) {
         const uint32_t i = tid + j * NTH;
-        bk[j] = i < nb ? (uint8_t)(255u - cost_bucket(cost[i])) : 0;
+        bk[j] = 0;
         if (i < nb) {
+            uint32_t c = cost[i];
+            if (ema) {  // the key: a running mean over this shape's frames (m = (m + c) / 2)
+                c = (uint32_t)(((uint64_t)ema[i] + c) >> 1);
+                ema[i] = c;
+            }
+            bk[j] = (uint8_t)(255u - cost_bucket(c));
             atomicAdd(&s_hist[bk[j]], 1u);
             cost[i] = 0u;
         }
@@ -959,10 +971,10 @@ __device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, ui
 }
 
 __global__ __launch_bounds__(1024) void k_tile_order(uint32_t* __restrict__ cost, uint32_t nb,
-                                                     uint32_t* __restrict__ order) {
+                                                     uint32_t* __restrict__ order, uint32_t* __restrict__ ema) {
     __shared__ uint32_t s_hist[256];
     __shared__ uint32_t s_sum[16];
-    tile_order_block<1024, kOrderPerThread>(cost, nb, order, s_hist, s_sum);
+    tile_order_block<1024, kOrderPerThread>(cost, nb, order, s_hist, s_sum, ema);
 }
 
 // ------------------------------------------------------ cooperative heavy rays
@@ -1209,7 +1221,8 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                                                     uint32_t* __restrict__ rgba,
                                                     unsigned long long* __restrict__ counters,
                                                     uint32_t* __restrict__ ord_cost = nullptr, uint32_t ord_nb = 0,
-                                                    uint32_t* __restrict__ ord_out = nullptr) {
+                                                    uint32_t* __restrict__ ord_out = nullptr,
+                                                    uint32_t* __restrict__ ord_ema = nullptr) {
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
@@ -1218,7 +1231,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     const bool order_block = ord_out && gridDim.x > 1;  // uniform
     if (order_block && blockIdx.x == 0) {
         tile_order_block<256, 16>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
-                                  reinterpret_cast<uint32_t*>(&s_l[0]) + 256);
+                                  reinterpret_cast<uint32_t*>(&s_l[0]) + 256, ord_ema);
         return;
     }
     const uint32_t b0 = order_block ? 1u : 0u;  // queue work over blocks [b0, gridDim.x)
@@ -2008,13 +2021,15 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
             hipError_t me = hipMemsetAsync(sched->cost_prev, 0, (size_t)nb * 4, s);
             if (me == hipSuccess) me = hipMemsetAsync(sched->cost_cur, 0, (size_t)nb * 4, s);
+            if (me == hipSuccess) me = hipMemsetAsync(sched->cost_ema, 0, (size_t)nb * 4, s);
             if (me != hipSuccess) return me;
             sched->fresh = false;
         }
         if (sched->have_prev) {
             // computed already by the previous frame's k_trace_coop (one rank's tiles), else here
             if (!sched->order_ready)
-                hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order);
+                hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order,
+                                   sched->cost_ema);
             order = sched->order;
         }
         sched->order_ready = false;
@@ -2117,13 +2132,14 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         const bool ord = cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
         uint32_t* ord_cost = ord ? cost_out : nullptr;
         uint32_t* ord_out = ord ? sched->order : nullptr;
+        uint32_t* ord_ema = ord ? sched->cost_ema : nullptr;
 #define RT_COOP_G(C, P, G)                                                                                        \
     if (warity == 8)                                                                                               \
         hipLaunchKernelGGL((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters, ord_cost, nb, ord_out);                                        \
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema);                               \
     else                                                                                                           \
         hipLaunchKernelGGL((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters, ord_cost, nb, ord_out)
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema)
 #define RT_COOP(C, P)                  \
     if (cfg.coop_lanes == 16) {        \
         RT_COOP_G(C, P, 16);           \

@@ -49,7 +49,10 @@ def _oracle(oracle, tris, view, w, h, spp):
 
 
 def _same(hits, rgba, eh, er):
-    assert np.array_equal(hits["prim"], eh["prim"])
+    d = np.nonzero(hits["prim"] != eh["prim"])[0]
+    assert len(d) == 0, (f"{len(d)} of {len(eh)} prims differ; first {d[:8].tolist()}: got "
+                         f"{hits['prim'][d[:8]].tolist()} t {hits['t'][d[:8]].tolist()}, expected "
+                         f"{eh['prim'][d[:8]].tolist()} t {eh['t'][d[:8]].tolist()}")
     for f in ("t", "u", "v"):
         assert np.array_equal(bits(hits[f]), bits(eh[f])), f
     assert np.array_equal(rgba, er)

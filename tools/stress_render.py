@@ -1,0 +1,57 @@
+"""Randomised render stress against the oracle: scenes of random size, arity,
+traversal variant, stack cap and frame shape, rendered fresh and on
+successive frames; any hit that differs from the oracle is reported.
+usage: python tools/stress_render.py [iterations] [seed]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import gpu_raytracer_amd as R  # noqa: E402
+from gpu_raytracer_amd import scenes as S  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+iters = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+rng = np.random.default_rng(int(sys.argv[2]) if len(sys.argv) > 2 else 0)
+presets = [(S.cornell_tris(), S.CORNELL_VIEW), (S.bunny_substitute_tris(), S.BUNNY_VIEW)]
+V = S.SOUP_VIEW
+bad = 0
+t0 = time.time()
+for it in range(iters):
+    kind = rng.integers(0, 3)
+    if kind < 2:
+        tris, view = presets[kind]
+        tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
+    else:
+        n = int(rng.integers(2, 40000))
+        tris = O.soup(n, int(rng.integers(1, 1000))).reshape(-1, 9)
+        view = V
+    ar = int(rng.choice([4, 8]))
+    var = int(rng.choice([0, 0, 0, 1, 2]))
+    cap = int(rng.choice([0, 0, 1, 3, 14]))
+    w, h = int(rng.integers(8, 200)), int(rng.integers(8, 120))
+    spp = int(rng.integers(1, 3))
+    R.config_set("build.wide_arity", ar)
+    R.config_set("trace.variant", var)
+    R.config_set("trace.stack_cap", cap)
+    b = O.build(tris)
+    ocam = O.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    eh, _ = O.trace(b["nodes"], tris, ocam, w, h, spp)
+    cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for f in range(2):  # fresh, then with the previous frame's orders
+            hits, rgba, _ = s.render(cam, w, h, spp)
+            d = np.nonzero(hits["prim"] != eh["prim"])[0]
+            if len(d):
+                bad += 1
+                print(f"MISMATCH it {it} frame {f}: n {len(tris)} arity {ar} variant {var} cap {cap} {w}x{h}x{spp}: "
+                      f"{len(d)} px, first {d[:5].tolist()} got {hits['prim'][d[:5]].tolist()} "
+                      f"exp {eh['prim'][d[:5]].tolist()}", flush=True)
+    if it % 20 == 0:
+        print(f"it {it} ({time.time() - t0:.0f} s)", flush=True)
+for k, v in (("build.wide_arity", 4), ("trace.variant", 0), ("trace.stack_cap", 0)):
+    R.config_set(k, v)
+print(f"done: {iters} scenes x 2 frames, {bad} mismatching renders", flush=True)
