@@ -31,7 +31,7 @@ Launch: `python bench.py --gpus N` spawns N rank processes itself (one per
 GPU, before any of them touches the GPU); under torch.distributed.run the
 ranks come from the environment.
 
-roofline: the trace launch (k_tile_order + k_trace) -- the bytes the kernel
+roofline: the trace launch (k_trace; its last block sorts the next frame's tile order) -- the bytes the kernel
   requests (64 B per K7w record + 48 B per triangle record fetched, its own
   deterministic counters, + 16 B hit + 4 B RGBA written per ray) over its
   event-timed duration, against the 8.0 TB/s HBM peak (frac) and the
@@ -558,7 +558,7 @@ def main():
                                      "total_with_stage_events": round(stage_total_ms, 4)},
             "trace_counters_rank0_static": {"nodes_fetched": int(cnt_static[0]), "tris_tested": int(cnt_static[1]),
                                             "rays": rank_rays},
-            "roofline": {"bound": "hbm", "kernel": "trace launch: k_tile_order + k_trace<wide>",
+            "roofline": {"bound": "hbm", "kernel": "trace launch: k_trace<wide> (+ k_tile_order when not folded)",
                          "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(frac, 4), "traffic": traffic,
                          "bytes_per_launch": kernel_bytes,

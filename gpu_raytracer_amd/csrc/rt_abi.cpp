@@ -362,12 +362,12 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
     const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     const uint32_t key[5] = {w, h, spp, rank, nranks};
     const bool same = std::memcmp(key, r.sched_key, sizeof(key)) == 0;
-    // [order][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per tile slot,
+    // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per tile slot,
     // then (trace.coop_cap) 2 queue counters and the heavy-ray queue
     const rt::TraceConfig cfg = rt::config_snapshot();
     // (64 shards of equal size, 2 x 64 counters)
     const uint32_t qcap = (cfg.coop_cap || cfg.coop_cap_tiles) ? (cfg.coop_max + 63u) & ~63u : 0u;
-    const size_t maps = 4ull * nb * 4 + 2ull * nb * 512;
+    const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
     const size_t qoff = (maps + 255) & ~size_t(255);
     const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
     if (!same || r.order_cap < need || r.sched.coop_qcap != qcap) {
@@ -375,10 +375,11 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
         RTR(grow(&r.d_order, &r.order_cap, need));
         uint32_t* b = static_cast<uint32_t*>(r.d_order);
         r.sched.order = b;
-        r.sched.cost_prev = b + nb;
-        r.sched.cost_cur = b + 2 * nb;
-        r.sched.cost_ema = b + 3 * nb;
-        r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 4 * nb);
+        r.sched.order_next = b + nb;
+        r.sched.cost_prev = b + 2 * nb;
+        r.sched.cost_cur = b + 3 * nb;
+        r.sched.cost_ema = b + 4 * nb;
+        r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 5 * nb);
         r.sched.px_cur = r.sched.px_prev + (size_t)nb * 256;
         char* qb = static_cast<char*>(r.d_order) + qoff;
         r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(qb) : nullptr;

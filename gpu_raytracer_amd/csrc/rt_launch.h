@@ -143,6 +143,7 @@ constexpr uint32_t kWide8MaxN = 1u << 26;  // 8-ary records need 32-bit buffer o
 // Per-launch tile scheduling state (owned by the scene, one per frame shape).
 struct TileSched {
     uint32_t* order = nullptr;      // [nb] dispatch index -> tile slot
+    uint32_t* order_next = nullptr; // [nb] the next frame's, sorted by this frame's k_trace (full frames)
     uint32_t* cost_prev = nullptr;  // [nb] previous frame's per-tile wave time
     uint32_t* cost_cur = nullptr;   // [nb] this frame's, written by k_trace
     uint32_t* cost_ema = nullptr;   // [nb] running mean of the frames' tile costs: the order's key

@@ -714,6 +714,110 @@ __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t
     return 0;
 }
 
+// ---------------------------------------------------------------- tile order
+// DESIGN.md "Tile order".  A frame's time is set by its longest waves (~1 us
+// per dependent record fetch, up to ~200 fetches for rays grazing the soup):
+// dispatched in row-major order they start late and the GPU idles behind
+// them.  Each wave of k_trace records its duration into cost[slot]
+// (atomicMax over the tile's waves); the next frame of the same size
+// dispatches its tiles longest-first from that map.  The order only decides
+// which block renders which tile, never a pixel's result.
+//
+// Counting sort, costliest first, on a log-scale key: 8 buckets per octave
+// of the duration (10-ns clock ticks).  Order within a bucket is free.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t d) {
+    if (d < 8) return d;
+    const uint32_t e = 31u - (uint32_t)__clz((int)d);  // d in [2^e, 2^(e+1)), e >= 3
+    return min(255u, (e - 2) * 8 + ((d >> (e - 3)) & 7u));
+}
+
+constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per rank (4K frames)
+
+// It also clears the map it consumed: after the host's swap that buffer is
+// the one the next frame writes, so no memset is needed per frame.
+// The counting sort of one block of NTH threads, PER costs per thread (nb <=
+// NTH * PER): k_tile_order (1024 threads, its own launch) or block 0 of the
+// previous frame's k_trace_coop (256 threads, nb <= 4096: one rank's tiles),
+// whose order the next frame then finds ready (TileSched::order_ready).
+// The sort key is not the last frame's cost but a running mean m = (m + c)/2
+// over the frames of this shape (`ema`, kept beside the maps): a tile's cost
+// is its slowest wave, set by one costly ray that a small camera move makes
+// or breaks, and the mean ranks the tiles that keep holding such rays (the
+// bench's orbit: 0.363 -> 0.353 ms, profiles/ab_order_ema_r02.log).
+template <int NTH, int PER>
+__device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, uint32_t nb,
+                                                 uint32_t* __restrict__ order, uint32_t* s_hist, uint32_t* s_sum,
+                                                 uint32_t* __restrict__ ema) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t j = tid; j < 256; j += NTH) s_hist[j] = 0u;
+    __syncthreads();
+    // each cost is read once: both passes see the same buckets, so `order`
+    // is a permutation even if the map were being rewritten meanwhile
+    uint8_t bk[PER];
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t i = tid + j * NTH;
+        bk[j] = 0;
+        if (i < nb) {
+            uint32_t c = cost[i];
+            if (ema) {  // the key: a running mean over this shape's frames (m = (m + c) / 2)
+                c = (uint32_t)(((uint64_t)ema[i] + c) >> 1);
+                ema[i] = c;
+            }
+            bk[j] = (uint8_t)(255u - cost_bucket(c));
+            atomicAdd(&s_hist[bk[j]], 1u);
+            cost[i] = 0u;
+        }
+    }
+    __syncthreads();
+    if (tid < 256) {  // exclusive scan of 256 buckets: 4 waves of 64
+        const uint32_t v = s_hist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        if (lane == 63) s_sum[wv] = x;
+    }
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
+        const uint32_t v = s_hist[tid];
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        s_hist[tid] = pre + x - v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t j = 0; j < PER; ++j) {
+        const uint32_t i = tid + j * NTH;
+        if (i < nb) order[atomicAdd(&s_hist[bk[j]], 1u)] = i;
+    }
+}
+
+// Full frames: the next frame's tile order sorted by one extra block of
+// this frame's k_trace (the grid's last block, dispatched when the frame's
+// tail is already running) from the previous frame's costs folded into the
+// running mean, instead of a k_tile_order launch at the head of the next
+// frame.  The order is then one frame older, which the running mean makes
+// cheap.
+struct OrderFold {
+    uint32_t* cost = nullptr;  // the previous frame's cost map (read and cleared)
+    uint32_t* out = nullptr;   // the next frame's order
+    uint32_t* ema = nullptr;   // the running mean
+    uint32_t nb = 0;
+};
+constexpr uint32_t kFoldPerThread = 32;  // 256 threads: up to 8192 tiles (a 1080p frame has 8160)
+#ifndef RT_ORDER_FOLD
+#define RT_ORDER_FOLD 1  // 0: k_tile_order at the head of every frame (A/B)
+#endif
+
 template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4>
 __global__ __launch_bounds__(NT, (SHADOW && WA == 4) ? RT_KSHADOW_WAVES : (PACKED && WA == 4) ? RT_KTILES_WAVES : RT_KTRACE_WAVES)
 void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
@@ -727,9 +831,17 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t* __restrict__ cost_out = nullptr,
                                                const uint16_t* __restrict__ px_prev = nullptr,
                                                uint16_t* __restrict__ px_cost = nullptr,
-                                               uint32_t coop_cap = 0, CoopQ cq = CoopQ{}) {
+                                               uint32_t coop_cap = 0, CoopQ cq = CoopQ{},
+                                               OrderFold fold = OrderFold{}) {
     __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
     __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
+    if constexpr (!PACKED && !SHADOW && !COUNT && NT == 256 && (WIDE || SHADOW)) {
+        if (fold.out && blockIdx.x == gridDim.x - 1) {  // uniform: the extra block sorts and leaves
+            static_assert((WideFmt<WA>::stack + 1) * NT >= 256 + 16, "tile_order_block's LDS");
+            tile_order_block<256, kFoldPerThread>(fold.cost, fold.nb, fold.out, s_ref, s_ref + 256, fold.ema);
+            return;
+        }
+    }
     // tile slot from the block id: consecutive tiles go to different XCDs
     // under the round-robin dispatch, which balances the image's cheap and
     // costly bands over the 8 XCDs (an XCD-banded remap measured 1.2x
@@ -880,93 +992,6 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
         atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
-    }
-}
-
-// ---------------------------------------------------------------- tile order
-// DESIGN.md "Tile order".  A frame's time is set by its longest waves (~1 us
-// per dependent record fetch, up to ~200 fetches for rays grazing the soup):
-// dispatched in row-major order they start late and the GPU idles behind
-// them.  Each wave of k_trace records its duration into cost[slot]
-// (atomicMax over the tile's waves); the next frame of the same size
-// dispatches its tiles longest-first from that map.  The order only decides
-// which block renders which tile, never a pixel's result.
-//
-// Counting sort, costliest first, on a log-scale key: 8 buckets per octave
-// of the duration (10-ns clock ticks).  Order within a bucket is free.
-__device__ __forceinline__ uint32_t cost_bucket(uint32_t d) {
-    if (d < 8) return d;
-    const uint32_t e = 31u - (uint32_t)__clz((int)d);  // d in [2^e, 2^(e+1)), e >= 3
-    return min(255u, (e - 2) * 8 + ((d >> (e - 3)) & 7u));
-}
-
-constexpr uint32_t kOrderPerThread = 32;  // k_tile_order: up to 32768 tiles per rank (4K frames)
-
-// It also clears the map it consumed: after the host's swap that buffer is
-// the one the next frame writes, so no memset is needed per frame.
-// The counting sort of one block of NTH threads, PER costs per thread (nb <=
-// NTH * PER): k_tile_order (1024 threads, its own launch) or block 0 of the
-// previous frame's k_trace_coop (256 threads, nb <= 4096: one rank's tiles),
-// whose order the next frame then finds ready (TileSched::order_ready).
-// The sort key is not the last frame's cost but a running mean m = (m + c)/2
-// over the frames of this shape (`ema`, kept beside the maps): a tile's cost
-// is its slowest wave, set by one costly ray that a small camera move makes
-// or breaks, and the mean ranks the tiles that keep holding such rays (the
-// bench's orbit: 0.363 -> 0.353 ms, profiles/ab_order_ema_r02.log).
-template <int NTH, int PER>
-__device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, uint32_t nb,
-                                                 uint32_t* __restrict__ order, uint32_t* s_hist, uint32_t* s_sum,
-                                                 uint32_t* __restrict__ ema) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    for (uint32_t j = tid; j < 256; j += NTH) s_hist[j] = 0u;
-    __syncthreads();
-    // each cost is read once: both passes see the same buckets, so `order`
-    // is a permutation even if the map were being rewritten meanwhile
-    uint8_t bk[PER];
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t i = tid + j * NTH;
-        bk[j] = 0;
-        if (i < nb) {
-            uint32_t c = cost[i];
-            if (ema) {  // the key: a running mean over this shape's frames (m = (m + c) / 2)
-                c = (uint32_t)(((uint64_t)ema[i] + c) >> 1);
-                ema[i] = c;
-            }
-            bk[j] = (uint8_t)(255u - cost_bucket(c));
-            atomicAdd(&s_hist[bk[j]], 1u);
-            cost[i] = 0u;
-        }
-    }
-    __syncthreads();
-    if (tid < 256) {  // exclusive scan of 256 buckets: 4 waves of 64
-        const uint32_t v = s_hist[tid];
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        if (lane == 63) s_sum[wv] = x;
-    }
-    __syncthreads();
-    if (tid < 256) {
-        uint32_t pre = 0;
-        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
-        const uint32_t v = s_hist[tid];
-        uint32_t x = v;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= (uint32_t)o) x += y;
-        }
-        s_hist[tid] = pre + x - v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t j = 0; j < PER; ++j) {
-        const uint32_t i = tid + j * NTH;
-        if (i < nb) order[atomicAdd(&s_hist[bk[j]], 1u)] = i;
     }
 }
 
@@ -2017,6 +2042,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // costliest tiles first from the previous frame's map (DESIGN.md "Tile order")
     const uint32_t* order = nullptr;
     uint32_t* cost_out = nullptr;
+    // full frames on 256-thread wide kernels (no queue, no counters): the
+    // next frame's order is sorted by an extra block of this launch
+    // (OrderFold) instead of a k_tile_order launch ahead of it
+    const bool can_fold = RT_ORDER_FOLD && sched && nranks == 1 && !packed && !small && wide && !counters &&
+                          !cfg.order_override && cfg.coop_cap == 0 && nb <= 256 * kFoldPerThread;
+    OrderFold fold;
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
             hipError_t me = hipMemsetAsync(sched->cost_prev, 0, (size_t)nb * 4, s);
@@ -2026,11 +2057,22 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             sched->fresh = false;
         }
         if (sched->have_prev) {
-            // computed already by the previous frame's k_trace_coop (one rank's tiles), else here
-            if (!sched->order_ready)
+            // computed already by the previous frame (its k_trace_coop for one rank's tiles, its
+            // k_trace's extra block for full frames), else here -- except that the first frame
+            // that folds runs in row-major order
+            if (sched->order_ready) {
+                order = sched->order;
+            } else if (!can_fold) {
                 hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order,
                                    sched->cost_ema);
-            order = sched->order;
+                order = sched->order;
+            }
+            if (can_fold) {
+                fold.cost = sched->cost_prev;
+                fold.out = sched->order_next;
+                fold.ema = sched->cost_ema;
+                fold.nb = nb;
+            }
         }
         sched->order_ready = false;
         cost_out = sched->cost_cur;
@@ -2079,9 +2121,9 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
-    k_trace_go<C, P, WI, NT>(buf, warity, nb * (256 / NT), s, nodes, wnodes, cap, tris, n, cam, w, h, spp, rank,    \
-                             nranks, tilesX, H, R, counters, (const float*)nullptr, Light{}, order, cost_out, px_prev, \
-                             px_cost, coop_cap, cq)
+    k_trace_go<C, P, WI, NT>(buf, warity, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, wnodes, cap, tris, n,     \
+                             cam, w, h, spp, rank, nranks, tilesX, H, R, counters, (const float*)nullptr, Light{},      \
+                             order, cost_out, px_prev, px_cost, coop_cap, cq, fold)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \
@@ -2098,6 +2140,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
 #undef RT_TRACE_W
 #undef RT_TRACE
 #undef RT_TRACE_NT
+    if (fold.out) {  // the order this launch sorts is the next frame's
+        std::swap(sched->order, sched->order_next);
+        sched->order_ready = true;
+    }
     if (coop_cap) {
         hipError_t le = hipGetLastError();
         if (le != hipSuccess) return le;
