@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -136,6 +137,46 @@ rt_status ensure_device(int dev) {
     HIPR(hipSetDevice(dev));
     return RT_OK;
 }
+
+// ---- roctx ranges (SURVEY.md §5 "tracing": the entry points show up as
+// named ranges in rocprofv3 --marker-trace).  Opt-in with RT_ROCTX=1: the
+// roctx library is then dlopen'ed on first use; otherwise (and when it is
+// absent) a range costs one branch.
+struct Roctx {
+    int (*push)(const char*) = nullptr;
+    int (*pop)() = nullptr;
+};
+
+const Roctx& roctx() {
+    static Roctx r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        const char* e = std::getenv("RT_ROCTX");
+        if (!e || std::strcmp(e, "1") != 0) return;
+        void* h = dlopen("librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librocprofiler-sdk-roctx.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) return;
+        auto push = reinterpret_cast<int (*)(const char*)>(dlsym(h, "roctxRangePushA"));
+        auto pop = reinterpret_cast<int (*)()>(dlsym(h, "roctxRangePop"));
+        if (push && pop) {
+            r.push = push;
+            r.pop = pop;
+        }
+    });
+    return r;
+}
+
+struct RtRange {
+    bool on;
+    explicit RtRange(const char* name) : on(roctx().push != nullptr) {
+        if (on) roctx().push(name);
+    }
+    ~RtRange() {
+        if (on) roctx().pop();
+    }
+    RtRange(const RtRange&) = delete;
+    RtRange& operator=(const RtRange&) = delete;
+};
 
 // ---- RCCL, loaded on first use (a host that never renders on several GPUs
 // never maps it).  An RCCL already in the process (e.g. torch's) is reused.
@@ -619,6 +660,7 @@ rt_status rt_camera_look_at(const double eye[3], const double at[3], const doubl
 
 // ------------------------------------------------------------------ build
 rt_status rt_bvh_build(rt_scene* s, int backend, uint32_t device_mask, double* ms_out) {
+    RtRange range_("rt_bvh_build");
     if (!s) return fail(RT_EINVAL, "null scene");
     if (backend == RT_BACKEND_CPU)
         return fail(RT_EINVAL, "librtamd has no CPU backend (the CPU oracle under oracle/ is test infrastructure)");
@@ -1037,6 +1079,7 @@ extern "C" {
 
 rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
                     rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
+    RtRange range_("rt_render");
     if (!s || !cam) return fail(RT_EINVAL, "bad render arguments");
     RTR(check_frame(w, h, spp));
     if (ngpus == 0 || ngpus > 64) return fail(RT_EINVAL, "ngpus must be 1..64");
@@ -1102,6 +1145,7 @@ extern "C" {
 rt_status rt_render_shadow_device(rt_scene* s, const rt_camera* cam, const float light[3], float ambient,
                                   uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba, void* stream,
                                   double* ms_out) {
+    RtRange range_("rt_render_shadow_device");
     if (!s || !cam || !light) return fail(RT_EINVAL, "bad render arguments");
     RTR(check_frame(w, h, spp));
     Replica* r = nullptr;
@@ -1189,6 +1233,7 @@ extern "C" {
 rt_status rt_render_path_device(rt_scene* s, const rt_camera* cam, const float light[3], float sky,
                                 uint32_t max_depth, uint32_t w, uint32_t h, uint32_t spp, void* d_hits, void* d_rgba,
                                 void* stream, double* ms_out) {
+    RtRange range_("rt_render_path_device");
     if (!s || !cam || !light) return fail(RT_EINVAL, "bad render arguments");
     RTR(check_frame(w, h, spp));
     if (max_depth > 64) return fail(RT_EINVAL, "max_depth exceeds 64");
@@ -1302,6 +1347,7 @@ rt_status rt_render_step_map(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, 
 
 rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, void* d_hits,
                            void* d_rgba, void* stream, double* ms_out) {
+    RtRange range_("rt_render_device");
     if (!s || !cam) return fail(RT_EINVAL, "bad render arguments");
     RTR(check_frame(w, h, spp));
     Replica* r = nullptr;
@@ -1325,6 +1371,7 @@ uint32_t rt_tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nrank
 rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                                  uint32_t rank, uint32_t nranks, void* d_packed_rgba, void* d_packed_hits,
                                  void* stream, double* ms_out) {
+    RtRange range_("rt_render_tiles_device");
     if (!s || !cam || !nranks || rank >= nranks) return fail(RT_EINVAL, "bad arguments");
     RTR(check_frame(w, h, spp));
     Replica* r = nullptr;
@@ -1632,6 +1679,7 @@ rt_status dbuild_replica(rt_scene* s, uint32_t rank, uint32_t nranks, Replica** 
 }  // namespace
 
 rt_status rt_dbuild_bounds(rt_scene* s, uint32_t rank, uint32_t nranks, float box_out[6]) {
+    RtRange range_("rt_dbuild_bounds");
     if (!box_out) return fail(RT_EINVAL, "null argument");
     Replica* r = nullptr;
     RTR(dbuild_replica(s, rank, nranks, &r));
@@ -1653,6 +1701,7 @@ rt_status rt_dbuild_bounds(rt_scene* s, uint32_t rank, uint32_t nranks, float bo
 }
 
 rt_status rt_dbuild_keys(rt_scene* s, uint32_t rank, uint32_t nranks, const float* boxes, uint32_t hist_out[1024]) {
+    RtRange range_("rt_dbuild_keys");
     if (!boxes || !hist_out) return fail(RT_EINVAL, "null argument");
     Replica* r = nullptr;
     RTR(dbuild_replica(s, rank, nranks, &r));
@@ -1672,6 +1721,7 @@ rt_status rt_dbuild_keys(rt_scene* s, uint32_t rank, uint32_t nranks, const floa
 }
 
 rt_status rt_dbuild_sort(rt_scene* s, uint32_t count) {
+    RtRange range_("rt_dbuild_sort");
     if (!s || count > s->n) return fail(RT_EINVAL, "bad arguments");
     if (s->reps.empty() || !s->reps[0]->d_n) return fail(RT_EINVAL, "rt_dbuild_keys first");
     Replica* r = s->reps[0].get();
@@ -1684,6 +1734,7 @@ rt_status rt_dbuild_sort(rt_scene* s, uint32_t count) {
 }
 
 rt_status rt_dbuild_subtrees(rt_scene* s, uint32_t rank, uint32_t nranks, uint32_t* ncross_out) {
+    RtRange range_("rt_dbuild_subtrees");
     if (!ncross_out) return fail(RT_EINVAL, "null argument");
     Replica* r = nullptr;
     RTR(dbuild_replica(s, rank, nranks, &r));
@@ -1710,6 +1761,7 @@ rt_status rt_dbuild_subtrees(rt_scene* s, uint32_t rank, uint32_t nranks, uint32
 }
 
 rt_status rt_dbuild_merge(rt_scene* s, uint32_t ncross_total) {
+    RtRange range_("rt_dbuild_merge");
     if (!s) return fail(RT_EINVAL, "null scene");
     if (s->reps.empty() || !s->reps[0]->d_n) return fail(RT_EINVAL, "rt_dbuild_subtrees first");
     Replica* r = s->reps[0].get();

@@ -28,6 +28,8 @@
  *   - HIP failures map to RT_EDEVICE, RCCL-side failures to RT_ECOMM;
  *   - there is NO CPU fallback: without a usable gfx950 device every compute
  *     entry point fails with RT_EDEVICE.
+ *   - environment RT_ROCTX=1: the device entry points are wrapped in roctx
+ *     ranges named after them (rocprofv3 --marker-trace).
  *
  * Numeric contract: SURVEY.md §9 (Appendix A).  Morton codes, sorted indices,
  * topology, AABBs and images are bit-exact vs the CPU oracle; hits match the
