@@ -8,7 +8,8 @@ frame i is then timed with tile orders sorted longest-first by
   sum      the tile's total steps
   q8       the tile's 8th-largest pixel step count
   self     frame i's own durations (upper bound)
-usage: python tools/order_predict_exp.py [frames] [reps]"""
+usage: python tools/order_predict_exp.py [frames] [reps]
+(own top-K: how much of the gap the K costliest tiles of the frame itself close)"""
 import ctypes as C
 import os
 import sys
@@ -67,9 +68,12 @@ for i in range(1, frames + 1):
     dur0, st0 = measure(cams[i - 1])
     dur1, _ = measure(cams[i])
     dm = prev if prev is not None else dur0
-    keys = {"dur": dur0, "q8": np.sort(st0, 1)[:, -8], "max2": np.maximum(dur0, dm), "mean2": dur0 + dm,
-            "dur+q8": np.argsort(np.argsort(dur0)) + np.argsort(np.argsort(np.sort(st0, 1)[:, -8])),
-            "self": dur1}
+    keys = {"mean2": dur0 + dm, "self": dur1}
+    base = np.argsort(-(dur0 + dm), kind="stable")
+    for K in (32, 128, 512):  # the frame's own K costliest tiles first, the rest by mean2
+        top = np.argsort(-dur1, kind="stable")[:K]
+        rest = base[~np.isin(base, top)]
+        res.setdefault(f"own top-{K} + mean2", []).append(timed(cams[i], np.concatenate([top, rest])))
     prev = dur0
     for k, v in keys.items():
         res.setdefault(k, []).append(timed(cams[i], np.argsort(-v, kind="stable")))
