@@ -1055,7 +1055,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     b.nzero = kZEnd;
     hipError_t e;
 #define RT_ALLOC(ptr, bytes) \
-    if ((e = hipMalloc((void**)&(ptr), (bytes))) != hipSuccess) { free_build(b); return e; }
+    if ((e = dev_alloc(&(ptr), (bytes))) != hipSuccess) { free_build(b); return e; }
     RT_ALLOC(b.tris, N * 36);
     RT_ALLOC(b.keys[0], N * 4);
     RT_ALLOC(b.keys[1], N * 4);

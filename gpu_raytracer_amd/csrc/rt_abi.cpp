@@ -39,6 +39,16 @@ constexpr uint32_t kMaxDbuildRanks = 64;             // rt_dbuild_*: ranks of on
 constexpr uint32_t kRefitLeaves = (uint32_t)rt::kRefitT;  // leaves per refit block (a share is whole blocks)
 
 // One device's copy of a scene's BVH plus that device's render scratch.
+// Tile-order state of one frame shape: the device maps (TileSched) and the
+// shape they belong to.
+struct SchedState {
+    void* d = nullptr;  // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per
+                        // tile slot, then the heavy-ray queue
+    size_t cap = 0;
+    rt::TileSched sched;
+    uint32_t key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the maps
+};
+
 struct Replica {
     int device = 0;
     hipStream_t stream = nullptr;  // the replica's own stream (builds, synchronous renders)
@@ -53,10 +63,9 @@ struct Replica {
     size_t rgba_cap = 0;
     unsigned long long* d_ctr = nullptr;
     uint32_t* d_work = nullptr;  // pool-trace unit counters
-    void* d_order = nullptr;     // tile-order state: [order][cost A][cost B] per tile slot
-    size_t order_cap = 0;
-    rt::TileSched sched;
-    uint32_t sched_key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the cost map
+    SchedState ord;       // the frames' tile-order state (sched_for)
+    SchedState ord_diag;  // scratch state of the counting launches: a diagnostic call never
+                          // perturbs the next frame's order
     rt::PathBufs path;                        // wavefront path-mode state (grown on demand)
     hipEvent_t r0 = nullptr, r1 = nullptr;
     // multi-GPU render: this rank's packed slabs; the root's gathered slabs
@@ -252,7 +261,7 @@ rt_status replica_init(Replica& r) {
     HIPR(hipEventCreateWithFlags(&r.r0, fl));
     HIPR(hipEventCreateWithFlags(&r.r1, fl));
     HIPR(hipEventCreateWithFlags(&r.last, hipEventDisableTiming | hipEventDisableSystemFence));
-    HIPR(hipMalloc((void**)&r.d_work, 4096));  // kPoolCounters x 128 B
+    HIPR(rt::dev_alloc(&r.d_work, 4096));  // kPoolCounters x 128 B
     return RT_OK;
 }
 
@@ -263,7 +272,7 @@ void replica_free(Replica& r) {
     (void)hipStreamSynchronize(r.stream);
     rt::free_build(r.bufs);
     rt::free_path(r.path);
-    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.d_order, r.d_slab, r.d_slab_hits, r.d_recv,
+    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.ord.d, r.ord_diag.d, r.d_slab, r.d_slab_hits, r.d_recv,
                     r.d_recv_hits, (void*)r.dk[0], (void*)r.dk[1], (void*)r.dv[0], (void*)r.dv[1], (void*)r.dcross,
                     (void*)r.dcross_all, (void*)r.dboxes})
         if (p) (void)hipFree(p);
@@ -290,7 +299,8 @@ rt_status primary(rt_scene* s, Replica** out) {
 }
 
 // record arity of the next build of an n-triangle scene (build.wide_arity;
-// the 8-ary records' 32-bit buffer offsets need n <= 2^26) and record size
+// the 8-ary records' 32-bit buffer offsets need n <= kWide8MaxN) and record size
+static_assert(rt::kWide8MaxN == RT_WIDE8_MAX_N, "header and library agree on the 8-ary size cap");
 uint32_t build_arity(uint32_t n) { return (rt::config_snapshot().wide_arity == 8 && n <= rt::kWide8MaxN) ? 8u : 4u; }
 uint64_t wide_bytes(uint32_t arity) { return arity == 8 ? 96u : 64u; }
 
@@ -356,6 +366,9 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         HIPR(hipSetDevice(r->device));
         RTR(join_caller_work(*r));
         r->bufs.warity = build_arity(s->n);
+        // a rebuild that fails half-way must not leave the old flag over a
+        // half-written BVH: built again only after the synchronize below
+        r->built = false;
         hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
     }
@@ -387,7 +400,7 @@ rt_status grow(void** p, size_t* cap, size_t need) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     *cap = 0;
-    hipError_t e = hipMalloc(p, need ? need : 16);
+    hipError_t e = rt::dev_alloc(p, need);
     if (e == hipErrorOutOfMemory) return fail(RT_ENOMEM, "device allocation failed");
     if (e != hipSuccess) return hip_fail(e, "hipMalloc");
     *cap = need;
@@ -398,11 +411,11 @@ rt_status grow(void** p, size_t* cap, size_t need) {
 // cost map of the previous frame with the same w, h, spp, rank, nranks
 // drives this frame's dispatch order.  A failed allocation is reported
 // (RT_ENOMEM / RT_EDEVICE), never silently replaced by row-major order.
-rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
+rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
                     rt::TileSched** out) {
     const uint32_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     const uint32_t key[5] = {w, h, spp, rank, nranks};
-    const bool same = std::memcmp(key, r.sched_key, sizeof(key)) == 0;
+    const bool same = std::memcmp(key, r.key, sizeof(key)) == 0;
     // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per tile slot,
     // then (trace.coop_cap) 2 queue counters and the heavy-ray queue
     const rt::TraceConfig cfg = rt::config_snapshot();
@@ -411,10 +424,10 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
     const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
     const size_t qoff = (maps + 255) & ~size_t(255);
     const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
-    if (!same || r.order_cap < need || r.sched.coop_qcap != qcap) {
-        std::memset(r.sched_key, 0, sizeof(r.sched_key));  // invalid until the maps exist
-        RTR(grow(&r.d_order, &r.order_cap, need));
-        uint32_t* b = static_cast<uint32_t*>(r.d_order);
+    if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
+        std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
+        RTR(grow(&r.d, &r.cap, need));
+        uint32_t* b = static_cast<uint32_t*>(r.d);
         r.sched.order = b;
         r.sched.order_next = b + nb;
         r.sched.cost_prev = b + 2 * nb;
@@ -422,7 +435,7 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
         r.sched.cost_ema = b + 4 * nb;
         r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 5 * nb);
         r.sched.px_cur = r.sched.px_prev + (size_t)nb * 256;
-        char* qb = static_cast<char*>(r.d_order) + qoff;
+        char* qb = static_cast<char*>(r.d) + qoff;
         r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(qb) : nullptr;
         r.sched.coop_q = qcap ? reinterpret_cast<uint4*>(qb + 512) : nullptr;
         r.sched.coop_qcap = qcap;
@@ -432,14 +445,14 @@ rt_status sched_for(Replica& r, uint32_t w, uint32_t h, uint32_t spp, uint32_t r
         r.sched.have_prev = false;
         r.sched.order_ready = false;
         r.sched.fresh = true;
-        std::memcpy(r.sched_key, key, sizeof(key));
+        std::memcpy(r.key, key, sizeof(key));
     }
     *out = &r.sched;
     return RT_OK;
 }
 
 // after a launch that used sched_for: this frame's map becomes the previous one
-void sched_done(Replica& r, const rt::TraceConfig& cfg) {
+void sched_done(SchedState& r, const rt::TraceConfig& cfg) {
     if (!cfg.tile_order) return;
     std::swap(r.sched.cost_prev, r.sched.cost_cur);
     std::swap(r.sched.px_prev, r.sched.px_cur);
@@ -458,7 +471,7 @@ struct DevBuf {
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
-    hipError_t alloc(size_t bytes) { return hipMalloc(&p, bytes ? bytes : 16); }
+    hipError_t alloc(size_t bytes) { return rt::dev_alloc(&p, bytes); }
     template <class T>
     T* as() const { return reinterpret_cast<T*>(p); }
 };
@@ -500,6 +513,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.buf_loads" && (value == 0 || value == 1)) c.buf_loads = (uint32_t)value;
     else if (k == "trace.coop_lanes" && (value == 16 || value == 32 || value == 64)) c.coop_lanes = (uint32_t)value;
     else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
+    else if (k == "debug.poison" && (value == 0 || value == 1)) c.poison = (uint32_t)value;
     else return false;
     return true;
 }
@@ -1018,13 +1032,13 @@ rt_status render_tiled(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h
         RTR(join_caller_work(R));
         if (r) HIPR(hipStreamWaitEvent(R.stream, root.r0, 0));
         rt::TileSched* sched = nullptr;
-        RTR(sched_for(R, w, h, spp, r, P, &sched));
+        RTR(sched_for(R.ord, w, h, spp, r, P, &sched));
         hipError_t e = rt::launch_trace(R.bufs.nodes, R.bufs.wnodes, R.bufs.warity,
                                         R.bufs.tri_s, s->n, camf(cam), w, h, spp, r, P,
                                         true, hits_out ? R.d_slab_hits : nullptr, R.d_slab, nullptr, false, R.d_work,
                                         sched, R.stream);
         if (e != hipSuccess) return hip_fail(e, "launch_trace");
-        sched_done(R, cfg);
+        sched_done(R.ord, cfg);
     }
     if (!emulate) {
         const Rccl& RC = rccl();
@@ -1096,14 +1110,14 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     RTR(grow(&r->d_rgba, &r->rgba_cap, (size_t)w * h * 4));
     RTR(join_caller_work(*r));
     rt::TileSched* sched = nullptr;
-    RTR(sched_for(*r, w, h, spp, 0, 1, &sched));
+    RTR(sched_for(r->ord, w, h, spp, 0, 1, &sched));
     HIPR(hipEventRecord(r->r0, r->stream));
     hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                     r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
                                     false, hits_out ? r->d_hits : nullptr, r->d_rgba, nullptr, false, r->d_work, sched,
                                     r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
-    sched_done(*r, cfg);
+    sched_done(r->ord, cfg);
     HIPR(hipEventRecord(r->r1, r->stream));
     HIPR(hipStreamSynchronize(r->stream));
     float ms = 0;
@@ -1181,7 +1195,7 @@ rt_status rt_render_shadow_work(rt_scene* s, const rt_camera* cam, const float l
     Replica* r = nullptr;
     RTR(need_built(s, &r));
     RTR(join_caller_work(*r));
-    if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
+    if (!r->d_ctr) HIPR(rt::dev_alloc(&r->d_ctr, 32));
     HIPR(hipMemsetAsync(r->d_ctr, 0, 16, r->stream));
     hipError_t e = rt::launch_trace_shadow(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                            r->bufs.tri_s, r->bufs.tris, s->n, camf(cam),
@@ -1272,7 +1286,7 @@ rt_status rt_render_path_work(rt_scene* s, const rt_camera* cam, const float lig
     Replica* r = nullptr;
     RTR(need_built(s, &r));
     RTR(join_caller_work(*r));
-    if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
+    if (!r->d_ctr) HIPR(rt::dev_alloc(&r->d_ctr, 32));
     HIPR(hipMemsetAsync(r->d_ctr, 0, 32, r->stream));
     std::string err;
     hipError_t e = path_launch(s, *r, cam, light, sky, max_depth, w, h, spp, nullptr, nullptr, r->d_ctr, r->stream, err);
@@ -1291,12 +1305,17 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     Replica* r = nullptr;
     RTR(need_built(s, &r));
     RTR(join_caller_work(*r));
-    if (!r->d_ctr) HIPR(hipMalloc((void**)&r->d_ctr, 32));
+    if (!r->d_ctr) HIPR(rt::dev_alloc(&r->d_ctr, 32));
     HIPR(hipMemsetAsync(r->d_ctr, 0, 16, r->stream));
     // the kernels' own work counters include the heavy-ray queue's pass when
     // it is on (trace.coop_cap*), which needs the frame shape's queue
     rt::TileSched* sched = nullptr;
-    if (!binary) RTR(sched_for(*r, w, h, spp, rank, nranks, &sched));
+    // (the replica's scratch state, reset every call: the counts do not
+    // depend on the dispatch order, and the frames' own maps stay untouched)
+    if (!binary) {
+        std::memset(r->ord_diag.key, 0, sizeof(r->ord_diag.key));
+        RTR(sched_for(r->ord_diag, w, h, spp, rank, nranks, &sched));
+    }
     hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                     r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
                                     nranks, packed, nullptr, nullptr, r->d_ctr, binary, r->d_work, sched, r->stream);
@@ -1334,14 +1353,14 @@ rt_status rt_render_step_map(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, 
     Replica* r = nullptr;
     RTR(need_built(s, &r));
     const uint32_t key[5] = {w, h, spp, rank, nranks};
-    if (!r->sched.have_prev || std::memcmp(key, r->sched_key, sizeof(key)) != 0)
+    if (!r->ord.sched.have_prev || std::memcmp(key, r->ord.key, sizeof(key)) != 0)
         return fail(RT_EINVAL, "no previous frame of this shape");
     const size_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     if (count < nb * 256) return fail(RT_EINVAL, "step map buffer too small");
     HIPR(hipSetDevice(r->device));
     if (r->last_stream) HIPR(hipEventSynchronize(r->last));
     HIPR(hipStreamSynchronize(r->stream));
-    HIPR(hipMemcpy(out, r->sched.px_prev, nb * 256 * sizeof(uint16_t), hipMemcpyDeviceToHost));
+    HIPR(hipMemcpy(out, r->ord.sched.px_prev, nb * 256 * sizeof(uint16_t), hipMemcpyDeviceToHost));
     return RT_OK;
 }
 
@@ -1354,13 +1373,13 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     RTR(need_built(s, &r));
     const rt::TraceConfig cfg = rt::config_snapshot();
     rt::TileSched* sched = nullptr;
-    RTR(sched_for(*r, w, h, spp, 0, 1, &sched));
+    RTR(sched_for(r->ord, w, h, spp, 0, 1, &sched));
     RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
         return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                 r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
                                 d_hits, d_rgba, nullptr, false, r->d_work, sched, hs);
     }));
-    sched_done(*r, cfg);
+    sched_done(r->ord, cfg);
     return RT_OK;
 }
 
@@ -1378,13 +1397,13 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     RTR(need_built(s, &r));
     const rt::TraceConfig cfg = rt::config_snapshot();
     rt::TileSched* sched = nullptr;
-    RTR(sched_for(*r, w, h, spp, rank, nranks, &sched));
+    RTR(sched_for(r->ord, w, h, spp, rank, nranks, &sched));
     RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
         return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                 r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks,
                                 true, d_packed_hits, d_packed_rgba, nullptr, false, r->d_work, sched, hs);
     }));
-    sched_done(*r, cfg);
+    sched_done(r->ord, cfg);
     return RT_OK;
 }
 
@@ -1662,14 +1681,14 @@ rt_status dbuild_replica(rt_scene* s, uint32_t rank, uint32_t nranks, Replica** 
         if (r->dboxes) { (void)hipFree(r->dboxes); r->dboxes = nullptr; }
         r->d_n = 0;
         for (uint32_t** p : {&r->dk[0], &r->dk[1], &r->dv[0], &r->dv[1]}) {
-            hipError_t e = hipMalloc((void**)p, n4);
+            hipError_t e = rt::dev_alloc(p, n4);
             if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "hipMalloc");
         }
         for (uint32_t** p : {&r->dcross, &r->dcross_all}) {
-            hipError_t e = hipMalloc((void**)p, cc);
+            hipError_t e = rt::dev_alloc(p, cc);
             if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "hipMalloc");
         }
-        hipError_t e = hipMalloc((void**)&r->dboxes, kMaxDbuildRanks * 6 * sizeof(float));
+        hipError_t e = rt::dev_alloc(&r->dboxes, kMaxDbuildRanks * 6 * sizeof(float));
         if (e != hipSuccess) return e == hipErrorOutOfMemory ? fail(RT_ENOMEM, "device allocation failed") : hip_fail(e, "hipMalloc");
         r->d_n = s->n;
     }

@@ -135,10 +135,23 @@ struct TraceConfig {
     uint32_t coop_lanes = 32;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
     uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
+    uint32_t poison = 0;          // debug.poison: fill every new device allocation with 0xFF bytes, so a
+                                  // read of a byte nothing wrote is deterministic (and visible)
 };
 
+// Every device buffer of the library is allocated here: hipMalloc, then
+// with debug.poison a 0xFF fill completed before the buffer is handed out.
+hipError_t dev_alloc(void** p, size_t bytes);
+template <class T>
+inline hipError_t dev_alloc(T** p, size_t bytes) { return dev_alloc(reinterpret_cast<void**>(p), bytes); }
+
 constexpr uint32_t kCoopEntryBytes = 208;  // heavy-ray queue entry (trace_kernels.hip kCoopEntry x 16 B)
-constexpr uint32_t kWide8MaxN = 1u << 26;  // 8-ary records need 32-bit buffer offsets ((n-1) x 96 B)
+// 8-ary records are read through 32-bit buffer offsets: the last record ends
+// at (n-1) x 96 B, which must not pass 2^32 - 1 (n <= 44,739,243; above that
+// the build writes 4-ary records, whose (n-1) x 64 B fit up to n = 2^26)
+constexpr uint32_t kWide8MaxN = 0xFFFFFFFFu / 96u + 1u;
+static_assert((uint64_t)(kWide8MaxN - 1) * 96u <= 0xFFFFFFFFull && (uint64_t)kWide8MaxN * 96u > 0xFFFFFFFFull,
+              "largest n whose 8-ary records fit 32-bit offsets");
 
 // Per-launch tile scheduling state (owned by the scene, one per frame shape).
 struct TileSched {

@@ -1957,6 +1957,20 @@ bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key
     return true;
 }
 
+hipError_t dev_alloc(void** p, size_t bytes) {
+    *p = nullptr;
+    hipError_t e = hipMalloc(p, bytes ? bytes : 16);
+    if (e != hipSuccess || !config_snapshot().poison) return e;
+    // debug.poison: 0xFF in every byte (a NaN float, RT_SENT index, 255 plane),
+    // finished before any stream can use the buffer
+    if ((e = hipMemset(*p, 0xFF, bytes ? bytes : 16)) == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(*p);
+        *p = nullptr;
+    }
+    return e;
+}
+
 // the wide stack entries a launch uses: trace.stack_cap (tests force
 // overflows with small values), at most the arity's stack; 0 = all of it
 static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity) {
@@ -1996,7 +2010,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     float4* H = reinterpret_cast<float4*>(hits);
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     if (warity != 4 && warity != 8) return hipErrorInvalidValue;
-    if (warity == 8 && n > kBufMaxN) return hipErrorInvalidValue;  // the build keeps 8-ary records to n <= 2^26
+    if (warity == 8 && n > kWide8MaxN) return hipErrorInvalidValue;  // the build keeps 8-ary records to n <= kWide8MaxN
     const uint32_t cap = stack_cap_for(cfg, warity);
     if (cfg.variant == 1 && wnodes && warity == 4 && n >= 2 && !binary_counts && work) {
         const uint32_t nunits = nb * 4;
@@ -2286,15 +2300,15 @@ hipError_t alloc_path(PathBufs& b, uint32_t cap) {
     free_path(b);
     const uint64_t q = 2ull * cap;
     hipError_t e;
-    if ((e = hipMalloc((void**)&b.f, (uint64_t)kPathF * cap * 4)) != hipSuccess) return e;
-    if ((e = hipMalloc((void**)&b.u, (uint64_t)kPathU * cap * 4)) != hipSuccess) return e;
-    if ((e = hipMalloc((void**)&b.rays, q * 32)) != hipSuccess) return e;
+    if ((e = dev_alloc(&b.f, (uint64_t)kPathF * cap * 4)) != hipSuccess) return e;
+    if ((e = dev_alloc(&b.u, (uint64_t)kPathU * cap * 4)) != hipSuccess) return e;
+    if ((e = dev_alloc(&b.rays, q * 32)) != hipSuccess) return e;
     for (int i = 0; i < 2; ++i) {
-        if ((e = hipMalloc((void**)&b.keys[i], q * 4)) != hipSuccess) return e;
-        if ((e = hipMalloc((void**)&b.vals[i], q * 4)) != hipSuccess) return e;
+        if ((e = dev_alloc(&b.keys[i], q * 4)) != hipSuccess) return e;
+        if ((e = dev_alloc(&b.vals[i], q * 4)) != hipSuccess) return e;
     }
-    if ((e = hipMalloc((void**)&b.counts, (uint64_t)sort_tiles((uint32_t)q) * 256 * 4 + 1024)) != hipSuccess) return e;
-    if ((e = hipMalloc((void**)&b.ghist, 4096 + 256)) != hipSuccess) return e;
+    if ((e = dev_alloc(&b.counts, (uint64_t)sort_tiles((uint32_t)q) * 256 * 4 + 1024)) != hipSuccess) return e;
+    if ((e = dev_alloc(&b.ghist, 4096 + 256)) != hipSuccess) return e;
     b.qcount = b.ghist + 1024;
     if ((e = hipHostMalloc((void**)&b.hq, 256, hipHostMallocDefault)) != hipSuccess) return e;
     b.cap = cap;

@@ -134,9 +134,13 @@ rt_status rt_bvh_load(rt_scene* s, const char* path);
 /* Read back the wide trace records, one per binary internal node: (n-1) x 64 B
  * for 4-ary K7w records, (n-1) x 96 B for 8-ary K7w8 records (layouts:
  * gpu_raytracer_amd/csrc/rt_device.h); nothing for n < 2.  The arity is the
- * build's rt_config_set("build.wide_arity", 4 | 8) (8 only for n <= 2^26), as
+ * build's rt_config_set("build.wide_arity", 4 | 8) (8 only for n <= RT_WIDE8_MAX_N), as
  * reported by rt_bvh_wide_arity.  SURVEY.md §8(f) row 1 ("4/8-wide"). */
 rt_status rt_bvh_read_wide(const rt_scene* s, void* records);
+/* largest n built with 8-ary records: the trace reads them through 32-bit
+ * byte offsets, and the last record ends at (n-1) x 96 B <= 2^32 - 1; larger
+ * scenes get 4-ary records whatever build.wide_arity says */
+#define RT_WIDE8_MAX_N 44739243u
 rt_status rt_bvh_wide_arity(const rt_scene* s, uint32_t* arity_out);
 
 /* ---- render (SURVEY.md §8(b) rt_render(scene, cam, w, h, spp, ngpus, hits,
@@ -332,8 +336,11 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * (default 65536; rays beyond it keep tracing alone).  "build.stage_events"
  * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
  * 0/1: timing events of scenes created afterwards record with the
- * system-scope fence (default 0: no L2 writeback at each record).  Results
- * are bit-identical for every setting. */
+ * system-scope fence (default 0: no L2 writeback at each record).
+ * "debug.poison" 0/1: every device buffer the library allocates from then on
+ * is filled with 0xFF bytes before first use, so reading a byte no kernel
+ * wrote gives the same (wrong) value every run instead of allocator luck.
+ * Results are bit-identical for every setting. */
 rt_status rt_config_set(const char* key, int64_t value);
 
 const char* rt_last_error(void);

@@ -249,6 +249,7 @@ CONFIG_KEYS = {
     "trace.buf_loads": ([0, 1], [2, -1], 1),
     "trace.coop_lanes": ([16, 32, 64], [0, 8, 48, 128], 32),
     "trace.coop_max": ([1, 64, 65536, 1 << 24], [0, -1, (1 << 24) + 1], 65536),
+    "debug.poison": ([0, 1], [2, -1], 0),
 }
 
 
@@ -272,3 +273,14 @@ def test_config_unknown_key(rt):
     with pytest.raises(rt.RtError) as e:
         rt.config_set("trace.no_such_knob", 1)
     assert e.value.status == -1
+
+
+def test_wide8_size_cap():
+    """RT_WIDE8_MAX_N: the largest n whose 8-ary records' last
+    byte offset (n-1) x 96 fits the trace's 32-bit buffer offsets; one more
+    triangle would wrap.  (rt_abi.cpp static_asserts the library agrees.)"""
+    import re
+    with open(os.path.join(ROOT, "include", "gpu_raytracer_amd.h")) as f:
+        m = re.search(r"#define RT_WIDE8_MAX_N (\d+)u", f.read())
+    cap = int(m.group(1))
+    assert (cap - 1) * 96 <= 2**32 - 1 < cap * 96
