@@ -87,6 +87,15 @@ def parse():
                     help="warm-up + timed steps only (the PMC passes of tools/profile_r02.sh)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for the benchmark; gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--extras", action="store_true",
+                    help="N>1: also time the BVH broadcast and the distributed build after the headline "
+                         "(off by default: the headline line must not depend on them)")
+    ap.add_argument("--pg-timeout", type=float, default=120.0,
+                    help="seconds before a stuck collective fails the process group")
+    ap.add_argument("--deadline", type=float, default=900.0,
+                    help="`--gpus N` without a launcher: seconds before the parent kills its rank processes")
+    ap.add_argument("--inject-hang", type=int, default=-1,
+                    help="testing only: this rank sleeps forever in the --extras leg")
     return ap.parse_args()
 
 
@@ -98,20 +107,48 @@ def _free_port():
     return p
 
 
+def supervise(procs, deadline_s, grace_s=10.0, poll_s=0.2) -> int:
+    """Wait for the rank processes; never forever.  A rank that exits non-zero
+    (or by a signal) fails the run: the others get `grace_s` to finish, then
+    are killed (they would otherwise sit in a collective with a dead peer).
+    Past `deadline_s` every rank still running is killed and the result is
+    124.  The parent never touched a GPU, so killing its children is safe.
+    Returns 0 only when every rank exited 0."""
+    t0 = time.monotonic()
+    fail_at, rc = None, 0
+    while True:
+        alive = [p for p in procs if p.poll() is None]
+        for p in procs:
+            if p.returncode not in (None, 0):
+                rc = max(rc, abs(p.returncode))
+                fail_at = fail_at if fail_at is not None else time.monotonic()
+        if not alive:
+            return rc
+        now = time.monotonic()
+        late = now - t0 > deadline_s
+        if late or (fail_at is not None and now - fail_at > grace_s):
+            for p in alive:
+                p.kill()
+            for p in alive:
+                p.wait()
+            print(f"bench: {'deadline of %.0f s passed' % deadline_s if late else 'a rank failed'}; killed "
+                  f"{len(alive)} rank process(es)", file=sys.stderr)
+            return 124 if late else max(rc, 1)
+        time.sleep(poll_s)
+
+
 def spawn_ranks(args) -> int:
     """`bench.py --gpus N` without a launcher: start N rank processes (one per
     GPU) with the torch.distributed env, before anything here touches a GPU;
-    rank 0 prints the JSON line.  Returns the worst exit status."""
+    rank 0 prints the JSON line.  Returns the worst exit status (124 when the
+    --deadline passed and the ranks were killed)."""
     port = str(_free_port())
     procs = []
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    for p in procs:
-        rc = max(rc, abs(p.wait()))
-    return rc
+    return supervise(procs, args.deadline)
 
 
 def orbit_view(view, step):
@@ -310,10 +347,14 @@ def main():
     local = local % max(ndev, 1)  # rehearsal: several ranks may share one GPU (gloo only)
     torch.cuda.set_device(local)
     if world > 1:
+        # a collective stuck longer than --pg-timeout fails the process group
+        # (the rank exits) instead of holding the run until an outside limit
+        from datetime import timedelta
+        tmo = timedelta(seconds=args.pg_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
 
     cfg = S.CONFIGS[args.config]
     view = S.VIEWS[cfg.scene]
@@ -445,8 +486,12 @@ def main():
 
     # "rank 0 builds and then broadcasts" measured next to the
     # replicated build (untimed by the step contract; 1 warm-up + 3 timed)
+    # Both are opt-in (--extras): the headline line must not wait on legs
+    # that are not part of it.
+    if world > 1 and args.extras and rank == args.inject_hang:
+        time.sleep(1e9)  # testing: a rank that never reaches the next collective
     bvh_exchange = None
-    if world > 1 and args.dist_backend == "nccl":
+    if world > 1 and args.extras and args.dist_backend == "nccl":
         try:
             bms = []
             for i in range(4):
@@ -469,13 +514,14 @@ def main():
     # prefix all-to-all, share gathers) timed next to the replicated build;
     # its BVH must equal the replicated one bit for bit (checked on device).
     dbuild = None
-    if world > 1:
+    if world > 1 and args.extras:
         try:
             dms, info = [], None
             for i in range(4):
                 barrier()
                 tb0 = time.perf_counter()
-                info = D.distributed_build(D.LibStages(scene, dev), D.Exchange(stage=args.dist_backend == "gloo"))
+                info = D.distributed_build(D.LibStages(scene, dev),
+                                           D.Exchange(stage=args.dist_backend == "gloo", device=dev))
                 barrier()
                 if i:
                     dms.append((time.perf_counter() - tb0) * 1e3)

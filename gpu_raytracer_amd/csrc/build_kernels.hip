@@ -1089,8 +1089,8 @@ void free_build(BuildBufs& b) {
 }
 
 hipError_t launch_bounds_only(const float* tris, uint32_t n, float* partials, BuildParams* params, hipStream_t s) {
-    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, tris, n, partials, (uint32_t*)nullptr, 0u);
-    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, partials, bounds_grid(n), params);
+    RT_KLAUNCH(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, tris, n, partials, (uint32_t*)nullptr, 0u);
+    RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, partials, bounds_grid(n), params);
     return hipGetLastError();
 }
 
@@ -1099,10 +1099,10 @@ static hipError_t launch_morton_impl(const float* tris, uint32_t n, BuildParams*
                                      hipStream_t s, bool msb = false) {
     if (!n) return hipSuccess;
     if (msb)
-        hipLaunchKernelGGL(k_morton<true>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials, nb,
+        RT_KLAUNCH(k_morton<true>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials, nb,
                            keys, vals, ghist, counts0);
     else
-        hipLaunchKernelGGL(k_morton<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials,
+        RT_KLAUNCH(k_morton<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, tris, n, params, partials,
                            nb, keys, vals, ghist, counts0);
     return hipGetLastError();
 }
@@ -1114,20 +1114,20 @@ hipError_t launch_morton(const float* tris, uint32_t n, const BuildParams* param
 
 hipError_t launch_leaf_nodes(const float4* tri_s, uint32_t n, void* nodes, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_leaf_nodes, dim3(cdiv(n, 256)), dim3(256), 0, s, tri_s, n, nodes);
+    RT_KLAUNCH(k_leaf_nodes, dim3(cdiv(n, 256)), dim3(256), 0, s, tri_s, n, nodes);
     return hipGetLastError();
 }
 
 hipError_t launch_leaf_tris(const void* nodes, const float* tris, uint32_t n, float4* tri_s, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_leaf_tris, dim3(cdiv(n, 256)), dim3(256), 0, s, nodes, tris, n, tri_s);
+    RT_KLAUNCH(k_leaf_tris, dim3(cdiv(n, 256)), dim3(256), 0, s, nodes, tris, n, tri_s);
     return hipGetLastError();
 }
 
 hipError_t launch_karras(const uint32_t* keys, const uint32_t* svals, const float* tris, uint32_t n, uint4* topo,
                          uint32_t* parent, void* nodes, float4* tri_s, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_karras_leaves, dim3(cdiv(n, 256)), dim3(256), 0, s, keys, svals, tris, n, topo, parent, nodes,
+    RT_KLAUNCH(k_karras_leaves, dim3(cdiv(n, 256)), dim3(256), 0, s, keys, svals, tris, n, topo, parent, nodes,
                        tri_s);
     return hipGetLastError();
 }
@@ -1168,22 +1168,22 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
         const size_t lds = 2ull * P * sizeof(Aabb);
         const hipError_t e = ensure_cross_attr();
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_refit_cross<true>, dim3(RT_CROSS_GRID), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
+        RT_KLAUNCH(k_refit_cross<true>, dim3(RT_CROSS_GRID), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
         const uint32_t L = sparse_levels(m);
         for (uint32_t lv = 1; lv < L; ++lv) {
-            hipLaunchKernelGGL(k_sparse_level, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table + (uint64_t)(lv - 1) * m * 6,
+            RT_KLAUNCH(k_sparse_level, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table + (uint64_t)(lv - 1) * m * 6,
                                b.table + (uint64_t)lv * m * 6, m, 1u << (lv - 1));
         }
-        hipLaunchKernelGGL(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
+        RT_KLAUNCH(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     if (arity == 8)
-        hipLaunchKernelGGL(k_wide_cross<8>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+        RT_KLAUNCH(k_wide_cross<8>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
                            cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     else
-        hipLaunchKernelGGL(k_wide_cross<4>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+        RT_KLAUNCH(k_wide_cross<4>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
                            cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     return hipGetLastError();
 }
@@ -1194,11 +1194,11 @@ static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wi
                                      uint32_t block0, uint32_t nblocks, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     if (arity == 8)
-        hipLaunchKernelGGL(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
+        RT_KLAUNCH(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
                            b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0);
     else
-        hipLaunchKernelGGL(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
+        RT_KLAUNCH(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
                            b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0);
     return hipGetLastError();
@@ -1226,9 +1226,9 @@ hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
 
 // centroid bounds of tris[lo, lo + cnt) -> b.params (lo, hi; inv of the slice)
 hipError_t launch_dbuild_bounds(const BuildBufs& b, uint32_t lo, uint32_t cnt, hipStream_t s) {
-    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(cnt)), dim3(256), 0, s, b.tris + (uint64_t)lo * 9, cnt, b.partials,
+    RT_KLAUNCH(k_bounds, dim3(bounds_grid(cnt)), dim3(256), 0, s, b.tris + (uint64_t)lo * 9, cnt, b.partials,
                        (uint32_t*)nullptr, 0u);
-    hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, bounds_grid(cnt), b.params);
+    RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, bounds_grid(cnt), b.params);
     return hipGetLastError();
 }
 
@@ -1242,7 +1242,7 @@ hipError_t launch_dbuild_keys(const BuildBufs& b, uint32_t lo, uint32_t cnt, con
     hipError_t e = hipMemsetAsync(ghist, 0, 1024 * 4, s);
     if (e != hipSuccess) return e;
     // block 0 also stores the global lo/hi/inv into params (rt_bvh_read)
-    hipLaunchKernelGGL(k_morton<true>, dim3(std::max(1u, sort_tiles(cnt))), dim3(kSortThreads), 0, s,
+    RT_KLAUNCH(k_morton<true>, dim3(std::max(1u, sort_tiles(cnt))), dim3(kSortThreads), 0, s,
                        b.tris + (uint64_t)lo * 9, cnt, b.params, boxes, nboxes, b.keys[1], b.vals[1], ghist, b.counts,
                        lo);
     return hipGetLastError();
@@ -1287,12 +1287,12 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
         return (ev && (stages || i == 0 || i == 6)) ? hipEventRecord(ev->e[i], s) : hipSuccess;
     };
     if ((e = rec(0)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.zero, kZEnd);
+    RT_KLAUNCH(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.zero, kZEnd);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     if ((e = rec(1)) != hipSuccess) return e;
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
-    if (!n) hipLaunchKernelGGL(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
+    if (!n) RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
     const bool msb = n >= 2 && n <= kMsbMaxN && cfg.sort_msb;
     if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
                                 b.zero + kZHist, counts[0], s, msb)) != hipSuccess)

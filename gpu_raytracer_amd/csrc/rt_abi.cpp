@@ -196,6 +196,8 @@ struct Rccl {
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGather) gather = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    decltype(&ncclCommCount) count = nullptr;
+    decltype(&ncclCommUserRank) user_rank = nullptr;
     std::string why;  // load failure
 };
 
@@ -219,7 +221,10 @@ const Rccl& rccl() {
         r.group_end = reinterpret_cast<decltype(r.group_end)>(dlsym(h, "ncclGroupEnd"));
         r.gather = reinterpret_cast<decltype(r.gather)>(dlsym(h, "ncclGather"));
         r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
-        if (!r.init_all || !r.destroy || !r.group_start || !r.group_end || !r.gather || !r.error_string) {
+        r.count = reinterpret_cast<decltype(r.count)>(dlsym(h, "ncclCommCount"));
+        r.user_rank = reinterpret_cast<decltype(r.user_rank)>(dlsym(h, "ncclCommUserRank"));
+        if (!r.init_all || !r.destroy || !r.group_start || !r.group_end || !r.gather || !r.error_string ||
+            !r.count || !r.user_rank) {
             r.init_all = nullptr;
             r.why = "librccl.so.1 lacks ncclCommInitAll/ncclGather";
         }
@@ -514,6 +519,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.coop_lanes" && (value == 16 || value == 32 || value == 64)) c.coop_lanes = (uint32_t)value;
     else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
     else if (k == "debug.poison" && (value == 0 || value == 1)) c.poison = (uint32_t)value;
+    else if (k == "debug.lds_scribble" && (value == 0 || value == 1)) c.lds_scribble = (uint32_t)value;
     else return false;
     return true;
 }
@@ -990,6 +996,18 @@ rt_status comms_for(rt_scene* s, const std::vector<int>& devs, std::vector<ncclC
         free_comms(s->comm);
         s->comm.comms.assign(devs.size(), nullptr);
         NCCLR(R.init_all(s->comm.comms.data(), (int)devs.size(), devs.data()));
+        // every communicator must span exactly the P devices, rank r on replica r:
+        // a gather over a smaller or reordered communicator would hang or mix slabs
+        for (size_t i = 0; i < devs.size(); ++i) {
+            int cnt = -1, rk = -1;
+            NCCLR(R.count(s->comm.comms[i], &cnt));
+            NCCLR(R.user_rank(s->comm.comms[i], &rk));
+            if (cnt != (int)devs.size() || rk != (int)i) {
+                free_comms(s->comm);
+                return fail(RT_ECOMM, "ncclCommInitAll gave a communicator of " + std::to_string(cnt) + " ranks (rank " +
+                                          std::to_string(rk) + ") for " + std::to_string(devs.size()) + " devices");
+            }
+        }
         s->comm.devs = devs;
     }
     *out = &s->comm.comms;

@@ -137,7 +137,21 @@ struct TraceConfig {
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
     uint32_t poison = 0;          // debug.poison: fill every new device allocation with 0xFF bytes, so a
                                   // read of a byte nothing wrote is deterministic (and visible)
+    uint32_t lds_scribble = 0;    // debug.lds_scribble: before every kernel launch, fill the LDS of the
+                                  // CUs with a fresh pseudo-random pattern, so a kernel that reads LDS
+                                  // it did not write gives a different (wrong) result every launch
 };
+// Both debug knobs also start on from the environment (RT_DEBUG_POISON=1,
+// RT_DEBUG_LDS_SCRIBBLE=1), so a whole test suite can run under them.
+
+// Every kernel launch of the library goes through RT_KLAUNCH: with
+// debug.lds_scribble on, the scribble kernel runs first on the same stream.
+void lds_scribble_if(hipStream_t s);
+#define RT_KLAUNCH(kernel, grid, block, lds, stream, ...)                  \
+    do {                                                                   \
+        ::rt::lds_scribble_if(stream);                                     \
+        hipLaunchKernelGGL(kernel, grid, block, lds, stream, __VA_ARGS__); \
+    } while (0)
 
 // Every device buffer of the library is allocated here: hipMalloc, then
 // with debug.poison a 0xFF fill completed before the buffer is handed out.

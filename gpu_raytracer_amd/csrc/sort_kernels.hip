@@ -608,13 +608,13 @@ uint32_t sort_tiles(uint32_t n) { return n ? sdiv(n, kSortTile) : 0u; }
 
 hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_digit_hist, dim3(std::min<uint32_t>(512, sdiv(n, 256))), dim3(256), 0, s, keys, n, ghist);
+    RT_KLAUNCH(k_digit_hist, dim3(std::min<uint32_t>(512, sdiv(n, 256))), dim3(256), 0, s, keys, n, ghist);
     return hipGetLastError();
 }
 
 hipError_t launch_tile_hist0(const uint32_t* keys, uint32_t n, uint32_t* counts, hipStream_t s) {
     if (!n) return hipSuccess;
-    hipLaunchKernelGGL(k_tile_hist<0>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, keys, n, counts);
+    RT_KLAUNCH(k_tile_hist<0>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, keys, n, counts);
     return hipGetLastError();
 }
 
@@ -623,10 +623,10 @@ static void scatter_pass(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, u
                          const uint32_t* gh, uint32_t* counts, hipStream_t s) {
     const uint32_t nt = sort_tiles(n);
     if (nt <= kPrefixInKernelMaxTiles) {
-        hipLaunchKernelGGL((k_scatter<SHIFT, true>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
+        RT_KLAUNCH((k_scatter<SHIFT, true>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
     } else {
-        hipLaunchKernelGGL(k_scan_tiles, dim3(256), dim3(256), 0, s, counts, nt);
-        hipLaunchKernelGGL((k_scatter<SHIFT, false>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
+        RT_KLAUNCH(k_scan_tiles, dim3(256), dim3(256), 0, s, counts, nt);
+        RT_KLAUNCH((k_scatter<SHIFT, false>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
     }
 }
 
@@ -637,11 +637,11 @@ hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const u
     if (n <= 1) return hipSuccess;
     const uint32_t nt = sort_tiles(n);
     scatter_pass<0>(keys[0], vals[0], keys[1], vals[1], n, ghist + 0, counts[0], s);
-    hipLaunchKernelGGL(k_tile_hist<8>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[1]);
+    RT_KLAUNCH(k_tile_hist<8>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[1]);
     scatter_pass<8>(keys[1], vals[1], keys[0], vals[0], n, ghist + 256, counts[1], s);
-    hipLaunchKernelGGL(k_tile_hist<16>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], n, counts[2]);
+    RT_KLAUNCH(k_tile_hist<16>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], n, counts[2]);
     scatter_pass<16>(keys[0], vals[0], keys[1], vals[1], n, ghist + 512, counts[2], s);
-    hipLaunchKernelGGL(k_tile_hist<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[3]);
+    RT_KLAUNCH(k_tile_hist<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[3]);
     scatter_pass<24>(keys[1], vals[1], keys[0], vals[0], n, ghist + 768, counts[3], s);
     return hipGetLastError();
 }
@@ -651,9 +651,9 @@ hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, con
     if (n <= 1) return hipSuccess;
     const uint32_t nt = sort_tiles(n);
     if (n > kMsbMaxN) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart);
-    hipLaunchKernelGGL(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts);
-    hipLaunchKernelGGL(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
+    RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart);
+    RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts);
+    RT_KLAUNCH(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
                        bstart);
     return hipGetLastError();
 }
@@ -669,7 +669,7 @@ hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, con
         const uint32_t dst = src ^ 1u;
         switch (dgt) {
 #define RT_SORT_PASS(SH)                                                                                            \
-    hipLaunchKernelGGL(k_tile_hist<SH>, dim3(nt), dim3(kSortThreads), 0, s, keys[src], n, counts);                 \
+    RT_KLAUNCH(k_tile_hist<SH>, dim3(nt), dim3(kSortThreads), 0, s, keys[src], n, counts);                 \
     scatter_pass<SH>(keys[src], vals[src], keys[dst], vals[dst], n, ghist + 256 * (SH / 8), counts, s);          \
     break
             case 0: RT_SORT_PASS(0);

@@ -12,6 +12,7 @@
 #include "rt_launch.h"
 
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -1940,9 +1941,46 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks) 
 }
 
 namespace {
-TraceConfig g_trace_config;
+TraceConfig initial_config() {
+    TraceConfig c;
+    const char* p = std::getenv("RT_DEBUG_POISON");
+    const char* l = std::getenv("RT_DEBUG_LDS_SCRIBBLE");
+    c.poison = (p && std::strcmp(p, "1") == 0) ? 1u : 0u;
+    c.lds_scribble = (l && std::strcmp(l, "1") == 0) ? 1u : 0u;
+    return c;
+}
+TraceConfig g_trace_config = initial_config();
 std::mutex g_config_mu;
+std::atomic<uint32_t> g_lds_scribble{g_trace_config.lds_scribble};
+std::atomic<uint32_t> g_scribble_seed{0x9E3779B9u};
 }  // namespace
+
+// debug.lds_scribble: fill as much of every CU's 160 KB LDS as the
+// dispatcher gives us (4 blocks x 40 KB per CU requested) with a pattern
+// that changes every launch.  The dummy global store keeps the LDS writes
+// alive; it never fires (no block reads the pattern it is looking for).
+constexpr uint32_t kScribbleBytes = 40 * 1024;
+__global__ __launch_bounds__(256) void k_lds_scribble(uint32_t seed, uint32_t* __restrict__ never) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_scr[];
+    uint32_t h = pcg_hash(seed ^ (blockIdx.x * 0x85EBCA6Bu) ^ threadIdx.x);
+    for (uint32_t i = threadIdx.x; i < kScribbleBytes / 4; i += 256) {
+        h = pcg_hash(h + i);
+        s_scr[i] = h;
+    }
+    __syncthreads();
+    if (s_scr[(threadIdx.x * 7u) % (kScribbleBytes / 4)] == seed && seed == 0u) never[0] = 1u;
+}
+
+void lds_scribble_if(hipStream_t s) {
+    if (!g_lds_scribble.load(std::memory_order_relaxed)) return;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        (void)hipFuncSetAttribute((const void*)k_lds_scribble, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)kScribbleBytes);
+    });
+    const uint32_t seed = g_scribble_seed.fetch_add(0x6D2B79F5u, std::memory_order_relaxed) | 1u;
+    hipLaunchKernelGGL(k_lds_scribble, dim3(1024), dim3(256), kScribbleBytes, s, seed, (uint32_t*)nullptr);
+}
 
 TraceConfig config_snapshot() {
     std::lock_guard<std::mutex> lk(g_config_mu);
@@ -1954,6 +1992,7 @@ bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key
     TraceConfig c = g_trace_config;
     if (!f(c, key, value)) return false;
     g_trace_config = c;
+    g_lds_scribble.store(c.lds_scribble, std::memory_order_relaxed);
     return true;
 }
 
@@ -1984,15 +2023,15 @@ template <bool C, bool P, bool WI, int NT, typename... A>
 static void k_trace_go(bool buf, uint32_t warity, uint32_t grid, hipStream_t s, A... a) {
     if constexpr (WI) {
         if (warity == 8) {
-            hipLaunchKernelGGL((k_trace<C, P, true, NT, false, true, 8>), dim3(grid), dim3(NT), 0, s, a...);
+            RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 8>), dim3(grid), dim3(NT), 0, s, a...);
             return;
         }
         if (buf) {
-            hipLaunchKernelGGL((k_trace<C, P, true, NT, false, true, 4>), dim3(grid), dim3(NT), 0, s, a...);
+            RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4>), dim3(grid), dim3(NT), 0, s, a...);
             return;
         }
     }
-    hipLaunchKernelGGL((k_trace<C, P, WI, NT, false, false, 4>), dim3(grid), dim3(NT), 0, s, a...);
+    RT_KLAUNCH((k_trace<C, P, WI, NT, false, false, 4>), dim3(grid), dim3(NT), 0, s, a...);
 }
 
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tris, uint32_t n,
@@ -2039,7 +2078,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         }
         const uint32_t grid = min(blocks, (nunits + 3) / 4);
 #define RT_POOL(C, P)                                                                                               \
-    hipLaunchKernelGGL((k_trace_pool<C, P>), dim3(grid), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
+    RT_KLAUNCH((k_trace_pool<C, P>), dim3(grid), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
                        rank, nranks, tilesX, nunits, H, R, counters, work)
         if (counters) {
             if (packed) RT_POOL(true, true); else RT_POOL(true, false);
@@ -2077,7 +2116,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             if (sched->order_ready) {
                 order = sched->order;
             } else if (!can_fold) {
-                hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order,
+                RT_KLAUNCH(k_tile_order, dim3(1), dim3(1024), 0, s, sched->cost_prev, nb, sched->order,
                                    sched->cost_ema);
                 order = sched->order;
             }
@@ -2195,10 +2234,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         uint32_t* ord_ema = ord ? sched->cost_ema : nullptr;
 #define RT_COOP_G(C, P, G)                                                                                        \
     if (warity == 8)                                                                                               \
-        hipLaunchKernelGGL((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
+        RT_KLAUNCH((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
                            spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema);                               \
     else                                                                                                           \
-        hipLaunchKernelGGL((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
+        RT_KLAUNCH((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
                            spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema)
 #define RT_COOP(C, P)                  \
     if (cfg.coop_lanes == 16) {        \
@@ -2242,7 +2281,7 @@ hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, uint32_t 
     const bool wide = wnodes && n >= 2 && cfg.variant != 2;
     const uint32_t cap = stack_cap_for(cfg, warity);
 #define RT_SHADOW(C, WI, WW)                                                                                       \
-    hipLaunchKernelGGL((k_trace<C, false, WI, 256, true, false, WW>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, \
+    RT_KLAUNCH((k_trace<C, false, WI, 256, true, false, WW>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, \
                        tri_s, n, cam, w, h, spp, 0u, 1u, tilesX, H, R, counters, tris, lt)
     if (counters) {
         if (wide && warity == 8) RT_SHADOW(true, true, 8);
@@ -2282,10 +2321,10 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, uint32_t wa
     const bool small = cfg.path_wg == 64;
 #define RT_PATH(C, NT)                                                                                                 \
     if (warity == 8)                                                                                                 \
-        hipLaunchKernelGGL((k_path<C, NT, 8>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
+        RT_KLAUNCH((k_path<C, NT, 8>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
                            cam, w, h, spp, tilesX, pc, H, R, counters);                                              \
     else                                                                                                             \
-        hipLaunchKernelGGL((k_path<C, NT, 4>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
+        RT_KLAUNCH((k_path<C, NT, 4>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
                            cam, w, h, spp, tilesX, pc, H, R, counters)
     if (counters) {
         if (small) { RT_PATH(true, 64); } else { RT_PATH(true, 256); }
@@ -2357,7 +2396,7 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
         const uint32_t nb = min(batch, nt - t0);
         const uint32_t np = nb * per_tile;
 #define RT_PW_PRIMARY(C, WW)                                                                                  \
-    hipLaunchKernelGGL((k_pw_primary<C, WW>), dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h, spp, \
+    RT_KLAUNCH((k_pw_primary<C, WW>), dim3(nb), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, cam, w, h, spp, \
                        tilesX, t0, pb.f, pb.u, pb.cap, H, counters)
         if (counters) {
             if (w8) RT_PW_PRIMARY(true, 8); else RT_PW_PRIMARY(true, 4);
@@ -2367,7 +2406,7 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
 #undef RT_PW_PRIMARY
         for (uint32_t depth = 0; depth <= max_depth + 1; ++depth) {
             if ((e = hipMemsetAsync(pb.qcount, 0, 4, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_pw_shade, dim3((np + 1023) / 1024), dim3(1024), 0, s, pb.f, pb.u, pb.cap, np, depth,
+            RT_KLAUNCH(k_pw_shade, dim3((np + 1023) / 1024), dim3(1024), 0, s, pb.f, pb.u, pb.cap, np, depth,
                                pc, tris, params, pb.rays, pb.keys[0], pb.vals[0], pb.qcount);
             if (depth == max_depth + 1) break;  // only the last shadow results were left to apply
             uint32_t count = 0, grid = 0;
@@ -2393,7 +2432,7 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
                 grid = (2 * np + 255) / 256;
             }
 #define RT_PW_TRACE(C, WW)                                                                                     \
-    hipLaunchKernelGGL((k_pw_trace<C, WW>), dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays, order, \
+    RT_KLAUNCH((k_pw_trace<C, WW>), dim3(grid), dim3(256), 0, s, nodes, wn, wcap, tri_s, n, pb.rays, order, \
                        count, count_dev, pb.f, pb.u, pb.cap, counters)
             if (counters) {
                 if (w8) RT_PW_TRACE(true, 8); else RT_PW_TRACE(true, 4);
@@ -2403,7 +2442,7 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
 #undef RT_PW_TRACE
         }
         if (rgba)
-            hipLaunchKernelGGL(k_pw_finish, dim3(nb), dim3(256), 0, s, pb.f, pb.cap, w, h, spp, tilesX, t0,
+            RT_KLAUNCH(k_pw_finish, dim3(nb), dim3(256), 0, s, pb.f, pb.cap, w, h, spp, tilesX, t0,
                                reinterpret_cast<uint32_t*>(rgba));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
@@ -2414,7 +2453,7 @@ hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w,
                          void* img, hipStream_t s) {
     if (!tiles_per_slab || !nranks) return hipSuccess;
     const uint32_t tilesX = (w + 15) / 16, nt = tilesX * ((h + 15) / 16);
-    hipLaunchKernelGGL(k_unpack, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const uint32_t*)slabs, tiles_per_slab,
+    RT_KLAUNCH(k_unpack, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const uint32_t*)slabs, tiles_per_slab,
                        w, h, nranks, tilesX, nt, (uint32_t*)img);
     return hipGetLastError();
 }
@@ -2423,7 +2462,7 @@ hipError_t launch_unpack_hits(const void* slabs, uint32_t tiles_per_slab, uint32
                               uint32_t nranks, void* hits, hipStream_t s) {
     if (!tiles_per_slab || !nranks) return hipSuccess;
     const uint32_t tilesX = (w + 15) / 16, nt = tilesX * ((h + 15) / 16);
-    hipLaunchKernelGGL(k_unpack_hits, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const float4*)slabs,
+    RT_KLAUNCH(k_unpack_hits, dim3(tiles_per_slab * nranks), dim3(256), 0, s, (const float4*)slabs,
                        tiles_per_slab, w, h, spp, nranks, tilesX, nt, (float4*)hits);
     return hipGetLastError();
 }
@@ -2431,13 +2470,13 @@ hipError_t launch_unpack_hits(const void* slabs, uint32_t tiles_per_slab, uint32
 hipError_t launch_intersect(uint32_t count, const float* o, const float* d, const float* tri, const float* tb,
                             uint32_t* hit, float* tuv, hipStream_t s) {
     if (!count) return hipSuccess;
-    hipLaunchKernelGGL(k_intersect, dim3((count + 255) / 256), dim3(256), 0, s, count, o, d, tri, tb, hit, tuv);
+    RT_KLAUNCH(k_intersect, dim3((count + 255) / 256), dim3(256), 0, s, count, o, d, tri, tb, hit, tuv);
     return hipGetLastError();
 }
 
 hipError_t launch_minmax(uint32_t count, const float* a, const float* b, float* out, hipStream_t s) {
     if (!count) return hipSuccess;
-    hipLaunchKernelGGL(k_minmax, dim3((count + 255) / 256), dim3(256), 0, s, count, a, b, out);
+    RT_KLAUNCH(k_minmax, dim3((count + 255) / 256), dim3(256), 0, s, count, a, b, out);
     return hipGetLastError();
 }
 

@@ -150,18 +150,26 @@ class LibStages:
 class Exchange:
     """The collectives the distributed build needs, over the default process
     group.  stage=True (gloo with device buffers) moves the bytes through
-    host memory."""
+    host memory.  Under 'nccl' (RCCL) every collective needs device tensors:
+    the small host arrays (boxes, histograms, counts) go through `device`
+    (default: the current GPU)."""
 
-    def __init__(self, stage: bool = False):
+    def __init__(self, stage: bool = False, device=None):
         self.stage = stage
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.bytes_in = 0  # bytes this rank received
+        self.device = None
+        if dist.get_backend() == "nccl":
+            self.device = torch.device(device) if device is not None else \
+                torch.device("cuda", torch.cuda.current_device())
 
     def gather_small(self, arr) -> _np.ndarray:
         a = torch.from_numpy(_np.ascontiguousarray(arr).copy())
+        if self.device is not None:
+            a = a.to(self.device)
         out = [torch.empty_like(a) for _ in range(self.world)]
         dist.all_gather(out, a)
-        return _np.stack([o.numpy() for o in out])
+        return _np.stack([o.cpu().numpy() for o in out])
 
     def alltoallv(self, send: torch.Tensor, scounts, recv: torch.Tensor, rcounts):
         self.bytes_in += 4 * (sum(rcounts) - rcounts[self.rank])

@@ -340,6 +340,10 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * "debug.poison" 0/1: every device buffer the library allocates from then on
  * is filled with 0xFF bytes before first use, so reading a byte no kernel
  * wrote gives the same (wrong) value every run instead of allocator luck.
+ * "debug.lds_scribble" 0/1: before every kernel launch a scribble kernel
+ * fills the CUs' LDS with a pattern that changes every launch, so a kernel
+ * reading LDS it did not write differs run to run.  Both debug knobs can
+ * start on from the environment: RT_DEBUG_POISON=1, RT_DEBUG_LDS_SCRIBBLE=1.
  * Results are bit-identical for every setting. */
 rt_status rt_config_set(const char* key, int64_t value);
 

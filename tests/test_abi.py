@@ -250,6 +250,7 @@ CONFIG_KEYS = {
     "trace.coop_lanes": ([16, 32, 64], [0, 8, 48, 128], 32),
     "trace.coop_max": ([1, 64, 65536, 1 << 24], [0, -1, (1 << 24) + 1], 65536),
     "debug.poison": ([0, 1], [2, -1], 0),
+    "debug.lds_scribble": ([0, 1], [2, -1], 0),
 }
 
 

@@ -2,7 +2,11 @@
 CPU oracle (SURVEY.md §8(c)): configs[1] bunny-class 1920x1080x1 every hit;
 configs[3] Sponza-class 1920x1080x16 sharded over 8 ranks' tiles and
 unpacked, every pixel and hit; configs[4] 10M soup 3840x2160x4 sharded over 8
-ranks == the full-frame render, and every 97th image row == the oracle.
+ranks == the full-frame render, and every 33rd image row (66 rows) == the
+oracle.  Both 8-rank configs also run through rt_render(ngpus=8) with
+render.emulate for two successive frames: each rank keeps its own tile-order
+state, so the second frame runs the per-rank longest-first order and the
+heavy-ray queue's resume exactly as a multi-GPU frame does.
 (The §9.9 substitutes stand in for the Stanford bunny and Crytek Sponza: no
 asset files exist offline.)"""
 import numpy as np
@@ -68,25 +72,46 @@ def test_config3_sponza_1080p_16spp_8_ranks(R, oracle):
         s.build()
         img = _tiled_image(R, s, cam, w, h, spp, 8)
         hits, _, _ = s.render(cam, w, h, spp, rgba=False)
-    assert np.array_equal(img, er)
-    assert np.array_equal(hits["prim"], eh["prim"])
-    assert np.array_equal(bits(hits["t"]), bits(eh["t"]))
+        assert np.array_equal(img, er)
+        assert np.array_equal(hits["prim"], eh["prim"])
+        assert np.array_equal(bits(hits["t"]), bits(eh["t"]))
+        R.config_set("render.emulate", 1)
+        try:
+            for frame in range(2):
+                h8, i8, _ = s.render(cam, w, h, spp, ngpus=8)
+                assert np.array_equal(i8, er), frame
+                assert np.array_equal(h8["prim"], eh["prim"]), frame
+                for f in ("t", "u", "v"):
+                    assert np.array_equal(bits(h8[f]), bits(eh[f])), (frame, f)
+        finally:
+            R.config_set("render.emulate", 0)
 
 
 def test_config4_10m_4k_4spp_8_ranks(R, oracle):
     from gpu_raytracer_amd.scenes import SOUP_VIEW as V
-    w, h, spp, step = 3840, 2160, 4, 97
+    w, h, spp, step = 3840, 2160, 4, 33
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    frames8 = []
     with R.Scene.generate_soup(10_000_000, 1) as s:
         s.build()
         tris = s.tris()
         img = _tiled_image(R, s, cam, w, h, spp, 8)
         hits, full, _ = s.render(cam, w, h, spp)
+        R.config_set("render.emulate", 1)
+        try:
+            for frame in range(2):
+                frames8.append(s.render(cam, w, h, spp, ngpus=8)[:2])
+        finally:
+            R.config_set("render.emulate", 0)
     assert np.array_equal(img, full)
+    for h8, i8 in frames8:
+        assert np.array_equal(i8, full)
+        assert np.array_equal(h8.view(np.uint32), hits.view(np.uint32))
     exp = oracle.build(tris)
     ocam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp, row0=3, row_step=step)
     rows = np.arange(3, h, step)
+    assert len(rows) >= 64
     g = hits.reshape(h, w * spp)[rows]
     e = eh.reshape(h, w * spp)[rows]
     assert np.array_equal(g["prim"], e["prim"])
