@@ -390,6 +390,25 @@ __device__ __forceinline__ uint4 bload_u4(__amdgpu_buffer_rsrc_t r, uint32_t off
 __device__ __forceinline__ float4 bload_f4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
 }
+__device__ __forceinline__ uint2 bload_u2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+// the third word of a triangle record {v2.z, prim, esc, 0}: a step needs its
+// first two only (8 B, two VGPRs in flight instead of four)
+__device__ __forceinline__ float4 bload_tri2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const uint2 v = bload_u2(r, off);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), 0.0f, 0.0f);
+}
+// record word k of a W-ary record; a 4-ary record's last word {ref2, ref3, 0, 0}
+// is loaded as 8 B
+template <int W>
+__device__ __forceinline__ uint4 bload_rec(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t k) {
+    if (W == 4 && k == WideFmt<4>::words - 1) {
+        const uint2 v = bload_u2(r, off);
+        return make_uint4(v.x, v.y, 0u, 0u);
+    }
+    return bload_u4(r, off);
+}
 
 template <bool COUNT, int NT, bool ANY = false, bool MTF = false, bool BUF = false, int W = 4>
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
@@ -417,9 +436,9 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     float4 T0, T1, T2;
     if (BUF) {
         const uint32_t wo = node ? R.cur * WideFmt<W>::bytes : M->wbytes;
-        T0 = bload_f4(M->tr, to); T1 = bload_f4(M->tr, to + 16); T2 = bload_f4(M->tr, to + 32);
+        T0 = bload_f4(M->tr, to); T1 = bload_f4(M->tr, to + 16); T2 = bload_tri2(M->tr, to + 32);
 #pragma unroll
-        for (uint32_t k = 0; k < NW; ++k) wr[k] = bload_u4(M->wr, wo + 16 * k);
+        for (uint32_t k = 0; k < NW; ++k) wr[k] = bload_rec<W>(M->wr, wo + 16 * k, k);
     } else {
         if (leaf) { T0 = tp[0]; T1 = tp[1]; T2 = tp[2]; }
         if (node) {
@@ -440,7 +459,7 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
             if (intersect_tri(o, R.d, tv, R.tb, t, u, v)) {
                 __asm__ volatile("" ::: "memory");  // reload below instead of keeping tv live
                 const float4 U0 = BUF ? bload_f4(M->tr, to) : tp[0], U1 = BUF ? bload_f4(M->tr, to + 16) : tp[1],
-                             U2 = BUF ? bload_f4(M->tr, to + 32) : tp[2];
+                             U2 = BUF ? bload_tri2(M->tr, to + 32) : tp[2];
                 const float uv[9] = {U0.x, U0.y, U0.z, U0.w, U1.x, U1.y, U1.z, U1.w, U2.x};
                 float lo[3], hi[3], tn;
                 tri_bounds(uv, lo, hi);
@@ -819,7 +838,11 @@ constexpr uint32_t kFoldPerThread = 32;  // 256 threads: up to 8192 tiles (a 108
 #define RT_ORDER_FOLD 1  // 0: k_tile_order at the head of every frame (A/B)
 #endif
 
-template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4>
+// CQ: compiled with the heavy-ray queue (trace.coop_cap*).  Without it the
+// queue's state (entry writes, the deferring lane's stack copy) drops out of
+// the loop: the full-frame primary kernel goes from 89 to 80 VGPRs, i.e. from
+// 5 to 6 waves per SIMD.
+template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4, bool CQ = true>
 __global__ __launch_bounds__(NT, (SHADOW && WA == 4) ? RT_KSHADOW_WAVES : (PACKED && WA == 4) ? RT_KTILES_WAVES : RT_KTRACE_WAVES)
 void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
@@ -873,7 +896,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     const SceneBox sb = scene_box(nodes);
     // uniform: with the queue off (full frames by default) the per-step cap
     // test, and its kernel-argument reload, drop out of the loop
-    const bool coop_on = !SHADOW && coop_cap != 0;
+    const bool coop_on = CQ && !SHADOW && coop_cap != 0;
     uint32_t cn = 0, ct = 0, steps = 0;
     uint32_t qslot = 0, dsamp = RT_SENT;  // heavy-ray queue entry, deferred sample
     const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -2020,14 +2043,16 @@ static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity) {
 // k_trace with the record arity and load form chosen at run time (the
 // binary kernel, WI = false, has one form)
 template <bool C, bool P, bool WI, int NT, typename... A>
-static void k_trace_go(bool buf, uint32_t warity, uint32_t grid, hipStream_t s, A... a) {
+static void k_trace_go(bool buf, uint32_t warity, bool cq, uint32_t grid, hipStream_t s, A... a) {
     if constexpr (WI) {
         if (warity == 8) {
-            RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 8>), dim3(grid), dim3(NT), 0, s, a...);
+            if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 8, true>), dim3(grid), dim3(NT), 0, s, a...);
+            else RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 8, false>), dim3(grid), dim3(NT), 0, s, a...);
             return;
         }
         if (buf) {
-            RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4>), dim3(grid), dim3(NT), 0, s, a...);
+            if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true>), dim3(grid), dim3(NT), 0, s, a...);
+            else RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, false>), dim3(grid), dim3(NT), 0, s, a...);
             return;
         }
     }
@@ -2174,7 +2199,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
-    k_trace_go<C, P, WI, NT>(buf, warity, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, wnodes, cap, tris, n,     \
+    k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, wnodes, cap, tris, n,     \
                              cam, w, h, spp, rank, nranks, tilesX, H, R, counters, (const float*)nullptr, Light{},      \
                              order, cost_out, px_prev, px_cost, coop_cap, cq, fold)
 #define RT_TRACE(C, P, WI) \

@@ -9,7 +9,7 @@
 #   bench:<tag>[:<bench.py args, ',' for ' '>]  -> gpurun_out/bench_<tag>.json/.err
 #   profile:<tag>:<config>:<steps>   kernel trace + FETCH/WRITE/SQ PMC passes of the
 #                                    timed bench steps -> gpurun_out/prof_<tag>/
-#   py:<tag>:<script>[:<args, ',' for ' '>]  a tools/ script -> gpurun_out/<tag>.log
+#   py:<tag>:<script>[:<args, "~" for " ">]  a tools/ script -> gpurun_out/<tag>.log
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -49,7 +49,7 @@ run_profile() {  # tag config steps
 }
 
 run_py() {  # tag script args
-    local tag=$1 script=$2 args=${3//,/ }
+    local tag=$1 script=$2 args=${3//\~/ }
     echo "[gpu_run] py $tag: $script $args"
     timeout -k 10 900 python -u $script $args > gpurun_out/$tag.log 2>&1 || { tail -40 gpurun_out/$tag.log; return 1; }
     tail -5 gpurun_out/$tag.log
