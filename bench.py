@@ -37,8 +37,10 @@ roofline: the trace launch (k_trace; its last block sorts the next frame's tile 
   event-timed duration, against the 8.0 TB/s HBM peak (frac) and the
   aggregate L2 bandwidth (l2_frac); beside it the PMC-measured HBM bytes
   (hbm_frac) and VALU issue (issue_frac) of the same kernel from the committed
-  profile (profiles/pmc_summary.json, tools/profile_r02.sh); `limiter` names
-  the largest fraction.  The SURVEY.md §8(d) binary-traversal byte model
+  profile (profiles/pmc_summary.json, tools/gpu_run.sh profile); `limiter`
+  names the largest MEASURED fraction (HBM traffic, L2 requests, VALU issue).
+  other_configs.config5 (soup-10M, the config whose trace structures exceed
+  the MALL) carries the same block from its own profile entry.  The SURVEY.md §8(d) binary-traversal byte model
   is kept as algo_bytes_binary_model (it charges node visits the wide kernel
   does not make, so its fraction is not a roofline of this kernel).
 cpu_baseline (rank 0, N=1 only): the CPU oracle (oracle/, a port of the same
@@ -279,7 +281,34 @@ def make_scene(R, S, cfg):
     return R.Scene.from_soup(S.tris_for(cfg.scene))
 
 
-def other_config(R, S, key, torch, dev, steps=8, warmup=2):
+def roofline_of(kernel_bytes, trace_ms, pmc):
+    """The trace kernel's roofline block: `frac` = the bytes it requests over
+    its event-timed launch against the HBM peak (the contract's memory
+    roofline); `hbm_frac` / `issue_frac` = the MEASURED HBM traffic and VALU
+    issue (PMC, from the committed profile of the same command); `limiter` =
+    the largest of the measured fractions only (HBM traffic, L2 requests,
+    VALU issue) -- the requested-bytes fraction is a model, not a resource."""
+    achieved = kernel_bytes / (trace_ms * 1e-3) / 1e9
+    hbm_frac = issue_frac = traffic = None
+    if pmc:
+        traffic = pmc.get("hbm_bytes_per_launch")
+        if traffic:
+            hbm_frac = traffic / (trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+        if pmc.get("valu_insts_per_launch") and pmc.get("cycles_per_launch"):
+            issue_frac = pmc["valu_insts_per_launch"] / (VALU_ISSUE_PER_CYCLE * pmc["cycles_per_launch"])
+    l2_frac = achieved / L2_PEAK_GBS
+    cands = {"hbm_measured": hbm_frac, "l2_requests": l2_frac, "valu_issue": issue_frac}
+    limiter = max((k for k in cands if cands[k] is not None), key=lambda k: cands[k])
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "bytes_per_launch": kernel_bytes,
+            "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
+            "l2_frac": round(l2_frac, 4), "l2_peak": L2_PEAK_GBS,
+            "issue_frac": round(issue_frac, 4) if issue_frac is not None else None,
+            "limiter": limiter,
+            "pmc_trace_kernel_us": pmc.get("trace_kernel_avg_us") if pmc else None}
+
+
+def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None):
     """One N=1 line for another BASELINE config (untimed by the step
     contract): build + full-frame trace, static camera, with its row-major
     (cold) time and the kernel's own byte rate."""
@@ -307,7 +336,10 @@ def other_config(R, S, key, torch, dev, steps=8, warmup=2):
     kb = 64.0 * float(wk[0]) + 48.0 * float(wk[1]) + 16.0 * rays + 4.0 * w * h
     tr, bd = float(np.mean(t)), float(np.mean(b))
     scene.close()
+    pmc = load_pmc(pmc_json, cfg.name, 1) if pmc_json else None
     return {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{key - 1}])", "n_tris": cfg.n,
+            "roofline": roofline_of(kb, tr, pmc),
+            "pmc_source": (os.path.relpath(pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]") if pmc else None,
             "n_gpus": 1, "value": round(rays / (tr * 1e-3) / 1e6, 2), "unit": "Mrays/s",
             "value_cold": round(rays / (cold * 1e-3) / 1e6, 2), "trace_ms": round(tr, 4),
             "trace_ms_row_major": round(cold, 4), "build_ms": round(bd, 4),
@@ -547,21 +579,8 @@ def main():
     out = None
     if rank == 0:
         value = rays / (frame_ms * 1e-3) / 1e6
-        achieved = kernel_bytes / (rank_trace_ms * 1e-3) / 1e9
-        frac = achieved / HBM_PEAK_GBS
         pmc = load_pmc(args.pmc_json, cfg.name, world)
-        hbm_frac = issue_frac = traffic = None
-        if pmc:
-            traffic = pmc.get("hbm_bytes_per_launch")
-            if traffic:
-                hbm_frac = traffic / (rank_trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-            if pmc.get("valu_insts_per_launch") and pmc.get("cycles_per_launch"):
-                issue_frac = pmc["valu_insts_per_launch"] / (VALU_ISSUE_PER_CYCLE * pmc["cycles_per_launch"])
-        l2_frac = achieved / L2_PEAK_GBS
-        # which resource is closest to its ceiling (the contract's `bound` stays
-        # the memory roofline this integer/branchy path is priced against)
-        cands = {"hbm_requested": frac, "hbm_measured": hbm_frac, "l2_requests": l2_frac, "valu_issue": issue_frac}
-        limiter = max((k for k in cands if cands[k] is not None), key=lambda k: cands[k])
+        roof = roofline_of(kernel_bytes, rank_trace_ms, pmc)
         build_gbs = BUILD_BYTES_PER_PRIM * n_tris / (build_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC,
@@ -604,25 +623,19 @@ def main():
                                      "total_with_stage_events": round(stage_total_ms, 4)},
             "trace_counters_rank0_static": {"nodes_fetched": int(cnt_static[0]), "tris_tested": int(cnt_static[1]),
                                             "rays": rank_rays},
-            "roofline": {"bound": "hbm", "kernel": "trace launch: k_trace<wide> (+ k_tile_order when not folded)",
-                         "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(frac, 4), "traffic": traffic,
-                         "bytes_per_launch": kernel_bytes,
-                         "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
-                         "l2_frac": round(l2_frac, 4), "l2_peak": L2_PEAK_GBS,
-                         "issue_frac": round(issue_frac, 4) if issue_frac is not None else None,
-                         "limiter": limiter,
-                         "pmc_source": (os.path.relpath(args.pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]")
-                         if pmc else None,
-                         "algo_bytes_binary_model": algo_bytes,
-                         "note": "achieved = bytes the wide kernel requests per launch (64 B per K7w record + "
-                                 "48 B per triangle record, its own counters, + 16 B hit + 4 B RGBA per ray) over "
-                                 "the event-timed launch, priced against HBM (frac) and the aggregate L2 (l2_frac: "
-                                 "every request passes L2); traffic = PMC HBM bytes per launch (2*FETCH_SIZE + "
-                                 "WRITE_SIZE, gfx950 correction), hbm_frac = traffic over the same time; "
-                                 "issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 x GRBM_GUI_ACTIVE/8); limiter = "
-                                 "the largest fraction; algo_bytes_binary_model = SURVEY.md §8(d) 32/node + 36/tri "
-                                 "+ 16/ray over the §9.7 binary traversal (not what this kernel fetches)"},
+            "roofline": dict(roof, kernel="trace launch: k_trace<wide> (+ k_tile_order when not folded)",
+                             pmc_source=(os.path.relpath(args.pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]")
+                             if pmc else None,
+                             algo_bytes_binary_model=algo_bytes,
+                             note="achieved = bytes the wide kernel requests per launch (64 B per K7w record + "
+                                  "48 B per triangle record, its own counters, + 16 B hit + 4 B RGBA per ray) over "
+                                  "the event-timed launch, priced against HBM (frac) and the aggregate L2 (l2_frac: "
+                                  "every request passes L2); traffic = PMC HBM bytes per launch (2*FETCH_SIZE + "
+                                  "WRITE_SIZE, gfx950 correction), hbm_frac = traffic over the same time; "
+                                  "issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 x GRBM_GUI_ACTIVE/8); limiter = "
+                                  "the largest MEASURED fraction (hbm_measured, l2_requests, valu_issue); "
+                                  "algo_bytes_binary_model = SURVEY.md §8(d) 32/node + 36/tri + 16/ray over the "
+                                  "§9.7 binary traversal (not what this kernel fetches)"),
             "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM,
@@ -660,7 +673,7 @@ def main():
             if key == args.config:
                 continue
             try:
-                out["other_configs"][f"config{key}"] = other_config(R, S, key, torch, dev)
+                out["other_configs"][f"config{key}"] = other_config(R, S, key, torch, dev, pmc_json=args.pmc_json)
             except Exception as exc:  # a side measurement: never lose the headline line over it
                 out["other_configs"][f"config{key}"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
     if rank == 0:
