@@ -91,6 +91,7 @@ def lib():
         L.orc_shade.argtypes = [P, u32, u32, u32, P]
         L.orc_render_shadow.argtypes = [P, u32, P, C.POINTER(Camera), u32, u32, u32, P, f32, P, P, P, i32]
         L.orc_render_path.argtypes = [P, u32, P, C.POINTER(Camera), u32, u32, u32, P, f32, u32, P, P, P, i32]
+        L.orc_debug_fail_spawn.argtypes = [i32]
         _lib = L
     return _lib
 

@@ -376,6 +376,22 @@ static void trace_ray(const orc_node* nodes, uint32_t n, const float* tris, cons
     trace_ray_t(nodes, n, tris, o, d, INFINITY, 0, hit, cn, ct);
 }
 
+/* Worker threads.  A thread that cannot be created (EAGAIN under a task
+ * limit: the GPU box caps a job's processes and threads) must not lose its
+ * share: the trace's shared cursor is drained by the calling thread, and a
+ * path job whose thread did not start runs on the caller.  (Until r03 the
+ * return value was ignored and glibc's pthread_join of the never-set id
+ * returns ESRCH without waiting: had every creation failed, the expected
+ * hits would have stayed at their "miss" initial values -- a wrong oracle,
+ * not a wrong GPU result.)  orc_debug_fail_spawn(1) makes every creation
+ * fail, for the CPU test of that path. */
+static atomic_int g_fail_spawn;
+void orc_debug_fail_spawn(int on) { atomic_store(&g_fail_spawn, on); }
+static unsigned char spawn(pthread_t* t, void* (*fn)(void*), void* arg) {
+    if (atomic_load(&g_fail_spawn)) return 0;
+    return pthread_create(t, NULL, fn, arg) == 0;
+}
+
 typedef struct {
     const orc_node* nodes; uint32_t n; const float* tris; const orc_camera* cam;
     uint32_t w, h, spp, row0, row_step; orc_hit* hits;
@@ -427,15 +443,18 @@ void orc_trace(const orc_node* nodes, uint32_t n, const float* tris, const orc_c
     if (row_step < 1) row_step = 1;
     trace_job* jobs = (trace_job*)calloc((size_t)nthreads, sizeof(trace_job));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    unsigned char* live = (unsigned char*)calloc((size_t)nthreads, 1);
     atomic_uint_fast64_t next;
     atomic_init(&next, 0);
     for (int t = 0; t < nthreads; ++t) {
         trace_job jb = {nodes, n, tris, cam, w, h, spp, row0, row_step, hits, &next, 0, 0};
         jobs[t] = jb;
-        if (nthreads > 1) pthread_create(&th[t], NULL, trace_worker, &jobs[t]);
     }
-    if (nthreads == 1) trace_worker(&jobs[0]);
-    else for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    for (int t = 1; t < nthreads; ++t) live[t] = spawn(&th[t], trace_worker, &jobs[t]);
+    trace_worker(&jobs[0]);  /* the caller is worker 0: the shared cursor is drained even if no thread starts */
+    for (int t = 1; t < nthreads; ++t)
+        if (live[t]) pthread_join(th[t], NULL);
+    free(live);
     if (counters) {
         counters[0] = counters[1] = 0;
         for (int t = 0; t < nthreads; ++t) { counters[0] += jobs[t].cn; counters[1] += jobs[t].ct; }
@@ -663,13 +682,18 @@ void orc_render_path(const orc_node* nodes, uint32_t n, const float* tris, const
     if (nthreads < 1) nthreads = 1;
     path_job* jobs = (path_job*)calloc((size_t)nthreads, sizeof(path_job));
     pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    unsigned char* live = (unsigned char*)calloc((size_t)nthreads, 1);
     for (int t = 0; t < nthreads; ++t) {
         path_job jb = {nodes, n, tris, cam, w, h, spp, max_depth, light, sky, hits, rgba, t, nthreads, {0, 0, 0}};
         jobs[t] = jb;
-        if (nthreads > 1) pthread_create(&th[t], NULL, path_worker, &jobs[t]);
     }
-    if (nthreads == 1) path_worker(&jobs[0]);
-    else for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+    for (int t = 1; t < nthreads; ++t) live[t] = spawn(&th[t], path_worker, &jobs[t]);
+    path_worker(&jobs[0]);
+    for (int t = 1; t < nthreads; ++t) {  /* a thread that did not start: its rows on the caller */
+        if (live[t]) pthread_join(th[t], NULL);
+        else path_worker(&jobs[t]);
+    }
+    free(live);
     if (counters) {
         counters[0] = counters[1] = counters[2] = 0;
         for (int t = 0; t < nthreads; ++t)

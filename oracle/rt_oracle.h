@@ -91,7 +91,8 @@ int orc_intersect_tri(const float o[3], const float d[3], const float* tri,
 /* §9.7 trace: hits[(y*w+x)*spp+s]; counters (nullable): [0]=nodes fetched,
  * [1]=tris tested, summed over all traced rays.  Rows traced: y = row0,
  * row0+row_step, ... (row_step>=1) -- lets the CPU baseline time a bounded
- * sample.  nthreads>=1 splits rows interleaved across POSIX threads. */
+ * sample.  nthreads>=1: 64-pixel row segments dealt to the calling thread
+ * and nthreads-1 POSIX threads from a shared cursor. */
 void orc_trace(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* cam,
                uint32_t w, uint32_t h, uint32_t spp, uint32_t row0, uint32_t row_step,
                orc_hit* hits, uint64_t counters[2], int nthreads);
@@ -116,6 +117,11 @@ void orc_render_shadow(const orc_node* nodes, uint32_t n, const float* tris, con
 void orc_render_path(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* cam,
                      uint32_t w, uint32_t h, uint32_t spp, const float light[3], float sky, uint32_t max_depth,
                      orc_hit* hits, uint8_t* rgba, uint64_t counters[3], int nthreads);
+
+/* Test hook: on != 0 makes every worker-thread creation fail, so the CPU
+ * suite checks that the traces still cover every pixel on the calling
+ * thread (tests/test_oracle.py). */
+void orc_debug_fail_spawn(int on);
 
 #ifdef __cplusplus
 }

@@ -49,3 +49,41 @@ def bits(a):
     if a.dtype == np.float32:
         return a.view(np.uint32)
     return a
+
+
+# Task accounting (DESIGN.md "The r02 8-ary wrong-hit record"): the oracle's
+# traces start up to 15 worker threads per call, and a GPU box caps a job's
+# tasks (threads count).  The session reports the most threads this process
+# held after any test and the cgroup's task limit, so a run shows how close
+# the suite came to the cap.
+_max_threads = [0, ""]
+
+
+def _threads():
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("Threads:"):
+                    return int(line.split()[1])
+    except OSError:
+        pass
+    return 0
+
+
+def pytest_runtest_teardown(item):
+    t = _threads()
+    if t > _max_threads[0]:
+        _max_threads[0], _max_threads[1] = t, item.nodeid
+
+
+def pytest_terminal_summary(terminalreporter):
+    lim = "unknown"
+    for p in ("/sys/fs/cgroup/pids.max", "/sys/fs/cgroup/pids/pids.max"):
+        try:
+            with open(p) as f:
+                lim = f.read().strip()
+            break
+        except OSError:
+            pass
+    terminalreporter.write_line(f"[tasks] most threads in this process after a test: {_max_threads[0]} "
+                                f"({_max_threads[1]}); cgroup pids.max: {lim}")

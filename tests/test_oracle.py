@@ -189,6 +189,32 @@ def test_trace_row_sampling_and_threads(oracle):
     assert c_sub[0] < c_full[0]
 
 
+def test_trace_survives_failed_thread_creation(oracle):
+    """A worker thread that cannot be created (EAGAIN under the GPU box's task
+    cap) must not leave pixels at the initial "miss": the calling thread
+    drains the trace's shared cursor and runs a path job's rows itself.  Before
+    r03 the creation status was ignored and glibc's pthread_join of the unset
+    id returns ESRCH at once -- with every creation failing the expected hits
+    were all misses (DESIGN.md "The r02 8-ary wrong-hit record")."""
+    from gpu_raytracer_amd import scenes as S
+    tris = np.ascontiguousarray(S.cornell_tris(), np.float32).reshape(-1, 9)
+    V, light = S.CORNELL_VIEW, S.LIGHTS["cornell"]
+    cam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, 64, 64)
+    b = oracle.build(tris)
+    ref, cref = oracle.trace(b["nodes"], tris, cam, 64, 64, 1, nthreads=1)
+    _, pref, pcref = oracle.render_path(b["nodes"], tris, cam, 32, 32, 2, light, 0.2, 2, nthreads=1)
+    lib = oracle.lib()
+    lib.orc_debug_fail_spawn(1)
+    try:
+        got, cgot = oracle.trace(b["nodes"], tris, cam, 64, 64, 1, nthreads=8)
+        _, pgot, pcgot = oracle.render_path(b["nodes"], tris, cam, 32, 32, 2, light, 0.2, 2, nthreads=8)
+    finally:
+        lib.orc_debug_fail_spawn(0)
+    assert (ref["prim"] != 0xFFFFFFFF).sum() > 1000
+    assert np.array_equal(got.view(np.uint32), ref.view(np.uint32)) and np.array_equal(cgot, cref)
+    assert np.array_equal(pgot, pref) and np.array_equal(pcgot, pcref)
+
+
 def _secondary_scenes(oracle):
     from gpu_raytracer_amd import scenes as S
     return [(np.ascontiguousarray(S.cornell_tris(), np.float32).reshape(-1, 9), S.CORNELL_VIEW, S.LIGHTS["cornell"], 24),
