@@ -86,7 +86,7 @@ def parse():
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     ap.add_argument("--dump", default="", help="write the rank-0 image as PPM")
     ap.add_argument("--only-timed", action="store_true",
-                    help="warm-up + timed steps only (the PMC passes of tools/profile_r02.sh)")
+                    help="warm-up + timed steps only (the PMC passes of tools/gpu_run.sh profile)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI) for the benchmark; gloo only to rehearse N>1 on one GPU")
     ap.add_argument("--extras", action="store_true",

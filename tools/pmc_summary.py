@@ -1,4 +1,4 @@
-"""Summarise one tools/profile_r02.sh run of `bench.py --only-timed` into
+"""Summarise one tools/gpu_run.sh profile run of `bench.py --only-timed` into
 profiles/: a markdown kernel table (rocprof kernel trace + PMC passes) and the
 per-launch entry bench.py's roofline reads (profiles/pmc_summary.json).
 
