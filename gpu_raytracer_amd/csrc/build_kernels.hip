@@ -48,31 +48,39 @@ __device__ __forceinline__ float wave_max(float v) {
     return v;
 }
 
-// 8 consecutive AoS triangles (tris [8g, 8g+8)): 18 independent 16-B loads,
-// no LDS, no barrier.  A full group is 288 B, 16-B aligned.  Tail groups use
-// predicated scalar loads with compile-time register indices (no scratch).
+// 8 triangles per thread, lane-interleaved: lane l of a wave whose span
+// starts at triangle `base` takes triangles base + 64q + l (q < 8), each as
+// three 12-B vertex loads.  Lanes are 36 B apart, so one wave-instruction
+// covers 2304 contiguous bytes (18 lines) and the wave's 24 instructions read
+// its 18-KB span with no LDS.  The r02 form (8 consecutive triangles per
+// thread as 18 x 16-B loads) put lanes 288 B apart -- 64 lines per
+// instruction -- and streamed at 3.8 TB/s against 6.1 TB/s for this one
+// (tools/bench_stream.hip, profiles/bench_stream_r03.log).
 // All index math is 32-bit (n <= 2^30): a 64-bit min() of the tail size was
 // miscompiled by hipcc 7.2 (v_cmp_*_u64 feeding an s_cselect on a stale SCC).
 constexpr uint32_t kTrisPerThread = 8;
+struct Vtx { float x, y, z; };
 
-__device__ __forceinline__ uint32_t load_tri8(const float* __restrict__ tris, uint32_t n, uint32_t g, float (&t)[72]) {
-    const uint32_t first = g * kTrisPerThread;
-    if (first + kTrisPerThread <= n) {
-        const float4* p = reinterpret_cast<const float4*>(tris + (uint64_t)first * 9);
-        float4 v[18];
+// t[q] = triangle base + 64q + lane (zeros past n); returns the valid mask
+__device__ __forceinline__ uint32_t load_tri_lanes(const float* __restrict__ tris, uint32_t n, uint32_t base,
+                                                   float (&t)[kTrisPerThread][9]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const Vtx* p = reinterpret_cast<const Vtx*>(tris);
+    uint32_t mask = 0;
 #pragma unroll
-        for (int j = 0; j < 18; ++j) v[j] = p[j];
+    for (uint32_t q = 0; q < kTrisPerThread; ++q) {
+        const uint32_t k = base + q * 64u + lane;
+        const bool ok = k < n;
+        mask |= (ok ? 1u : 0u) << q;
 #pragma unroll
-        for (int j = 0; j < 18; ++j) {
-            t[4 * j] = v[j].x; t[4 * j + 1] = v[j].y; t[4 * j + 2] = v[j].z; t[4 * j + 3] = v[j].w;
+        for (uint32_t j = 0; j < 3; ++j) {
+            const Vtx v = ok ? p[(uint64_t)k * 3 + j] : Vtx{0.0f, 0.0f, 0.0f};
+            t[q][3 * j] = v.x;
+            t[q][3 * j + 1] = v.y;
+            t[q][3 * j + 2] = v.z;
         }
-        return kTrisPerThread;
     }
-    const uint32_t cnt = first < n ? n - first : 0u;
-    const float* src = tris + (uint64_t)first * 9;
-#pragma unroll
-    for (int j = 0; j < 72; ++j) t[j] = ((uint32_t)j < cnt * 9u) ? src[j] : 0.0f;
-    return cnt;
+    return mask;
 }
 
 // ---------------------------------------------------------------- K0
@@ -86,13 +94,13 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
 #pragma unroll
     for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
     {
-        float t[72];
-        const uint32_t cnt = load_tri8(tris, n, blockIdx.x * 256u + threadIdx.x, t);
+        float t[kTrisPerThread][9];
+        const uint32_t ok = load_tri_lanes(tris, n, (blockIdx.x * 4u + (threadIdx.x >> 6)) * 64u * kTrisPerThread, t);
 #pragma unroll
         for (uint32_t q = 0; q < kTrisPerThread; ++q) {
-            if (q < cnt) {
+            if ((ok >> q) & 1u) {
                 float bmin[3], bmax[3];
-                tri_bounds(t + 9 * q, bmin, bmax);
+                tri_bounds(t[q], bmin, bmax);
 #pragma unroll
                 for (int c = 0; c < 3; ++c) {
                     const float cc = (bmin[c] + bmax[c]) * 0.5f;
@@ -187,9 +195,11 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
     __shared__ uint32_t hist[4 * 256];
     __shared__ float red[kSortThreads / 64][6];
     for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) hist[j] = 0u;
-    const uint32_t g = blockIdx.x * (uint32_t)kSortThreads + threadIdx.x;
-    float t[72];
-    const uint32_t cnt = load_tri8(tris, n, g, t);  // in flight while the bounds are reduced
+    // wave w of the tile: triangles tile*4096 + 512w + 64q + lane
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wbase = blockIdx.x * (uint32_t)kSortTile + (threadIdx.x >> 6) * 64u * kTrisPerThread;
+    float t[kTrisPerThread][9];
+    const uint32_t ok = load_tri_lanes(tris, n, wbase, t);  // in flight while the bounds are reduced
     BuildParams p;
     if (partials) {
         p = bounds_final<kSortThreads>(partials, nb, red);
@@ -201,30 +211,23 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
 #pragma unroll
     for (uint32_t q = 0; q < kTrisPerThread; ++q) {
         float bmin[3], bmax[3];
-        tri_bounds(t + 9 * q, bmin, bmax);
+        tri_bounds(t[q], bmin, bmax);
         uint32_t qq[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
         k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
     }
-    const uint32_t first = g * kTrisPerThread;
-    if (cnt == kTrisPerThread) {
-        uint4* kp = reinterpret_cast<uint4*>(keys + first);
-        uint4* vp = reinterpret_cast<uint4*>(vals + first);
-        kp[0] = make_uint4(k8[0], k8[1], k8[2], k8[3]);
-        kp[1] = make_uint4(k8[4], k8[5], k8[6], k8[7]);
-        const uint32_t v = vbase + first;
-        vp[0] = make_uint4(v, v + 1, v + 2, v + 3);
-        vp[1] = make_uint4(v + 4, v + 5, v + 6, v + 7);
-    } else {
 #pragma unroll
-        for (uint32_t q = 0; q < kTrisPerThread; ++q)
-            if (q < cnt) { keys[first + q] = k8[q]; vals[first + q] = vbase + first + q; }
-    }
+    for (uint32_t q = 0; q < kTrisPerThread; ++q)  // 256 contiguous bytes per wave-instruction
+        if ((ok >> q) & 1u) {
+            const uint32_t k = wbase + q * 64u + lane;
+            keys[k] = k8[q];
+            vals[k] = vbase + k;
+        }
     __syncthreads();
 #pragma unroll
     for (uint32_t q = 0; q < kTrisPerThread; ++q)
-        if (q < cnt) {
+        if ((ok >> q) & 1u) {
             if (MSB) {
                 atomicAdd(&hist[k8[q] >> kMsbShift], 1u);  // 30-bit keys: < 1024
             } else {
@@ -378,9 +381,14 @@ struct LeafTri { float v[9]; uint32_t prim; };
 __device__ __forceinline__ LeafTri gather_leaf(uint32_t prim, const float* __restrict__ tris) {
     LeafTri t;
     t.prim = prim;
-    const float* src = tris + (uint64_t)t.prim * 9;
+    const Vtx* src = reinterpret_cast<const Vtx*>(tris) + (uint64_t)t.prim * 3;  // three 12-B loads
 #pragma unroll
-    for (int c = 0; c < 9; ++c) t.v[c] = src[c];
+    for (int j = 0; j < 3; ++j) {
+        const Vtx v = src[j];
+        t.v[3 * j] = v.x;
+        t.v[3 * j + 1] = v.y;
+        t.v[3 * j + 2] = v.z;
+    }
     return t;
 }
 
@@ -926,16 +934,53 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
     RT_STAMP(5);
 }
 
-__global__ __launch_bounds__(256) void k_sparse_level(const float* __restrict__ src, float* __restrict__ dst, uint32_t m, uint32_t half) {
-    const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+// Global sparse table over the m per-block totals (more than
+// kLdsTreeMaxBlocks blocks, the 10M path): level k entry b = U totals
+// [b, min(b + 2^k, m)), table + k*m*6.  Two launches instead of one per
+// level (14 at 10M, ~4.6 us each, almost all of it launch and drain):
+//   k_sparse_near: levels 1..kSparseNear, each block doubling a window of
+//     512 totals in LDS for its 256 entries;
+//   k_sparse_far: levels above, each entry the union of level kSparseNear
+//     entries 256 apart (<= 2^(L-1-kSparseNear) L2-resident loads).
+// min/max are exact, so every entry is the same union as the level-by-level
+// doubling's.
+constexpr uint32_t kSparseNear = 8;
+__global__ __launch_bounds__(256) void k_sparse_near(float* __restrict__ table, uint32_t m, uint32_t levels) {
+    __shared__ Aabb s_w[512];
+    const uint32_t c0 = blockIdx.x * 256u, t = threadIdx.x;
+    s_w[t] = c0 + t < m ? load_aabb(table, c0 + t) : aabb_empty();
+    s_w[t + 256] = c0 + t + 256 < m ? load_aabb(table, c0 + t + 256) : aabb_empty();
+    __syncthreads();
+    for (uint32_t lv = 1; lv < levels && lv <= kSparseNear; ++lv) {
+        const uint32_t h = 1u << (lv - 1);
+        Aabb a = s_w[t], b = s_w[t + 256];
+        aabb_union(a, s_w[t + h]);
+        if (t + 256 + h < 512) aabb_union(b, s_w[t + 256 + h]);
+        __syncthreads();
+        s_w[t] = a;
+        s_w[t + 256] = b;
+        __syncthreads();
+        if (c0 + t < m) store_aabb(table + (uint64_t)lv * m * 6, c0 + t, a);
+    }
+}
+__global__ __launch_bounds__(256) void k_sparse_far(float* __restrict__ table, uint32_t m, uint32_t levels) {
+    const uint32_t b = blockIdx.x * 256u + threadIdx.x;
     if (b >= m) return;
-    Aabb a = load_aabb(src, b);
-    if (b + half < m) aabb_union(a, load_aabb(src, b + half));
-    store_aabb(dst, b, a);
+    const float* near = table + (uint64_t)kSparseNear * m * 6;
+    Aabb a = load_aabb(near, b);
+    uint32_t have = 1;  // level-kSparseNear entries folded in: b, b + 256, ...
+    for (uint32_t lv = kSparseNear + 1; lv < levels; ++lv) {
+        const uint32_t want = 1u << (lv - kSparseNear);
+        for (; have < want; ++have) {
+            const uint64_t j = (uint64_t)b + (uint64_t)have * (1u << kSparseNear);
+            if (j < m) aabb_union(a, load_aabb(near, j));
+        }
+        store_aabb(table + (uint64_t)lv * m * 6, b, a);
+    }
 }
 
 // LDS segment tree over the M per-block totals (M <= kLdsTreeMaxBlocks) or a
-// global sparse table (levels built by k_sparse_level) for larger M.
+// global sparse table (levels built by k_sparse_near / k_sparse_far) for larger M.
 template <bool LDS_TREE>
 __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ topo,
                                                      const float* __restrict__ prebuf, const float* __restrict__ sufbuf,
@@ -1172,10 +1217,8 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
         const uint32_t L = sparse_levels(m);
-        for (uint32_t lv = 1; lv < L; ++lv) {
-            RT_KLAUNCH(k_sparse_level, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table + (uint64_t)(lv - 1) * m * 6,
-                               b.table + (uint64_t)lv * m * 6, m, 1u << (lv - 1));
-        }
+        RT_KLAUNCH(k_sparse_near, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table, m, L);
+        if (L > kSparseNear + 1) RT_KLAUNCH(k_sparse_far, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table, m, L);
         RT_KLAUNCH(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
@@ -1293,14 +1336,16 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
     if (!n) RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
-    const bool msb = n >= 2 && n <= kMsbMaxN && cfg.sort_msb;
+    const bool msb = n >= 2 && n <= kMsbBigMaxN && cfg.sort_msb;
     if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
                                 b.zero + kZHist, counts[0], s, msb)) != hipSuccess)
         return e;
     if ((e = rec(2)) != hipSuccess) return e;
     uint32_t* K[2] = {b.keys[0], b.keys[1]};
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
-    if (msb) e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, s);
+    // scratch for the chunked tile scan (n > kMsbMaxN): the parent array, which
+    // the build does not write (ceil(tiles/32) x 1024 words <= 2n - 1)
+    if (msb) e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, s);
     else e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
     if (e != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;

@@ -70,10 +70,14 @@ constexpr int kSortItems = 8;
 constexpr int kSortTile = kSortThreads * kSortItems;   // 4096 keys / tile
 constexpr uint32_t kPrefixInKernelMaxTiles = 256;      // <= 1M keys: cross-tile prefix inside k_scatter
 // MSB bucket sort (sort_kernels.hip): bucket = key >> kMsbShift of the 30-bit
-// Morton keys, used by the build for 2 <= n <= kMsbMaxN (<= 512 tiles)
+// Morton keys, used by the build for 2 <= n <= kMsbBigMaxN
 constexpr uint32_t kMsbShift = 20;
 constexpr uint32_t kMsbBuckets = 1024;
 constexpr uint32_t kMsbMaxN = 512u * kSortTile;
+// above kMsbMaxN (the 10M path) the same two levels with a chunked tile scan
+// and 1024-thread bucket sorts of up to 12288 keys (sort_kernels.hip); a
+// uniform soup's buckets hold n/1024 +- a few sigma keys
+constexpr uint32_t kMsbBigMaxN = 12u * 1000u * 1000u;
 constexpr int kRefitT = 512;                           // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
 

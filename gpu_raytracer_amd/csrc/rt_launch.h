@@ -122,7 +122,7 @@ struct TraceConfig {
                                 // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t wide_arity = 4;    // build.wide_arity: 4 = K7w 64-B records, 8 = K7w8 96-B records (greedy cut)
-    uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbMaxN, 0 = 4-pass LSB always
+    uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbBigMaxN, 0 = 4-pass LSB always
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
     uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
@@ -249,11 +249,12 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
 // top `digits` (1..4) bytes of 32-bit keys, stable; returns the buffer index
 // (0 or 1) holding the result.  counts: tiles(n)*256 words; ghist: [4][256]
 // totals of all four digits (launch_digit_hist).
-// MSB bucket sort of 30-bit keys (2 <= n <= kMsbMaxN): keys[0]/vals[0] ->
+// MSB bucket sort of 30-bit keys (2 <= n <= kMsbBigMaxN): keys[0]/vals[0] ->
 // keys[0]/vals[0] via keys[1]/vals[1]; ghist = [1024] bucket totals and
-// counts = [tile][1024] bucket counts (both from k_morton<true>).
+// counts = [tile][1024] bucket counts (both from k_morton<true>); scratch:
+// ceil(tiles/32) x 1024 words, needed above kMsbMaxN.
 hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
-                           uint32_t* bstart, hipStream_t s);
+                           uint32_t* bstart, uint32_t* scratch, hipStream_t s);
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
                            uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,

@@ -19,6 +19,7 @@
 #include "rt_launch.h"
 
 #include <algorithm>
+#include <mutex>
 
 namespace rt {
 
@@ -283,11 +284,12 @@ constexpr uint32_t kBucketCap = kBucketThreads * kSortItems;  // keys per LDS so
 
 // Stable rank of each item among the equal 10-bit digits of its wave, in
 // (item, lane) order, on top of the wave's running digit counters s_wc[w].
-__device__ __forceinline__ void rank10(const uint32_t (&dg)[kSortItems], const bool (&ok)[kSortItems],
-                                       uint32_t (*s_wc)[kMsbBuckets], uint32_t (&r)[kSortItems]) {
+template <int P = kSortItems>
+__device__ __forceinline__ void rank10(const uint32_t (&dg)[P], const bool (&ok)[P],
+                                       uint32_t (*s_wc)[kMsbBuckets], uint32_t (&r)[P]) {
     const uint32_t w = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < kSortItems; ++i) {
+    for (int i = 0; i < P; ++i) {
         const uint32_t d = dg[i];
         uint64_t peers = __ballot(ok[i]);
         if (!peers) continue;  // wave-uniform: no item of this group (a bucket's tail)
@@ -407,87 +409,118 @@ __global__ __launch_bounds__(1024) void k_msb_scan(uint32_t* __restrict__ offs, 
     }
 }
 
-// First level: one 4096-key tile per block, bucket d = key >> 20.
-__global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __restrict__ kin,
-                                                              const uint32_t* __restrict__ vin,
-                                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                              uint32_t n, const uint32_t* __restrict__ offs) {
-    constexpr int W = kSortThreads / 64;
-    static_assert(W * kMsbBuckets == 2 * kSortTile, "counters and bucketed tile share one buffer");
-    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
-    __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
-    __shared__ uint32_t s_gofs[kMsbBuckets];
-    __shared__ uint32_t s_sw[W];
+// First level: one tile of NT * P keys per block (kSortTile = 4096 for
+// n <= kMsbMaxN; 4 sort tiles = 16384 keys per 1024-thread block above, so a
+// bucket's run from one block is ~16 keys instead of ~4 -- the 10M path's
+// output writes), bucket d = key >> 20.  offs = the exclusive destinations
+// of the block's first sort tile.
+template <int NT, int P>
+__device__ __forceinline__ void msb_scatter_tile(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
+                                                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout, uint32_t n,
+                                                 const uint32_t* __restrict__ offs, uint32_t* s_buf,
+                                                 uint32_t* s_start, uint32_t* s_gofs, uint32_t* s_sw) {
+    constexpr int W = NT / 64;
+    constexpr uint32_t TILE = (uint32_t)NT * P;
+    static_assert(W * kMsbBuckets <= 2 * (int)TILE, "counters and bucketed tile share one buffer");
     uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_buf);
     uint32_t* s_key = s_buf;
-    uint32_t* s_val = s_buf + kSortTile;
+    uint32_t* s_val = s_buf + TILE;
     const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const uint32_t tile = blockIdx.x, base = tile * (uint32_t)kSortTile;
-    for (uint32_t j = tid; j < 2 * kSortTile / 4; j += kSortThreads) reinterpret_cast<uint4*>(s_buf)[j] = make_uint4(0, 0, 0, 0);
-    for (uint32_t j = tid; j < kMsbBuckets; j += kSortThreads) s_gofs[j] = offs[(uint64_t)tile * kMsbBuckets + j];
-    uint32_t k[kSortItems], v[kSortItems], dg[kSortItems], r[kSortItems];
-    bool ok[kSortItems];
+    const uint32_t base = blockIdx.x * TILE;
+    for (uint32_t j = tid; j < W * kMsbBuckets / 4; j += NT) reinterpret_cast<uint4*>(s_buf)[j] = make_uint4(0, 0, 0, 0);
+    const uint64_t orow = (uint64_t)blockIdx.x * (TILE / kSortTile) * kMsbBuckets;
+    for (uint32_t j = tid; j < kMsbBuckets; j += NT) s_gofs[j] = offs[orow + j];
+    uint32_t k[P], v[P], dg[P], r[P];
+    bool ok[P];
 #pragma unroll
-    for (int i = 0; i < kSortItems; ++i) {
-        const uint32_t idx = base + w * (64u * kSortItems) + i * 64u + l;
+    for (int i = 0; i < P; ++i) {
+        const uint32_t idx = base + w * (64u * P) + i * 64u + l;
         ok[i] = idx < n;
         k[i] = ok[i] ? kin[idx] : 0u;
         v[i] = ok[i] ? vin[idx] : 0u;
         dg[i] = (k[i] >> kMsbShift) & (kMsbBuckets - 1);
     }
     __syncthreads();
-    rank10(dg, ok, s_wc, r);
+    rank10<P>(dg, ok, s_wc, r);
     __syncthreads();
-    wave_prefix4<W, kSortThreads>(s_wc, s_start);
+    wave_prefix4<W, NT>(s_wc, s_start);
     __syncthreads();
-    scan1024<kSortThreads>(s_start, s_sw);
-    uint32_t pos[kSortItems];
+    scan1024<NT>(s_start, s_sw);
+    uint32_t pos[P];
 #pragma unroll
-    for (int i = 0; i < kSortItems; ++i) pos[i] = s_start[dg[i]] + s_wc[w][dg[i]] + r[i];
+    for (int i = 0; i < P; ++i) pos[i] = s_start[dg[i]] + s_wc[w][dg[i]] + r[i];
     __syncthreads();  // the counters are dead: the buffer becomes the bucketed tile
 #pragma unroll
-    for (int i = 0; i < kSortItems; ++i)
+    for (int i = 0; i < P; ++i)
         if (ok[i]) {
             s_key[pos[i]] = k[i];
             s_val[pos[i]] = v[i];
         }
     __syncthreads();
     const uint32_t trem = n - base;
-    const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
+    const uint32_t tcount = trem < TILE ? trem : TILE;
 #pragma unroll
-    for (int m = 0; m < kSortItems; ++m) {
-        const uint32_t p = tid + m * kSortThreads;
-        if (p < tcount) {
-            const uint32_t key = s_key[p];
+    for (int m = 0; m < P; ++m) {
+        const uint32_t q = tid + m * NT;
+        if (q < tcount) {
+            const uint32_t key = s_key[q];
             const uint32_t d = (key >> kMsbShift) & (kMsbBuckets - 1);
-            const uint32_t o = s_gofs[d] + (p - s_start[d]);
+            const uint32_t o = s_gofs[d] + (q - s_start[d]);
             kout[o] = key;
-            vout[o] = s_val[p];
+            vout[o] = s_val[q];
         }
     }
+}
+
+__global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __restrict__ kin,
+                                                              const uint32_t* __restrict__ vin,
+                                                              uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                              uint32_t n, const uint32_t* __restrict__ offs) {
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
+    __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
+    __shared__ uint32_t s_gofs[kMsbBuckets];
+    __shared__ uint32_t s_sw[kSortThreads / 64];
+    msb_scatter_tile<kSortThreads, kSortItems>(kin, vin, kout, vout, n, offs, s_buf, s_start, s_gofs, s_sw);
+}
+
+constexpr int kScatterBigItems = 16;
+constexpr uint32_t kScatterBigTile = 1024u * kScatterBigItems;  // 4 sort tiles
+constexpr size_t kScatterBigLds = (size_t)2 * kScatterBigTile * 4 + (size_t)kMsbBuckets * 4 * 2 + 64;
+__global__ __launch_bounds__(1024) void k_msb_scatter_big(const uint32_t* __restrict__ kin,
+                                                          const uint32_t* __restrict__ vin,
+                                                          uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                          uint32_t n, const uint32_t* __restrict__ offs) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    uint32_t* s_buf = s_dyn;
+    uint32_t* s_start = s_dyn + 2 * kScatterBigTile;
+    uint32_t* s_gofs = s_start + kMsbBuckets;
+    uint32_t* s_sw = s_gofs + kMsbBuckets;
+    msb_scatter_tile<1024, kScatterBigItems>(kin, vin, kout, vout, n, offs, s_buf, s_start, s_gofs, s_sw);
 }
 
 // Ranks one chunk (<= kBucketCap items in registers, item j = w*64*per +
 // i*64 + lane, wave-major) by the 10-bit digit at `shift`: r[i] = the item's position among its
 // digit's items of the chunk (earlier waves first, then item order); s_cnt =
 // the chunk's digit counts.  Callers barrier before reusing s_wc.
-__device__ __forceinline__ void bucket_rank(const uint32_t (&k)[kSortItems], const bool (&ok)[kSortItems],
+template <int NT = kBucketThreads, int P = kSortItems>
+__device__ __forceinline__ void bucket_rank(const uint32_t (&k)[P], const bool (&ok)[P],
                                             uint32_t shift, uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt,
-                                            uint32_t (&dg)[kSortItems], uint32_t (&r)[kSortItems]) {
-    {  // 16-B stores: 4 per thread instead of 16
+                                            uint32_t (&dg)[P], uint32_t (&r)[P]) {
+    constexpr int NW = NT / 64;
+    {  // 16-B stores
         uint4* z = reinterpret_cast<uint4*>(&s_wc[0][0]);
-        for (uint32_t j = threadIdx.x; j < kBucketWaves * kMsbBuckets / 4; j += kBucketThreads) z[j] = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = threadIdx.x; j < NW * kMsbBuckets / 4; j += NT) z[j] = make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < kSortItems; ++i) dg[i] = (k[i] >> shift) & (kMsbBuckets - 1);
-    rank10(dg, ok, s_wc, r);
+    for (int i = 0; i < P; ++i) dg[i] = (k[i] >> shift) & (kMsbBuckets - 1);
+    rank10<P>(dg, ok, s_wc, r);
     __syncthreads();
-    wave_prefix4<kBucketWaves, kBucketThreads>(s_wc, s_cnt);
+    wave_prefix4<NW, NT>(s_wc, s_cnt);
     __syncthreads();
     const uint32_t w = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < kSortItems; ++i) r[i] += s_wc[w][dg[i]];
+    for (int i = 0; i < P; ++i) r[i] += s_wc[w][dg[i]];
 }
 
 // Second level: one bucket [bstart[b], bstart[b+1]) per block, sorted stably by
@@ -601,6 +634,155 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
     }
 }
 
+// ---- large n (kMsbMaxN < n <= kMsbBigMaxN, the 10M path): the same two
+// levels with more tiles and bigger buckets (~n/1024 keys each).
+//   k_msb_chunk_sum, k_msb_scan, k_msb_chunk_apply: the tile-count prefix for
+//     any number of tiles, over chunks of kMsbChunk tiles (per-chunk column
+//     sums, their exclusive scan from the bucket starts by k_msb_scan on the
+//     [chunk][1024] sums, then each chunk's tiles) instead of one 16-block
+//     k_msb_scan whose threads would walk ~150 tiles each;
+//   k_msb_scatter_big: the first level over 16384-key blocks;
+//   k_bucket_sort_big: one bucket per 1024-thread block, the same two stable
+//     10-bit passes in LDS (capacity kBigCap keys: 12 per thread), the
+//     counters (16 waves x 1024) sharing the tile buffer; a bucket beyond
+//     kBigCap runs the passes chunk by chunk through global memory.
+constexpr uint32_t kMsbChunk = 32;
+constexpr int kBigThreads = 1024;
+constexpr int kBigWaves = kBigThreads / 64;
+constexpr int kBigItems = 12;
+constexpr uint32_t kBigCap = kBigThreads * kBigItems;  // 12288 keys
+constexpr size_t kBigLds = (size_t)2 * kBigCap * 4 + (size_t)kMsbBuckets * 4 * 2 + 64;  // tile + s_cnt + s_run + s_sw
+static_assert(kBigWaves * kMsbBuckets <= 2 * (int)kBigCap, "the counters fit the tile buffer");
+
+__global__ __launch_bounds__(1024) void k_msb_chunk_sum(const uint32_t* __restrict__ counts, uint32_t nt,
+                                                         uint32_t* __restrict__ csum) {
+    const uint32_t c = blockIdx.x, d = threadIdx.x, t0 = c * kMsbChunk;
+    const uint32_t t1 = t0 + kMsbChunk < nt ? t0 + kMsbChunk : nt;
+    uint32_t v[kMsbChunk], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < kMsbChunk; ++j) v[j] = t0 + j < t1 ? counts[(uint64_t)(t0 + j) * kMsbBuckets + d] : 0u;
+#pragma unroll
+    for (uint32_t j = 0; j < kMsbChunk; ++j) sum += v[j];
+    csum[(uint64_t)c * kMsbBuckets + d] = sum;
+}
+
+__global__ __launch_bounds__(1024) void k_msb_chunk_apply(uint32_t* __restrict__ counts, uint32_t nt,
+                                                           const uint32_t* __restrict__ csum) {
+    const uint32_t c = blockIdx.x, d = threadIdx.x, t0 = c * kMsbChunk;
+    const uint32_t t1 = t0 + kMsbChunk < nt ? t0 + kMsbChunk : nt;
+    uint32_t v[kMsbChunk];
+#pragma unroll
+    for (uint32_t j = 0; j < kMsbChunk; ++j) v[j] = t0 + j < t1 ? counts[(uint64_t)(t0 + j) * kMsbBuckets + d] : 0u;
+    uint32_t run = csum[(uint64_t)c * kMsbBuckets + d];
+#pragma unroll
+    for (uint32_t j = 0; j < kMsbChunk; ++j)
+        if (t0 + j < t1) {
+            counts[(uint64_t)(t0 + j) * kMsbBuckets + d] = run;
+            run += v[j];
+        }
+}
+
+__global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __restrict__ kin, uint32_t* __restrict__ vin,
+                                                                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                                 const uint32_t* __restrict__ bstart) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_big[];
+    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_big);  // counters, then the tile
+    uint32_t* s_key = s_big;
+    uint32_t* s_val = s_big + kBigCap;
+    uint32_t* s_cnt = s_big + 2 * kBigCap;
+    uint32_t* s_run = s_cnt + kMsbBuckets;
+    uint32_t* s_sw = s_run + kMsbBuckets;
+    const uint32_t s = bstart[blockIdx.x], m = bstart[blockIdx.x + 1] - s;
+    if (m == 0) return;
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    uint32_t k[kBigItems], v[kBigItems], dg[kBigItems], r[kBigItems];
+    bool ok[kBigItems];
+    if (m <= kBigCap) {
+        // per items per lane: wave w holds [64 per w, 64 per (w + 1)) (index
+        // order = wave, item, lane -- the ranking's order)
+        const uint32_t per = (m + kBigThreads - 1) / kBigThreads;
+#pragma unroll
+        for (int i = 0; i < kBigItems; ++i) {
+            const uint32_t j = w * (64u * per) + i * 64u + l;
+            ok[i] = (uint32_t)i < per && j < m;
+            k[i] = ok[i] ? kin[s + j] : 0u;
+            v[i] = ok[i] ? vin[s + j] : 0u;
+        }
+        for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+            bucket_rank<kBigThreads, kBigItems>(k, ok, shift, s_wc, s_cnt, dg, r);
+            scan1024<kBigThreads>(s_cnt, s_sw);  // its barriers also end every counter read
+#pragma unroll
+            for (int i = 0; i < kBigItems; ++i)
+                if (ok[i]) {
+                    const uint32_t p = s_cnt[dg[i]] + r[i];
+                    s_key[p] = k[i];
+                    s_val[p] = v[i];
+                }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < kBigItems; ++i) {
+                const uint32_t j = w * (64u * per) + i * 64u + l;
+                if (ok[i]) {
+                    k[i] = s_key[j];
+                    v[i] = s_val[j];
+                }
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < kBigItems; ++i) {
+            const uint32_t j = w * (64u * per) + i * 64u + l;
+            if (ok[i]) {
+                kout[s + j] = k[i];
+                vout[s + j] = v[i];
+            }
+        }
+        return;
+    }
+    // beyond one LDS sort: k_bucket_sort's chunked global passes with this
+    // block's width (kin -> kout, kout -> kin, then the copy kin -> kout)
+    uint32_t *sk = kin, *sv = vin, *dk = kout, *dv = vout;
+    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+        for (uint32_t j = tid; j < kMsbBuckets; j += kBigThreads) s_run[j] = 0u;
+        __syncthreads();
+        for (uint32_t j = tid; j < m; j += kBigThreads) atomicAdd(&s_run[(sk[s + j] >> shift) & (kMsbBuckets - 1)], 1u);
+        __syncthreads();
+        scan1024<kBigThreads>(s_run, s_sw);
+        for (uint32_t c0 = 0; c0 < m; c0 += kBigCap) {
+#pragma unroll
+            for (int i = 0; i < kBigItems; ++i) {
+                const uint32_t j = c0 + w * (64u * kBigItems) + i * 64u + l;
+                ok[i] = j < m;
+                k[i] = ok[i] ? sk[s + j] : 0u;
+                v[i] = ok[i] ? sv[s + j] : 0u;
+            }
+            bucket_rank<kBigThreads, kBigItems>(k, ok, shift, s_wc, s_cnt, dg, r);
+#pragma unroll
+            for (int i = 0; i < kBigItems; ++i)
+                if (ok[i]) {
+                    const uint32_t o = s_run[dg[i]] + r[i];
+                    dk[s + o] = k[i];
+                    dv[s + o] = v[i];
+                }
+            __syncthreads();  // s_run and s_wc reads done
+            for (uint32_t d = tid; d < kMsbBuckets; d += kBigThreads) s_run[d] += s_cnt[d];
+            __syncthreads();
+        }
+        __threadfence();  // this pass's stores before the next pass's loads (also drops stale L1 lines)
+        __syncthreads();
+        uint32_t* t0 = sk;
+        sk = dk;
+        dk = t0;
+        t0 = sv;
+        sv = dv;
+        dv = t0;
+    }
+    for (uint32_t j = tid; j < m; j += kBigThreads) {  // the result is in kin/vin
+        kout[s + j] = kin[s + j];
+        vout[s + j] = vin[s + j];
+    }
+}
+
 // ================================================================ launchers
 static inline uint32_t sdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
@@ -646,15 +828,47 @@ hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const u
     return hipGetLastError();
 }
 
+static hipError_t ensure_big_attr() {
+    static std::once_flag once;
+    static hipError_t err = hipSuccess;
+    std::call_once(once, [] {
+        err = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bucket_sort_big),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kBigLds);
+        if (err == hipSuccess)
+            err = hipFuncSetAttribute(reinterpret_cast<const void*>(k_msb_scatter_big),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kScatterBigLds);
+    });
+    return err;
+}
+
 hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
-                           uint32_t* bstart, hipStream_t s) {
+                           uint32_t* bstart, uint32_t* scratch, hipStream_t s) {
     if (n <= 1) return hipSuccess;
     const uint32_t nt = sort_tiles(n);
-    if (n > kMsbMaxN) return hipErrorInvalidValue;
-    RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart);
-    RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts);
-    RT_KLAUNCH(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
-                       bstart);
+    if (n > kMsbBigMaxN) return hipErrorInvalidValue;
+    if (n <= kMsbMaxN) {
+        RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart);
+    } else {
+        if (!scratch) return hipErrorInvalidValue;
+        const uint32_t nch = sdiv(nt, kMsbChunk);
+        RT_KLAUNCH(k_msb_chunk_sum, dim3(nch), dim3(1024), 0, s, counts, nt, scratch);
+        // the chunk sums' exclusive scan from the bucket starts is k_msb_scan's
+        // job on a [chunk][1024] table (nch <= 512: n <= 67M)
+        RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, scratch, nch, ghist, bstart);
+        RT_KLAUNCH(k_msb_chunk_apply, dim3(nch), dim3(1024), 0, s, counts, nt, scratch);
+    }
+    if (n <= kMsbMaxN) {
+        RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts);
+        RT_KLAUNCH(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
+                   bstart);
+    } else {
+        const hipError_t e = ensure_big_attr();
+        if (e != hipSuccess) return e;
+        RT_KLAUNCH(k_msb_scatter_big, dim3(sdiv(n, kScatterBigTile)), dim3(1024), kScatterBigLds, s, keys[0], vals[0],
+                   keys[1], vals[1], n, counts);
+        RT_KLAUNCH(k_bucket_sort_big, dim3(kMsbBuckets), dim3(kBigThreads), kBigLds, s, keys[1], vals[1], keys[0],
+                   vals[0], bstart);
+    }
     return hipGetLastError();
 }
 

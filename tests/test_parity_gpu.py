@@ -180,7 +180,7 @@ def test_build_degenerate_inputs(R, oracle):
 
 
 def _compare_sorts(R, tris):
-    """The build with the MSB bucket sort (default for 2 <= n <= 2^21) and with
+    """The build with the MSB bucket sort (default for 2 <= n <= 12M) and with
     the 4-pass LSB sort (build.sort = 0) must give the same BVH."""
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     outs = []
@@ -198,7 +198,7 @@ def _compare_sorts(R, tris):
     assert np.array_equal(a["nodes"].view(np.uint32), b["nodes"].view(np.uint32))
 
 
-@pytest.mark.parametrize("n", [2, 3, 4097, 70000, 1000000, 2097152])
+@pytest.mark.parametrize("n", [2, 3, 4097, 70000, 1000000, 2097152, 2097153, 3000017, 10000000])
 def test_build_sort_paths_agree(R, oracle, n):
     _compare_sorts(R, soup(oracle, n, 11))
 
@@ -213,6 +213,11 @@ def test_build_sort_paths_agree_clustered(R, oracle):
     mixed = soup(oracle, 60000, 13).copy()
     mixed[:25000] = mixed[:25000] * 1e-4 + 0.5     # one dense cell inside a uniform soup
     _compare_sorts(R, mixed)
+    # n > 2^21 (1024-thread bucket sorts): a dense cell beyond one LDS sort
+    # (12288 keys) takes the chunked path, the rest the LDS path
+    big = soup(oracle, 2500000, 14).copy()
+    big[:40000] = big[:40000] * 1e-4 + 0.25
+    _compare_sorts(R, big)
 
 
 def test_build_repeat_and_rebuild(R, oracle):
