@@ -420,3 +420,200 @@ void wsim_chain(const node_t* nodes, uint32_t n, const float* tris, const uint32
             hitp[p] = hp;
         }
 }
+
+/* ---- SAH-optimal K-ary cut (r03 design experiment).  C(x) = ci*SA(x) +
+ * min over cuts of x's subtree with <= K entries of sum(cost(e)), cost(leaf)
+ * = cl*SA(leaf), cost(internal e) = C(e): a post-order DP with B(y, j) = the
+ * cheapest cover of y's subtree by <= j entries.  Entries in preorder. */
+#define SAH_KMAX 8
+static float* g_B;      /* [node][j], j = 1..K (index j-1), unified index */
+static uint8_t* g_ch;   /* split choice: 0 = y itself, else j1 for the left child */
+static uint32_t g_K;
+static void sah_emit(const node_t* nodes, uint32_t L0, uint32_t y, uint32_t j, uint32_t* e, uint32_t* m) {
+    const uint8_t c = (y < L0) ? g_ch[(size_t)y * SAH_KMAX + (j - 1)] : 0;
+    if (c == 0) { e[(*m)++] = y; return; }
+    const uint32_t l = nodes[y].a, r = nodes[l].esc;
+    sah_emit(nodes, L0, l, c, e, m);
+    sah_emit(nodes, L0, r, j - c, e, m);
+}
+void wsim_cut_sah(const node_t* nodes, uint32_t n, uint32_t K, float ci, float cl, uint32_t* cut) {
+    const uint32_t L0 = n - 1, NN = 2 * n - 1;
+    g_K = K;
+    g_B = (float*)malloc(sizeof(float) * (size_t)NN * SAH_KMAX);
+    g_ch = (uint8_t*)calloc((size_t)NN * SAH_KMAX, 1);
+    uint8_t* top = (uint8_t*)calloc((size_t)n, 1); /* best split for the record of x (j1 for left) */
+    for (uint32_t k = 0; k < n; ++k)
+        for (uint32_t j = 0; j < SAH_KMAX; ++j) g_B[(size_t)(L0 + k) * SAH_KMAX + j] = cl * area(&nodes[L0 + k]);
+    /* iterative post-order over internal nodes */
+    uint32_t* st = (uint32_t*)malloc(sizeof(uint32_t) * 2 * n);
+    uint8_t* vis = (uint8_t*)calloc(n, 1);
+    uint32_t sp = 0;
+    st[sp++] = 0;
+    while (sp) {
+        const uint32_t y = st[sp - 1];
+        const uint32_t l = nodes[y].a, r = nodes[l].esc;
+        if (!vis[y]) {
+            vis[y] = 1;
+            if (r < L0) st[sp++] = r;
+            if (l < L0) st[sp++] = l;
+            continue;
+        }
+        --sp;
+        const float* Bl = &g_B[(size_t)l * SAH_KMAX];
+        const float* Br = &g_B[(size_t)r * SAH_KMAX];
+        float best = INFINITY;
+        uint8_t bj = 1;
+        for (uint32_t j1 = 1; j1 < K; ++j1)
+            for (uint32_t j2 = 1; j1 + j2 <= K; ++j2) {
+                const float c = Bl[j1 - 1] + Br[j2 - 1];
+                if (c < best) { best = c; bj = (uint8_t)j1; top[y] = (uint8_t)j1; top[y] |= (uint8_t)(j2 << 4); }
+            }
+        (void)bj;
+        const float C = ci * area(&nodes[y]) + best;
+        float* By = &g_B[(size_t)y * SAH_KMAX];
+        uint8_t* cy = &g_ch[(size_t)y * SAH_KMAX];
+        for (uint32_t j = 1; j <= K; ++j) {
+            float b = C;
+            uint8_t c = 0;
+            for (uint32_t j1 = 1; j1 < j; ++j1) {
+                const float v = Bl[j1 - 1] + Br[j - j1 - 1];
+                if (v < b) { b = v; c = (uint8_t)j1; }
+            }
+            By[j - 1] = b;
+            cy[j - 1] = c;
+        }
+    }
+    for (uint32_t x = 0; x + 1 < n; ++x) {
+        uint32_t e[SAH_KMAX], m = 0;
+        const uint32_t l = nodes[x].a, r = nodes[l].esc;
+        sah_emit(nodes, L0, l, top[x] & 15u, e, &m);
+        sah_emit(nodes, L0, r, top[x] >> 4, e, &m);
+        for (uint32_t i = 0; i < K; ++i) cut[(size_t)x * K + i] = i < m ? e[i] : 0xFFFFFFFFu;
+    }
+    free(st); free(vis); free(top); free(g_B); free(g_ch);
+}
+
+/* ---- In-block wave merging model (r03 design experiment).  One 16x16 tile =
+ * four 8x8 quadrant waves stepping in lockstep rounds.  From round S on, a
+ * wave with fewer than A live lanes hands its live rays to the block's pool
+ * and exits, provided another wave of the block is still live; every round a
+ * live wave first fills its finished lanes from the pool.  out[0] wave-steps,
+ * out[1] leaf blocks, out[2] record blocks, out[3] VALU model, out[4] sum of
+ * tile durations (rounds), out[5] rays moved, out[6] max tile rounds. */
+typedef struct { lane_t L; uint32_t pend; } mray_t;
+static int mlane_gather(uint32_t L0, lane_t* L, uint32_t* pend) {
+    if (L->done) return 0;
+    if (*pend == 0xFFFFFFFFu) {
+        if (L->cur == 0xFFFFFFFFu && L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+        if (L->cur != 0xFFFFFFFFu && L->cur >= L0) {
+            *pend = L->cur; L->cur = 0xFFFFFFFFu;
+            if (L->sp) { --L->sp; L->cur = L->stk[L->sp]; L->ctn = L->stn[L->sp]; }
+        }
+    }
+    if (*pend == 0xFFFFFFFFu && L->cur == 0xFFFFFFFFu) { L->done = 1; return 0; }
+    return 1;
+}
+static void mlane_step(const node_t* nodes, uint32_t L0, const float* tris, const uint32_t* cut, uint32_t K,
+                       const float* o, lane_t* L, uint32_t* pend, int* lb, int* rb) {
+    if (*pend != 0xFFFFFFFFu) { *lb = 1; leaf_test(nodes, tris, o, L, *pend); *pend = 0xFFFFFFFFu; }
+    if (L->cur == 0xFFFFFFFFu || L->cur >= L0) return;
+    if (L->ctn > L->tb) { L->cur = 0xFFFFFFFFu; return; }
+    *rb = 1;
+    const uint32_t* e = cut + (size_t)L->cur * K;
+    uint32_t hit[16], m = 0;
+    float htn[16];
+    for (uint32_t i = 0; i < K && e[i] != 0xFFFFFFFFu; ++i) {
+        float tn;
+        if (slab(&nodes[e[i]], o, L->invd, L->tb, &tn)) { hit[m] = e[i]; htn[m] = tn; ++m; }
+    }
+    L->cur = 0xFFFFFFFFu;
+    if (m) {
+        for (uint32_t i = m - 1; i >= 1; --i) { L->stk[L->sp] = hit[i]; L->stn[L->sp] = htn[i]; ++L->sp; }
+        L->cur = hit[0]; L->ctn = htn[0];
+    }
+}
+void wsim_merge(const node_t* nodes, uint32_t n, const float* tris, const uint32_t* cut, uint32_t K, const cam_t* c,
+                uint32_t w, uint32_t h, uint32_t ty0, uint32_t ty1, uint32_t A, uint32_t S, double* out,
+                uint32_t* hitp) {
+    const uint32_t L0 = n - 1;
+    static __thread lane_t lanes[4][64];
+    static __thread uint32_t pend[4][64];
+    static __thread mray_t pool[256];
+    for (uint32_t ty = ty0; ty < ty1; ++ty)
+        for (uint32_t tx = 0; tx < w / 16; ++tx) {
+            int wlive[4] = {1, 1, 1, 1};
+            uint32_t np = 0;
+            for (int wv = 0; wv < 4; ++wv)
+                for (int l = 0; l < 64; ++l) {
+                    lane_t* L = &lanes[wv][l];
+                    const uint32_t x = tx * 16 + (wv & 1) * 8 + (l & 7), y = ty * 16 + (wv >> 1) * 8 + (l >> 3);
+                    const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+                    for (int a = 0; a < 3; ++a) {
+                        L->d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
+                        L->invd[a] = 1.0f / L->d[a];
+                    }
+                    L->tb = INFINITY; L->hp = 0xFFFFFFFFu; L->sp = 0; L->cur = 0; L->ctn = 0.0f; L->done = 0;
+                    L->pix = y * w + x;
+                    pend[wv][l] = 0xFFFFFFFFu;
+                }
+            uint32_t round = 0;
+            for (;; ++round) {
+                int any = 0;
+                for (int wv = 0; wv < 4; ++wv) {
+                    if (!wlive[wv]) continue;
+                    int act = 0;
+                    for (int l = 0; l < 64; ++l) {
+                        lane_t* L = &lanes[wv][l];
+                        if (!L->done) { act += mlane_gather(L0, L, &pend[wv][l]); }
+                        if (L->done && np && (A & 0x10000u) == 0) {  /* refill a finished lane from the pool */
+                            hitp[L->pix] = L->hp;
+                            --np; *L = pool[np].L; pend[wv][l] = pool[np].pend; L->done = 0;
+                            act += mlane_gather(L0, L, &pend[wv][l]);
+                        }
+                    }
+                    if (!act && np && (A & 0x10000u)) {  /* empty-only refill: a whole wave of pool rays */
+                        for (int l = 0; l < 64; ++l) {
+                            lane_t* L = &lanes[wv][l];
+                            hitp[L->pix] = L->hp;
+                            if (np) { --np; *L = pool[np].L; pend[wv][l] = pool[np].pend; L->done = 0;
+                                      act += mlane_gather(L0, L, &pend[wv][l]); }
+                        }
+                    }
+                    if (!act) {
+                        for (int l = 0; l < 64; ++l) hitp[lanes[wv][l].pix] = lanes[wv][l].hp;
+                        wlive[wv] = 0;
+                        continue;
+                    }
+                    int others = 0;
+                    for (int k = 0; k < 4; ++k) others += (k != wv) && wlive[k];
+                    if (round >= S && (uint32_t)act < (A & 0xFFFFu) && others) {  /* donate and exit */
+                        for (int l = 0; l < 64; ++l) {
+                            lane_t* L = &lanes[wv][l];
+                            if (L->done) { hitp[L->pix] = L->hp; continue; }
+                            pool[np].L = *L; pool[np].pend = pend[wv][l]; ++np;
+                            out[5] += 1;
+                            L->done = 1;
+                        }
+                        wlive[wv] = 0;
+                        continue;
+                    }
+                    int lb = 0, rb = 0;
+                    for (int l = 0; l < 64; ++l) {
+                        lane_t* L = &lanes[wv][l];
+                        if (L->done) continue;
+                        mlane_step(nodes, L0, tris, cut, K, c->eye, L, &pend[wv][l], &lb, &rb);
+                    }
+                    out[0] += 1; out[1] += lb; out[2] += rb;
+                    out[3] += 40.0 + 116.0 * lb + 136.0 * rb;
+                    any = 1;
+                }
+                if (!any && np == 0) break;
+                if (!any && np) {  /* every wave exited with rays pooled: cannot happen (donation needs a live wave) */
+                    out[6] = -1e9;
+                    break;
+                }
+            }
+            out[4] += round;
+            if (round > out[6]) out[6] = round;
+        }
+}
