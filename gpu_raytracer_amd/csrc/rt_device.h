@@ -101,9 +101,12 @@ constexpr uint32_t kWideWild = 1u;
 // child counts as hit whatever the planes say (record_test).
 constexpr uint32_t kWideWildExp = 255u;
 // per-ray LDS stack entries (+1 spare slot, 6 B each, x 256 threads = 22.5 KB
-// per workgroup: the 7 workgroups per CU the kernel's registers allow);
+// per workgroup: 7 workgroups per CU fit the 160 KB of LDS);
 // overflow -> exact binary traversal from the overflowing record
-constexpr int kWideStack = 14;
+#ifndef RT_WIDE_STACK
+#define RT_WIDE_STACK 14
+#endif
+constexpr int kWideStack = RT_WIDE_STACK;
 
 // ---- K7w8: the 8-ary form (build.wide_arity = 8, SURVEY.md §8(f) row 1's
 // "4/8-wide").  Record X holds up to 8 entries of X's greedy

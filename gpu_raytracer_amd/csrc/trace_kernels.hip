@@ -621,10 +621,15 @@ __device__ __forceinline__ uint32_t px_bucket(uint32_t c) {
     return min(15u, 2u * (e - 2u) + ((c >> (e - 1u)) & 1u));
 }
 
-__device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict__ px_prev, uint32_t tid) {
-    __shared__ uint32_t s_cnt[4][16];  // [wave][bucket] pixel counts
-    __shared__ uint32_t s_pre[16];     // pixels in costlier buckets
-    __shared__ uint8_t s_perm[256];
+// lds: >= 144 words of the caller's LDS, free until this returns (k_trace
+// passes its stack array: the ranking's 576 B would otherwise take the block
+// past 160 KB / 7, i.e. cost a block per CU).  Ends with a barrier, so the
+// caller may overwrite them at once.
+__device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict__ px_prev, uint32_t tid,
+                                                     uint32_t* lds) {
+    uint32_t (*s_cnt)[16] = reinterpret_cast<uint32_t (*)[16]>(lds);  // [wave][bucket] pixel counts
+    uint32_t* s_pre = lds + 64;                                        // pixels in costlier buckets
+    uint8_t* s_perm = reinterpret_cast<uint8_t*>(lds + 80);
     const uint32_t lane = tid & 63, wv = tid >> 6;
     const uint32_t b = 15u - px_bucket(px_prev[tid]);  // 0 = costliest
     uint32_t rank = 0;
@@ -650,7 +655,9 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
     for (uint32_t q = 0; q < wv; ++q) pos += s_cnt[q][b];
     s_perm[pos] = (uint8_t)tid;
     __syncthreads();
-    return s_perm[tid];
+    const uint32_t li = s_perm[tid];
+    __syncthreads();
+    return li;
 }
 
 // Heavy-ray queue (trace.coop_cap, DESIGN.md "Cooperative heavy rays"): a
@@ -842,11 +849,14 @@ constexpr uint32_t kFoldPerThread = 32;  // 256 threads: up to 8192 tiles (a 108
 // queue's state (entry writes, the deferring lane's stack copy) drops out of
 // the loop: the full-frame primary kernel goes from 89 to 80 VGPRs, i.e. from
 // 5 to 6 waves per SIMD.
-template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4, bool CQ = true>
+// SPPC: the sample count as a compile-time constant (1: the colour sums and
+// the sample loop are not live across the traversal), 0 = the argument.
+template <bool COUNT, bool PACKED, bool WIDE, int NT, bool SHADOW = false, bool BUF = false, int WA = 4, bool CQ = true,
+          int SPPC = 0>
 __global__ __launch_bounds__(NT, (SHADOW && WA == 4) ? RT_KSHADOW_WAVES : (PACKED && WA == 4) ? RT_KTILES_WAVES : RT_KTRACE_WAVES)
 void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
-                                               Cam cam, uint32_t W, uint32_t H, uint32_t spp,
+                                               Cam cam, uint32_t W, uint32_t H, uint32_t spp_in,
                                                uint32_t rank, uint32_t nranks, uint32_t tilesX,
                                                float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                unsigned long long* __restrict__ counters,
@@ -859,6 +869,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                OrderFold fold = OrderFold{}) {
     __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
     __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
+    const uint32_t spp = SPPC ? (uint32_t)SPPC : spp_in;
     if constexpr (!PACKED && !SHADOW && !COUNT && NT == 256 && (WIDE || SHADOW)) {
         if (fold.out && blockIdx.x == gridDim.x - 1) {  // uniform: the extra block sorts and leaves
             static_assert((WideFmt<WA>::stack + 1) * NT >= 256 + 16, "tile_order_block's LDS");
@@ -887,7 +898,8 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     constexpr bool PX = !SHADOW && !COUNT && NT == 256;
     uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
     if (PX && px_prev) {  // uniform: the whole block
-        const uint32_t li = tile_pixel_order(px_prev + (uint64_t)slot * 256, threadIdx.x);
+        static_assert((WideFmt<WA>::stack + 1) * NT >= 144, "tile_pixel_order's LDS");
+        const uint32_t li = tile_pixel_order(px_prev + (uint64_t)slot * 256, threadIdx.x, s_ref);
         lx = li & 15;
         ly = li >> 4;
     }
@@ -2042,8 +2054,11 @@ static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity) {
 
 // k_trace with the record arity and load form chosen at run time (the
 // binary kernel, WI = false, has one form)
+#ifndef RT_SPP1
+#define RT_SPP1 1  // 0: 1-spp full frames run the generic kernel (A/B)
+#endif
 template <bool C, bool P, bool WI, int NT, typename... A>
-static void k_trace_go(bool buf, uint32_t warity, bool cq, uint32_t grid, hipStream_t s, A... a) {
+static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t grid, hipStream_t s, A... a) {
     if constexpr (WI) {
         if (warity == 8) {
             if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 8, true>), dim3(grid), dim3(NT), 0, s, a...);
@@ -2051,7 +2066,11 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, uint32_t grid, hipStr
             return;
         }
         if (buf) {
+            // (one rank's tiles keep the generic kernel: its 1-spp instance, 77 VGPRs / 6 waves
+            // instead of 96 / 5, measured no faster per rank, profiles/ab_occupancy_r03.log)
             if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true>), dim3(grid), dim3(NT), 0, s, a...);
+            else if (RT_SPP1 && !C && !P && NT == 256 && spp1)  // the headline kernel: 1 spp full frames
+                RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, false, 1>), dim3(grid), dim3(NT), 0, s, a...);
             else RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, false>), dim3(grid), dim3(NT), 0, s, a...);
             return;
         }
@@ -2199,7 +2218,8 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
-    k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, wnodes, cap, tris, n,     \
+    k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, spp == 1, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, \
+                             wnodes, cap, tris, n,                                                                       \
                              cam, w, h, spp, rank, nranks, tilesX, H, R, counters, (const float*)nullptr, Light{},      \
                              order, cost_out, px_prev, px_cost, coop_cap, cq, fold)
 #define RT_TRACE(C, P, WI) \
