@@ -31,8 +31,9 @@ Launch: `python bench.py --gpus N` spawns N rank processes itself (one per
 GPU, before any of them touches the GPU); under torch.distributed.run the
 ranks come from the environment.
 
-roofline: the trace launch (k_trace; its last block sorts the next frame's tile order) -- the bytes the kernel
-  requests (64 B per K7w record + 48 B per triangle record fetched, its own
+roofline: the trace launch (k_trace, then k_trace_coop for the rays past the heavy-ray cap, whose block 0
+  sorts the next frame's tile order) -- the bytes the kernels
+  request (64 B per K7w record + 48 B per triangle record fetched, its own
   deterministic counters, + 16 B hit + 4 B RGBA written per ray) over its
   event-timed duration, against the 8.0 TB/s HBM peak (frac) and the
   aggregate L2 bandwidth (l2_frac); beside it the PMC-measured HBM bytes
@@ -623,7 +624,7 @@ def main():
                                      "total_with_stage_events": round(stage_total_ms, 4)},
             "trace_counters_rank0_static": {"nodes_fetched": int(cnt_static[0]), "tris_tested": int(cnt_static[1]),
                                             "rays": rank_rays},
-            "roofline": dict(roof, kernel="trace launch: k_trace<wide> (+ k_tile_order when not folded)",
+            "roofline": dict(roof, kernel="trace launch: k_trace<wide> + k_trace_coop (the heavy-ray pass) (+ k_tile_order when not folded)",
                              pmc_source=(os.path.relpath(args.pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]")
                              if pmc else None,
                              algo_bytes_binary_model=algo_bytes,

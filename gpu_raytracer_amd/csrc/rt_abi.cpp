@@ -512,7 +512,8 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "path.batch" && value >= 0 && value <= (1 << 28)) c.path_batch = (uint32_t)value;
     else if (k == "render.emulate" && (value == 0 || value == 1)) c.render_emulate = (uint32_t)value;
     else if (k == "render.rccl1" && (value == 0 || value == 1)) c.render_rccl1 = (uint32_t)value;
-    else if (k == "trace.coop_cap" && value >= 0 && value <= (1 << 20)) c.coop_cap = (uint32_t)value;
+    else if (k == "trace.coop_cap" && value >= -1 && value <= (1 << 20))
+        c.coop_cap = value < 0 ? rt::kCoopCapAuto : (uint32_t)value;
     else if (k == "trace.coop_cap_tiles" && value >= -1 && value <= (1 << 20))
         c.coop_cap_tiles = value < 0 ? rt::kCoopCapAuto : (uint32_t)value;
     else if (k == "trace.buf_loads" && (value == 0 || value == 1)) c.buf_loads = (uint32_t)value;

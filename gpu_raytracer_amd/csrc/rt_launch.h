@@ -101,6 +101,14 @@ inline uint32_t coop_cap_for_tiles(uint32_t knob, uint32_t nranks) {
     if (knob != kCoopCapAuto) return knob;
     return nranks <= 2 ? 88u : 80u;
 }
+// full frames: auto = 96 steps for 1-spp frames on 256-thread tiles, whose
+// k_trace instance (SPPC = 1) has the queue at no register cost (72 VGPRs
+// either way); off otherwise (the generic queue kernel drops a wave per SIMD).
+// tools/ab_moving.py, profiles/ab_coop_full_r03.log
+inline uint32_t coop_cap_for_frame(uint32_t knob, uint32_t spp, bool small) {
+    if (knob != kCoopCapAuto) return knob;
+    return spp == 1 && !small ? 96u : 0u;
+}
 
 // Trace kernel selection / tuning (rt_config_set); every setting gives
 // bit-identical hits and images.
@@ -127,8 +135,9 @@ struct TraceConfig {
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
     uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
     uint32_t buf_loads = 1;       // wide step loads through buffer descriptors (one round trip per step)
-    uint32_t coop_cap = 0;        // primary full frames: rays past this many wide steps finish in k_trace_coop
-                                  // (one wave per ray); 0 = off
+    uint32_t coop_cap = kCoopCapAuto;  // primary full frames: rays past this many wide steps finish in
+                                  // k_trace_coop (lane groups per ray); 0 = off; auto (default):
+                                  // coop_cap_for_frame
     uint32_t coop_cap_tiles = kCoopCapAuto;  // the same for one rank's tiles of a multi-GPU frame;
                                   // auto (default): coop_cap_for_tiles (tools/coop_sweep.py,
                                   // profiles/coop_sweep_r02b.log, profiles/coop_sweep_hi_r02.log)

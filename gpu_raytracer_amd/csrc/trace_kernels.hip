@@ -1274,7 +1274,7 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // k_trace just wrote into the next frame's tile order -- the k_tile_order
 // launch (8-11 us, all of it latency) leaves the next frame's critical path
 // -- and leaves the queue to the other blocks.
-constexpr uint32_t kOrderInCoop = 256 * 16;
+constexpr uint32_t kOrderInCoop = 256 * 32;  // up to 8192 tiles: a 1080p full frame has 8160
 template <bool COUNT, bool PACKED, int G, int WA = 4>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     static_assert(sizeof(CoopLds<G, WA>) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
     const bool order_block = ord_out && gridDim.x > 1;  // uniform
     if (order_block && blockIdx.x == 0) {
-        tile_order_block<256, 16>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
+        tile_order_block<256, kOrderInCoop / 256>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
                                   reinterpret_cast<uint32_t*>(&s_l[0]) + 256, ord_ema);
         return;
     }
@@ -2068,7 +2068,9 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t g
         if (buf) {
             // (one rank's tiles keep the generic kernel: its 1-spp instance, 77 VGPRs / 6 waves
             // instead of 96 / 5, measured no faster per rank, profiles/ab_occupancy_r03.log)
-            if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true>), dim3(grid), dim3(NT), 0, s, a...);
+            if (cq && RT_SPP1 && !C && !P && NT == 256 && spp1)  // full frames with the queue (trace.coop_cap)
+                RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true, 1>), dim3(grid), dim3(NT), 0, s, a...);
+            else if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true>), dim3(grid), dim3(NT), 0, s, a...);
             else if (RT_SPP1 && !C && !P && NT == 256 && spp1)  // the headline kernel: 1 spp full frames
                 RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, false, 1>), dim3(grid), dim3(NT), 0, s, a...);
             else RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, false>), dim3(grid), dim3(NT), 0, s, a...);
@@ -2142,8 +2144,13 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // full frames on 256-thread wide kernels (no queue, no counters): the
     // next frame's order is sorted by an extra block of this launch
     // (OrderFold) instead of a k_tile_order launch ahead of it
+    // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
+    const uint32_t coop_cap =
+        wide && sched && sched->coop_q && n <= kBufMaxN
+            ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : coop_cap_for_frame(cfg.coop_cap, spp, small))
+            : 0u;
     const bool can_fold = RT_ORDER_FOLD && sched && nranks == 1 && !packed && !small && wide && !counters &&
-                          !cfg.order_override && cfg.coop_cap == 0 && nb <= 256 * kFoldPerThread;
+                          !cfg.order_override && coop_cap == 0 && nb <= 256 * kFoldPerThread;
     OrderFold fold;
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
@@ -2200,9 +2207,6 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         sched->prev_cam = c;
         sched->prev_cam_valid = true;
     }
-    // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
-    const uint32_t coop_cap = wide && sched && sched->coop_q && n <= kBufMaxN
-                                  ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : cfg.coop_cap) : 0u;
     CoopQ cq;
     if (coop_cap) {
         if (sched->coop_fresh) {

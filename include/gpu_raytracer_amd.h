@@ -330,9 +330,10 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * (a 1-rank communicator).  "trace.coop_cap" / "trace.coop_cap_tiles"
  * 0..2^20: a primary ray still traversing after that many wide steps is
  * queued and finished by a whole wave (k_trace_coop, DESIGN.md "Cooperative
- * heavy rays"); 0 = off; defaults 0 for full frames and, for one rank's
- * tiles of a multi-GPU frame, -1 = by rank count (88 steps for P = 2, 80 for
- * P >= 3); "trace.coop_max" queue entries per frame shape
+ * heavy rays"); 0 = off; -1 = auto, the defaults: for full frames 96 steps
+ * at 1 spp on 256-thread tiles (off otherwise) and, for one rank's tiles of a
+ * multi-GPU frame, by rank count (88 steps for P = 2, 80 for P >= 3);
+ * "trace.coop_max" queue entries per frame shape
  * (default 65536; rays beyond it keep tracing alone).  "build.stage_events"
  * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
  * 0/1: timing events of scenes created afterwards record with the

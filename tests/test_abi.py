@@ -244,7 +244,7 @@ CONFIG_KEYS = {
     "path.batch": ([0, 1 << 20], [-1], 0),
     "render.emulate": ([0, 1], [2], 0),
     "render.rccl1": ([0, 1], [2], 0),
-    "trace.coop_cap": ([0, 1, 96, 1 << 20], [-1, (1 << 20) + 1], 0),
+    "trace.coop_cap": ([-1, 0, 1, 96, 1 << 20], [-2, (1 << 20) + 1], -1),
     "trace.coop_cap_tiles": ([-1, 0, 1, 96, 1 << 20], [-2, (1 << 20) + 1], -1),
     "trace.buf_loads": ([0, 1], [2, -1], 1),
     "trace.coop_lanes": ([16, 32, 64], [0, 8, 48, 128], 32),

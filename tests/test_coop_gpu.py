@@ -59,7 +59,7 @@ def test_coop_full_frame(R, oracle, cfg, cap, spp, lanes):
     tris = oracle.soup(40000, 11).reshape(-1, 9)
     w, h = 200, 120
     eh, er = _frame(oracle, tris, V, w, h, spp)
-    cfg("trace.coop_cap", cap, 0)
+    cfg("trace.coop_cap", cap, -1)
     cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
@@ -81,7 +81,7 @@ def test_coop_changes_work_not_result(R, oracle, cfg):
         s.build()
         base = s.render_work(cam, w, h, 1)
         _, img0, _ = s.render(cam, w, h, 1)
-        cfg("trace.coop_cap", 2, 0)
+        cfg("trace.coop_cap", 2, -1)
         coop = s.render_work(cam, w, h, 1)
         _, img1, _ = s.render(cam, w, h, 1)
     assert np.array_equal(img0, img1)
@@ -95,7 +95,7 @@ def test_coop_queue_full(R, oracle, cfg, qmax):
     w, h, spp = 150, 100, 2
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("trace.coop_max", qmax, 65536)
-    cfg("trace.coop_cap", 3, 0)
+    cfg("trace.coop_cap", 3, -1)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -138,7 +138,7 @@ def test_coop_frontier_handoff(R, oracle, cfg, lanes):
     V = _soup_view()
     w, h = 96, 64
     eh, er = _frame(oracle, tris, V, w, h, 1)
-    cfg("trace.coop_cap", 1, 0)
+    cfg("trace.coop_cap", 1, -1)
     cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
@@ -155,7 +155,7 @@ def test_coop_headline_1m(R, oracle, cfg):
     tris = oracle.soup(1_000_000, 1).reshape(-1, 9)
     w, h = 1920, 1080
     eh, er = _frame(oracle, tris, V, w, h, 1)
-    cfg("trace.coop_cap", 48, 0)
+    cfg("trace.coop_cap", 48, -1)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()

@@ -29,7 +29,7 @@ def poison(R):
     R.config_set("debug.poison", 1)
     yield
     for k, v in (("debug.poison", 0), ("build.wide_arity", 4), ("render.emulate", 0),
-                 ("trace.coop_cap", 0), ("trace.coop_cap_tiles", -1)):
+                 ("trace.coop_cap", -1), ("trace.coop_cap_tiles", -1)):
         R.config_set(k, v)
 
 

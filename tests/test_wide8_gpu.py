@@ -132,7 +132,7 @@ def test_wide8_coop_full_frame(R, oracle, cfg, lanes, cap):
     tris = oracle.soup(40000, 11).reshape(-1, 9)
     w, h, spp = 200, 120, 2
     eh, er = _oracle(oracle, tris, V, w, h, spp)
-    cfg("trace.coop_cap", cap, 0)
+    cfg("trace.coop_cap", cap, -1)
     cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
@@ -170,7 +170,7 @@ def test_wide8_coop_frontier_handoff(R, oracle, cfg, lanes):
     V = _soup_view()
     w, h = 96, 64
     eh, er = _oracle(oracle, tris, V, w, h, 1)
-    cfg("trace.coop_cap", 1, 0)
+    cfg("trace.coop_cap", 1, -1)
     cfg("trace.coop_lanes", lanes, 32)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:

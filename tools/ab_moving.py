@@ -38,7 +38,7 @@ for _ in range(rounds):
         t = [scene.render_device(cams[2 + i], w, h, spp, d_rgba=img.data_ptr(), timed=True) for i in range(frames)]
         res[name].append(float(np.mean(t)))
         for k in kv:  # back to the library defaults
-            R.config_set(k, {"trace.coop_cap": 0, "trace.tile_order": 1, "trace.px_sort": 1, "trace.wg": 256,
+            R.config_set(k, {"trace.coop_cap": -1, "trace.tile_order": 1, "trace.px_sort": 1, "trace.wg": 256,
                              "trace.buf_loads": 1, "trace.coop_lanes": 32, "trace.coop_cap_tiles": -1}.get(k, 0))
 for name, _ in configs:
     print(f"{name:<22s} mean trace {np.median(res[name]):.4f} ms  (rounds: {' '.join(f'{x:.4f}' for x in res[name])})",

@@ -5,8 +5,9 @@ per-launch entry bench.py's roofline reads (profiles/pmc_summary.json).
 usage: python tools/pmc_summary.py <prof dir> <tag> <config name> <warmup> [n_gpus]
 
 Only the timed steps count: the first <warmup> frames' dispatches are dropped.
-A frame's trace launch = k_tile_order (when present) + k_trace<...>; a build =
-every build kernel between two trace launches.
+A frame's trace launch = k_tile_order (when present) + k_trace<...> + k_trace_coop
+(the heavy-ray pass, when the queue is on); a build = every build kernel between
+two trace launches.
 
 PMC corrections (MI355X_MICROARCH.md §HBM): HBM bytes = 2 x FETCH_SIZE (gfx950
 tallies a 128-B read request at 64 B) + WRITE_SIZE, both reported in KiB.
@@ -66,8 +67,10 @@ def frames(seq, warmup):
         elif b == "k_tile_order":
             pend_order = v
         elif b == "k_trace":
-            fr.append({"trace": v, "order": pend_order or 0.0, "build": sum(build), "trace_name": k})
+            fr.append({"trace": v, "order": pend_order or 0.0, "coop": 0.0, "build": sum(build), "trace_name": k})
             build, pend_order = [], None
+        elif b == "k_trace_coop" and fr:
+            fr[-1]["coop"] += v
     return fr[warmup:]
 
 
@@ -80,7 +83,8 @@ def main():
     ngpu = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     tr = dispatches(os.path.join(d, "trace", "**", "*kernel_trace.csv"))
     ft = frames(tr, warmup)
-    trace_us = mean([f["trace"] for f in ft])
+    trace_us = mean([f["trace"] + f["coop"] for f in ft])
+    coop_us = mean([f["coop"] for f in ft])
     order_us = mean([f["order"] for f in ft])
     build_us = mean([f["build"] for f in ft])
     kname = ft[0]["trace_name"] if ft else "?"
@@ -88,7 +92,7 @@ def main():
     def per_frame(sub, counter):
         seq = dispatches(os.path.join(d, sub, "**", "*counter_collection.csv"), counter)
         f = frames(seq, warmup)
-        return (mean([x["trace"] + x["order"] for x in f]), mean([x["trace"] for x in f]),
+        return (mean([x["trace"] + x["coop"] + x["order"] for x in f]), mean([x["trace"] + x["coop"] for x in f]),
                 mean([x["build"] for x in f]))
 
     fetch = per_frame("fetch", "FETCH_SIZE")
@@ -111,7 +115,8 @@ def main():
         tree = "?"
     entry = {
         "config": cfg, "n_gpus": ngpu, "tag": tag, "tree": tree, "kernel": kname, "timed_frames": len(ft),
-        "trace_kernel_avg_us": trace_us, "tile_order_avg_us": order_us, "build_kernel_sum_ms": build_us / 1e3
+        "trace_kernel_avg_us": trace_us, "coop_kernel_avg_us": coop_us, "tile_order_avg_us": order_us,
+        "build_kernel_sum_ms": build_us / 1e3
         if build_us is not None else None,
         "hbm_bytes_per_launch": hbm, "fetch_kib_raw": fetch[0], "write_kib": write[0],
         "build_hbm_bytes": bhbm,
@@ -119,7 +124,8 @@ def main():
         "cycles_vs_duration_at_2p4ghz": cyc / (trace_us * 2400.0) if cyc and trace_us else None,
         "waves": waves[1], "wait_any_frac": wait[1] / wcyc[1] if wait[1] and wcyc[1] else None,
         "valu_lane_util": thr[1] / (64.0 * act[1]) if thr[1] and act[1] else None,
-        "note": "per timed trace launch (k_tile_order + k_trace; VALU/cycles: k_trace only); hbm = 2*FETCH_SIZE + "
+        "note": "per timed trace launch (k_tile_order + k_trace + k_trace_coop; trace_kernel_avg_us and VALU/cycles: "
+                "k_trace + k_trace_coop); hbm = 2*FETCH_SIZE + "
                 "WRITE_SIZE (KiB x 1024, gfx950 read correction); cycles = GRBM_GUI_ACTIVE / 8 XCDs",
     }
     jp = os.path.join("profiles", "pmc_summary.json")
@@ -145,7 +151,8 @@ def main():
          f"command: `rocprofv3 --kernel-trace --stats -- python3 bench.py --only-timed ...` (+ one `--pmc` pass "
          f"each for FETCH_SIZE, WRITE_SIZE and the SQ group), tree {tree}; warm-up frames dropped: {warmup}", "",
          "## timed frames (means per frame)", "",
-         f"- trace kernel `{kname}`: {trace_us:.2f} us; k_tile_order {order_us:.2f} us" if trace_us else "- none",
+         f"- trace kernels `{kname}` + k_trace_coop: {trace_us:.2f} us (k_trace_coop {coop_us:.2f}); "
+         f"k_tile_order {order_us:.2f} us" if trace_us else "- none",
          f"- build kernels (sum): {build_us:.2f} us" if build_us else "",
          f"- HBM bytes per trace launch (PMC): {hbm:.4g}; per build: {bhbm:.4g}" if hbm and bhbm else "",
          f"- VALU wave-instructions per trace launch: {valu[1]:.4g}; cycles (GRBM/8): {cyc:.4g}; "
