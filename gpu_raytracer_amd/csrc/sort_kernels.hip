@@ -619,7 +619,10 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
             for (uint32_t d = tid; d < kMsbBuckets; d += kBucketThreads) s_run[d] += s_cnt[d];
             __syncthreads();
         }
-        __threadfence();  // this pass's stores before the next pass's loads (also drops stale L1 lines)
+        // this pass's stores before the next pass's loads by the block's other waves
+        // (one CU, one L1: a workgroup-scope fence; __threadfence would also write
+        // back the XCD's L2, ~60 us, profiles/calib_barrier_r03.log)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
         uint32_t* t0 = sk;
         sk = dk;
@@ -768,7 +771,10 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
             for (uint32_t d = tid; d < kMsbBuckets; d += kBigThreads) s_run[d] += s_cnt[d];
             __syncthreads();
         }
-        __threadfence();  // this pass's stores before the next pass's loads (also drops stale L1 lines)
+        // this pass's stores before the next pass's loads by the block's other waves
+        // (one CU, one L1: a workgroup-scope fence; __threadfence would also write
+        // back the XCD's L2, ~60 us, profiles/calib_barrier_r03.log)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         __syncthreads();
         uint32_t* t0 = sk;
         sk = dk;
