@@ -1323,6 +1323,10 @@ hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s) {
     return n ? launch_cross(b, n, config_snapshot().wide_collapse, b.warity, s) : hipSuccess;
 }
 
+bool build_uses_msb(const BuildBufs& b, uint32_t n) {
+    return n >= 2 && n <= kMsbBigMaxN && config_snapshot().sort_msb && b.sort_mode != 2;
+}
+
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages) {
     const TraceConfig cfg = config_snapshot();
     hipError_t e;
@@ -1336,7 +1340,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
     if (!n) RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
-    const bool msb = n >= 2 && n <= kMsbBigMaxN && cfg.sort_msb;
+    const bool msb = n >= 2 && n <= kMsbBigMaxN && cfg.sort_msb && b.sort_mode != 2;
     if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
                                 b.zero + kZHist, counts[0], s, msb)) != hipSuccess)
         return e;

@@ -54,6 +54,7 @@ struct Replica {
     hipStream_t stream = nullptr;  // the replica's own stream (builds, synchronous renders)
     rt::BuildBufs bufs;
     bool uploaded = false, built = false;
+    bool msb_probe = false;  // this build decides the scene's sort (BuildBufs::sort_mode)
     rt::BuildEvents ev;
     rt_build_times times{};
     // render scratch (grown on demand)
@@ -374,6 +375,7 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         // a rebuild that fails half-way must not leave the old flag over a
         // half-written BVH: built again only after the synchronize below
         r->built = false;
+        r->msb_probe = r->bufs.sort_mode == 0 && rt::build_uses_msb(r->bufs, s->n);
         hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
     }
@@ -393,6 +395,14 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         float tot = 0;
         HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
         r->times.total = tot;
+        if (r->msb_probe) {  // the scene's first MSB build: keep the MSB sort unless a bucket outgrew it
+            uint32_t bs[rt::kMsbBuckets + 1];
+            HIPR(hipMemcpy(bs, r->bufs.bstart, sizeof(bs), hipMemcpyDeviceToHost));
+            uint32_t big = 0;
+            for (uint32_t b = 0; b < rt::kMsbBuckets; ++b) big = std::max(big, bs[b + 1] - bs[b]);
+            r->bufs.sort_mode = big > rt::msb_bucket_cap(s->n) ? 2u : 1u;
+            r->msb_probe = false;
+        }
         r->built = true;
         worst = std::max(worst, (double)tot);
     }

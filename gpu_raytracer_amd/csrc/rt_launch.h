@@ -36,7 +36,16 @@ struct BuildBufs {
     uint32_t ntiles = 0;            // sort tiles at cap_n
     uint32_t m_blocks = 0;          // refit blocks at cap_n
     uint32_t levels = 0;            // sparse-table levels at cap_n
+    // the scene's sort: 0 = not yet known (the MSB bucket sort), 1 = MSB, 2 = the
+    // 4-pass LSB sort -- a bucket of the first MSB build outgrew one block's LDS
+    // sort (clustered geometry: that bucket is sorted by one block through
+    // global memory, ~10x the build); a scene's triangles never change
+    uint32_t sort_mode = 0;
 };
+// keys one MSB bucket may hold for the LDS bucket sort at this n
+uint32_t msb_bucket_cap(uint32_t n);
+// whether launch_build(b, n) sorts with the MSB bucket sort
+bool build_uses_msb(const BuildBufs& b, uint32_t n);
 
 // zero region layout (uint32 words)
 constexpr uint32_t kZHist = 0;          // [4][256] digit histograms

@@ -649,6 +649,8 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __rest
 //     10-bit passes in LDS (capacity kBigCap keys: 12 per thread), the
 //     counters (16 waves x 1024) sharing the tile buffer; a bucket beyond
 //     kBigCap runs the passes chunk by chunk through global memory.
+uint32_t msb_bucket_cap(uint32_t n) { return n <= kMsbMaxN ? kBucketCap : (uint32_t)(1024 * 12); }
+
 constexpr uint32_t kMsbChunk = 32;
 constexpr int kBigThreads = 1024;
 constexpr int kBigWaves = kBigThreads / 64;

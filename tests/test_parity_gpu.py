@@ -220,6 +220,27 @@ def test_build_sort_paths_agree_clustered(R, oracle):
     _compare_sorts(R, big)
 
 
+def test_clustered_scene_switches_sort(R, oracle):
+    """A scene whose first (MSB) build finds a bucket beyond one LDS sort --
+    a quarter of a 1M soup in one tiny cell -- is rebuilt with the 4-pass LSB
+    sort (BuildBufs::sort_mode): every build equals the oracle, and the
+    rebuilds no longer pay for one block sorting the dense cell."""
+    rng = np.random.default_rng(5)
+    n = 1_000_000
+    t = rng.random((n, 9), dtype=np.float32)
+    t[: n // 4] = 0.5 + rng.random((n // 4, 9), dtype=np.float32) * np.float32(1e-4)
+    exp = oracle.build(t)
+    ms = []
+    with R.Scene.from_soup(t) as s:
+        for _ in range(3):
+            ms.append(s.build())
+            got = s.read_bvh()
+            assert np.array_equal(got["keys"], exp["keys"])
+            assert np.array_equal(got["vals"], exp["vals"])
+            assert np.array_equal(got["nodes"].view(np.uint32), exp["nodes"].view(np.uint32))
+    assert ms[2] < 0.5 * ms[0], ms
+
+
 def test_build_repeat_and_rebuild(R, oracle):
     """Control words are re-armed between builds (zeroed per build)."""
     tris = soup(oracle, 70000, 2)
