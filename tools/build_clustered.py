@@ -14,7 +14,9 @@ rng = np.random.default_rng(5)
 t = rng.random((n, 9), dtype=np.float32)
 k = n // 4
 t[:k] = 0.5 + rng.random((k, 9), dtype=np.float32) * 1e-4  # a quarter of the soup in one tiny cell
+with R.Scene.from_soup(rng.random((n, 9), dtype=np.float32)) as w:  # loads every build kernel first
+    [w.build() for _ in range(3)]
 with R.Scene.from_soup(t) as s:
     ms = [s.build() for _ in range(12)]
-print(f"clustered n={n}: first build {ms[0]:.4f} ms, then median {np.median(ms[2:]):.4f} ms (min {min(ms[2:]):.4f})",
+print(f"clustered n={n}: first build (MSB, decides the sort) {ms[0]:.4f} ms, then median {np.median(ms[2:]):.4f} ms (min {min(ms[2:]):.4f})",
       flush=True)
