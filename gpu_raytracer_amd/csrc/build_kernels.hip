@@ -1349,7 +1349,10 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
     // scratch for the chunked tile scan (n > kMsbMaxN): the parent array, which
     // the build does not write (ceil(tiles/32) x 1024 words <= 2n - 1)
-    if (msb) e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, s);
+    if (msb && b.sort_mode == 0)  // the scene's first build: both sorts, gated on the bucket totals
+        e = launch_sort_probe(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, b.zero + kZHist4,
+                              b.zero + kZDense, s);
+    else if (msb) e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, s);
     else e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
     if (e != hipSuccess) return e;
     if ((e = rec(3)) != hipSuccess) return e;

@@ -395,12 +395,10 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         float tot = 0;
         HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
         r->times.total = tot;
-        if (r->msb_probe) {  // the scene's first MSB build: keep the MSB sort unless a bucket outgrew it
-            uint32_t bs[rt::kMsbBuckets + 1];
-            HIPR(hipMemcpy(bs, r->bufs.bstart, sizeof(bs), hipMemcpyDeviceToHost));
-            uint32_t big = 0;
-            for (uint32_t b = 0; b < rt::kMsbBuckets; ++b) big = std::max(big, bs[b + 1] - bs[b]);
-            r->bufs.sort_mode = big > rt::msb_bucket_cap(s->n) ? 2u : 1u;
+        if (r->msb_probe) {  // the scene's first build ran both sorts gated on k_msb_scan's verdict: keep it
+            uint32_t dense = 0;
+            HIPR(hipMemcpy(&dense, r->bufs.zero + rt::kZDense, 4, hipMemcpyDeviceToHost));
+            r->bufs.sort_mode = dense ? 2u : 1u;
             r->msb_probe = false;
         }
         r->built = true;

@@ -59,6 +59,15 @@ __device__ __forceinline__ uint32_t pcg_hash(uint32_t x) {
 }
 
 // Build-time scalar parameters written by K0 (bounds) for K1 (Morton).
+// A kernel's run condition on a device word written by an earlier kernel of
+// the same stream (the first build of a scene runs both sorts, each gated on
+// the MSB scan's verdict, launch_build): p = nullptr runs unconditionally.
+struct Gate {
+    const uint32_t* p = nullptr;
+    uint32_t want = 0;
+};
+__device__ __forceinline__ bool gated_off(const Gate& g) { return g.p && *g.p != g.want; }
+
 struct BuildParams {
     float lo[3], hi[3], inv[3];
     uint32_t pad[7];

@@ -53,7 +53,9 @@ constexpr uint32_t kZTileCtr = 1024;    // [4] onesweep tile tickets
 constexpr uint32_t kZErr = 1028;        // sticky error bits (reserved)
 constexpr uint32_t kZCrossCtr = 1040;   // [kCrossShards] crossing-list shard lengths
 constexpr uint32_t kCrossShards = 16;
-constexpr uint32_t kZEnd = 1056;        // words zeroed by K0 every build
+constexpr uint32_t kZHist4 = 1056;      // [4][256] digit histograms of a probe build's LSB leg
+constexpr uint32_t kZDense = 2080;      // a probe build's verdict (k_msb_scan writes it)
+constexpr uint32_t kZEnd = 2084;        // words zeroed by K0 every build
 
 
 hipError_t alloc_build(BuildBufs& b, uint32_t n);
@@ -271,8 +273,16 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
 // keys[0]/vals[0] via keys[1]/vals[1]; ghist = [1024] bucket totals and
 // counts = [tile][1024] bucket counts (both from k_morton<true>); scratch:
 // ceil(tiles/32) x 1024 words, needed above kMsbMaxN.
+// dense: when set, k_msb_scan writes 1 there if a bucket holds more than
+// msb_bucket_cap(n) keys (else 0) and the scatter/bucket kernels run only on 0.
 hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
-                           uint32_t* bstart, uint32_t* scratch, hipStream_t s);
+                           uint32_t* bstart, uint32_t* scratch, hipStream_t s, uint32_t* dense = nullptr);
+// A scene's first sort: the MSB sort gated on its own verdict (*dense == 0),
+// then the 4-pass LSB sort gated on *dense == 1 (ghist4: [4][256] zeroed
+// words; counts as for launch_sort_msb).  The caller reads *dense afterwards.
+hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
+                             uint32_t* counts, uint32_t* bstart, uint32_t* scratch, uint32_t* ghist4,
+                             uint32_t* dense, hipStream_t s);
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
                            uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,

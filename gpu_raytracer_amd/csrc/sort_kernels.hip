@@ -52,7 +52,9 @@ __device__ __forceinline__ uint32_t scan256(uint32_t v, uint32_t* sw /* [4] */) 
 // ---------------------------------------------------------------- histogram
 template <int SHIFT>
 __global__ __launch_bounds__(kSortThreads) void k_tile_hist(const uint32_t* __restrict__ keys, uint32_t n,
-                                                            uint32_t* __restrict__ counts /* [tile][256] */) {
+                                                            uint32_t* __restrict__ counts /* [tile][256] */,
+                                                            Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     __shared__ uint32_t h[256];
     if (threadIdx.x < 256) h[threadIdx.x] = 0u;
     __syncthreads();
@@ -74,7 +76,9 @@ __global__ __launch_bounds__(kSortThreads) void k_tile_hist(const uint32_t* __re
 
 // In-place exclusive scan of counts[tile][d] over tiles, one workgroup per
 // digit (used when tiles > kPrefixInKernelMaxTiles).
-__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ counts, uint32_t ntiles) {
+__global__ __launch_bounds__(256) void k_scan_tiles(uint32_t* __restrict__ counts, uint32_t ntiles,
+                                                    Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     __shared__ uint32_t sw[4];
     __shared__ uint32_t s_carry;
     const uint32_t d = blockIdx.x;
@@ -118,7 +122,9 @@ template <int SHIFT, bool PREFIX_IN_KERNEL>
 __global__ __launch_bounds__(kSortThreads) void k_scatter(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ vin,
                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                           uint32_t n, const uint32_t* __restrict__ ghist /* this digit's 256 */,
-                                                          const uint32_t* __restrict__ counts /* [tile][256] counts or offsets */) {
+                                                          const uint32_t* __restrict__ counts /* [tile][256] counts or offsets */,
+                                                          Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     constexpr int W = kSortThreads / 64;  // 8 waves
     __shared__ uint32_t s_wc[W][256];
     __shared__ uint32_t s_key[kSortTile];
@@ -245,7 +251,9 @@ __global__ __launch_bounds__(kSortThreads) void k_scatter(const uint32_t* __rest
 
 // Stand-alone 4-digit global histogram (rt_stage_sort on caller keys; the
 // build gets it from K1).
-__global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ ghist) {
+__global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ ghist,
+                                                    Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     __shared__ uint32_t hist[4 * 256];
     for (int j = threadIdx.x; j < 1024; j += 256) hist[j] = 0u;
     __syncthreads();
@@ -372,8 +380,11 @@ __device__ __forceinline__ void scan1024(uint32_t* a, uint32_t* s_sw /* [NT / 64
 // sum_{t' < t} counts[t'][d], in place; bstart[0..1024] = bucket starts.
 // 16 blocks x 1024 threads: block b owns buckets [64b, 64b + 64), a thread
 // one bucket and a chunk of <= 32 tiles.
+// dense (optional): 1 when a bucket holds more than cap keys (a probe build's
+// verdict: the gated MSB kernels below stand down and the LSB sort runs), else 0
 __global__ __launch_bounds__(1024) void k_msb_scan(uint32_t* __restrict__ offs, uint32_t nt,
-                                                   const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bstart) {
+                                                   const uint32_t* __restrict__ ghist, uint32_t* __restrict__ bstart,
+                                                   uint32_t cap = 0, uint32_t* __restrict__ dense = nullptr) {
     __shared__ uint32_t s_base[kMsbBuckets];
     __shared__ uint32_t s_sw[16];
     __shared__ uint32_t s_csum[16][64];
@@ -385,6 +396,10 @@ __global__ __launch_bounds__(1024) void k_msb_scan(uint32_t* __restrict__ offs, 
     if (blockIdx.x == 0) {
         bstart[t] = s_base[t];
         if (t == kMsbBuckets - 1) bstart[kMsbBuckets] = s_base[t] + g;
+        if (dense) {  // block-uniform branch: every thread of block 0 reaches the barrier
+            const int big = __syncthreads_or(g > cap);
+            if (t == 0) dense[0] = big ? 1u : 0u;
+        }
     }
     const uint32_t dl = t & 63, c = t >> 6, d = blockIdx.x * 64 + dl;
     const uint32_t C = (nt + 15) / 16;
@@ -475,7 +490,8 @@ __device__ __forceinline__ void msb_scatter_tile(const uint32_t* __restrict__ ki
 __global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __restrict__ kin,
                                                               const uint32_t* __restrict__ vin,
                                                               uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                              uint32_t n, const uint32_t* __restrict__ offs) {
+                                                              uint32_t n, const uint32_t* __restrict__ offs, Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
     __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
     __shared__ uint32_t s_gofs[kMsbBuckets];
@@ -489,7 +505,8 @@ constexpr size_t kScatterBigLds = (size_t)2 * kScatterBigTile * 4 + (size_t)kMsb
 __global__ __launch_bounds__(1024) void k_msb_scatter_big(const uint32_t* __restrict__ kin,
                                                           const uint32_t* __restrict__ vin,
                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                          uint32_t n, const uint32_t* __restrict__ offs) {
+                                                          uint32_t n, const uint32_t* __restrict__ offs, Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
     uint32_t* s_buf = s_dyn;
     uint32_t* s_start = s_dyn + 2 * kScatterBigTile;
@@ -527,7 +544,8 @@ __device__ __forceinline__ void bucket_rank(const uint32_t (&k)[P], const bool (
 // key bits 0..19 (the bucket shares bits 20..29).
 __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint32_t* __restrict__ kin, uint32_t* __restrict__ vin,
                                                                 uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                                const uint32_t* __restrict__ bstart) {
+                                                                const uint32_t* __restrict__ bstart, Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     static_assert(kBucketWaves * kMsbBuckets == 2 * kBucketCap, "counters and sorted chunk share one buffer");
     __shared__ __attribute__((aligned(16))) uint32_t s_wc[kBucketWaves][kMsbBuckets];  // ranking counters; fast path: then the sorted chunk
     __shared__ __attribute__((aligned(16))) uint32_t s_cnt[kMsbBuckets];
@@ -689,7 +707,8 @@ __global__ __launch_bounds__(1024) void k_msb_chunk_apply(uint32_t* __restrict__
 
 __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __restrict__ kin, uint32_t* __restrict__ vin,
                                                                  uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                                 const uint32_t* __restrict__ bstart) {
+                                                                 const uint32_t* __restrict__ bstart, Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_big[];
     uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_big);  // counters, then the tile
     uint32_t* s_key = s_big;
@@ -796,44 +815,57 @@ static inline uint32_t sdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b -
 
 uint32_t sort_tiles(uint32_t n) { return n ? sdiv(n, kSortTile) : 0u; }
 
-hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s) {
+static hipError_t digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s, Gate g = Gate{}) {
     if (!n) return hipSuccess;
-    RT_KLAUNCH(k_digit_hist, dim3(std::min<uint32_t>(512, sdiv(n, 256))), dim3(256), 0, s, keys, n, ghist);
+    RT_KLAUNCH(k_digit_hist, dim3(std::min<uint32_t>(512, sdiv(n, 256))), dim3(256), 0, s, keys, n, ghist, g);
     return hipGetLastError();
 }
 
-hipError_t launch_tile_hist0(const uint32_t* keys, uint32_t n, uint32_t* counts, hipStream_t s) {
+static hipError_t tile_hist0(const uint32_t* keys, uint32_t n, uint32_t* counts, hipStream_t s, Gate g = Gate{}) {
     if (!n) return hipSuccess;
-    RT_KLAUNCH(k_tile_hist<0>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, keys, n, counts);
+    RT_KLAUNCH(k_tile_hist<0>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, keys, n, counts, g);
     return hipGetLastError();
+}
+
+hipError_t launch_digit_hist(const uint32_t* keys, uint32_t n, uint32_t* ghist, hipStream_t s) {
+    return digit_hist(keys, n, ghist, s);
+}
+
+hipError_t launch_tile_hist0(const uint32_t* keys, uint32_t n, uint32_t* counts, hipStream_t s) {
+    return tile_hist0(keys, n, counts, s);
 }
 
 template <int SHIFT>
 static void scatter_pass(const uint32_t* ki, const uint32_t* vi, uint32_t* ko, uint32_t* vo, uint32_t n,
-                         const uint32_t* gh, uint32_t* counts, hipStream_t s) {
+                         const uint32_t* gh, uint32_t* counts, hipStream_t s, Gate g = Gate{}) {
     const uint32_t nt = sort_tiles(n);
     if (nt <= kPrefixInKernelMaxTiles) {
-        RT_KLAUNCH((k_scatter<SHIFT, true>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
+        RT_KLAUNCH((k_scatter<SHIFT, true>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts, g);
     } else {
-        RT_KLAUNCH(k_scan_tiles, dim3(256), dim3(256), 0, s, counts, nt);
-        RT_KLAUNCH((k_scatter<SHIFT, false>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts);
+        RT_KLAUNCH(k_scan_tiles, dim3(256), dim3(256), 0, s, counts, nt, g);
+        RT_KLAUNCH((k_scatter<SHIFT, false>), dim3(nt), dim3(kSortThreads), 0, s, ki, vi, ko, vo, n, gh, counts, g);
     }
+}
+
+static hipError_t sort_lsb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
+                           uint32_t* counts[4], hipStream_t s, Gate g = Gate{}) {
+    if (n <= 1) return hipSuccess;
+    const uint32_t nt = sort_tiles(n);
+    scatter_pass<0>(keys[0], vals[0], keys[1], vals[1], n, ghist + 0, counts[0], s, g);
+    RT_KLAUNCH(k_tile_hist<8>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[1], g);
+    scatter_pass<8>(keys[1], vals[1], keys[0], vals[0], n, ghist + 256, counts[1], s, g);
+    RT_KLAUNCH(k_tile_hist<16>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], n, counts[2], g);
+    scatter_pass<16>(keys[0], vals[0], keys[1], vals[1], n, ghist + 512, counts[2], s, g);
+    RT_KLAUNCH(k_tile_hist<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[3], g);
+    scatter_pass<24>(keys[1], vals[1], keys[0], vals[0], n, ghist + 768, counts[3], s, g);
+    return hipGetLastError();
 }
 
 // 4 passes, ping-pong 0->1->0->1->0.  Needs: ghist [4][256] (all digits) and
 // counts0 = pass-0 tile counts; counts[1..3] are scratch of ntiles*256 words.
 hipError_t launch_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts[4],
                        hipStream_t s) {
-    if (n <= 1) return hipSuccess;
-    const uint32_t nt = sort_tiles(n);
-    scatter_pass<0>(keys[0], vals[0], keys[1], vals[1], n, ghist + 0, counts[0], s);
-    RT_KLAUNCH(k_tile_hist<8>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[1]);
-    scatter_pass<8>(keys[1], vals[1], keys[0], vals[0], n, ghist + 256, counts[1], s);
-    RT_KLAUNCH(k_tile_hist<16>, dim3(nt), dim3(kSortThreads), 0, s, keys[0], n, counts[2]);
-    scatter_pass<16>(keys[0], vals[0], keys[1], vals[1], n, ghist + 512, counts[2], s);
-    RT_KLAUNCH(k_tile_hist<24>, dim3(nt), dim3(kSortThreads), 0, s, keys[1], n, counts[3]);
-    scatter_pass<24>(keys[1], vals[1], keys[0], vals[0], n, ghist + 768, counts[3], s);
-    return hipGetLastError();
+    return sort_lsb(keys, vals, n, ghist, counts, s);
 }
 
 static hipError_t ensure_big_attr() {
@@ -850,34 +882,53 @@ static hipError_t ensure_big_attr() {
 }
 
 hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
-                           uint32_t* bstart, uint32_t* scratch, hipStream_t s) {
+                           uint32_t* bstart, uint32_t* scratch, hipStream_t s, uint32_t* dense) {
     if (n <= 1) return hipSuccess;
     const uint32_t nt = sort_tiles(n);
     if (n > kMsbBigMaxN) return hipErrorInvalidValue;
+    const uint32_t cap = msb_bucket_cap(n);
+    const Gate g{dense, 0u};  // with dense: the MSB kernels run only when no bucket outgrew cap
     if (n <= kMsbMaxN) {
-        RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart);
+        RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, counts, nt, ghist, bstart, cap, dense);
     } else {
         if (!scratch) return hipErrorInvalidValue;
         const uint32_t nch = sdiv(nt, kMsbChunk);
         RT_KLAUNCH(k_msb_chunk_sum, dim3(nch), dim3(1024), 0, s, counts, nt, scratch);
         // the chunk sums' exclusive scan from the bucket starts is k_msb_scan's
         // job on a [chunk][1024] table (nch <= 512: n <= 67M)
-        RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, scratch, nch, ghist, bstart);
+        RT_KLAUNCH(k_msb_scan, dim3(kMsbBuckets / 64), dim3(1024), 0, s, scratch, nch, ghist, bstart, cap, dense);
         RT_KLAUNCH(k_msb_chunk_apply, dim3(nch), dim3(1024), 0, s, counts, nt, scratch);
     }
     if (n <= kMsbMaxN) {
-        RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts);
+        RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts,
+                   g);
         RT_KLAUNCH(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
-                   bstart);
+                   bstart, g);
     } else {
         const hipError_t e = ensure_big_attr();
         if (e != hipSuccess) return e;
         RT_KLAUNCH(k_msb_scatter_big, dim3(sdiv(n, kScatterBigTile)), dim3(1024), kScatterBigLds, s, keys[0], vals[0],
-                   keys[1], vals[1], n, counts);
+                   keys[1], vals[1], n, counts, g);
         RT_KLAUNCH(k_bucket_sort_big, dim3(kMsbBuckets), dim3(kBigThreads), kBigLds, s, keys[1], vals[1], keys[0],
-                   vals[0], bstart);
+                   vals[0], bstart, g);
     }
     return hipGetLastError();
+}
+
+hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
+                             uint32_t* counts, uint32_t* bstart, uint32_t* scratch, uint32_t* ghist4,
+                             uint32_t* dense, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    hipError_t e = launch_sort_msb(keys, vals, n, ghist, counts, bstart, scratch, s, dense);
+    if (e != hipSuccess) return e;
+    // dense: keys[0]/vals[0] are still K1's; the MSB counts are spent, so the
+    // LSB passes reuse their words ([4][tile][256] = [tile][1024])
+    const Gate g{dense, 1u};
+    const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
+    uint32_t* c4[4] = {counts, counts + cs, counts + 2 * cs, counts + 3 * cs};
+    if ((e = digit_hist(keys[0], n, ghist4, s, g)) != hipSuccess) return e;
+    if ((e = tile_hist0(keys[0], n, c4[0], s, g)) != hipSuccess) return e;
+    return sort_lsb(keys, vals, n, ghist4, c4, s, g);
 }
 
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
