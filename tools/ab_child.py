@@ -70,6 +70,24 @@ if "shadow" in modes:
 if "path" in modes:
     out["path"] = med(lambda: s.render_path_device(cam, w, h, spp, (2.0, 3.0, -2.0), 0.3, 2, d_rgba=img.data_ptr(), timed=True), 4)
     out["crc_path"] = crc(img)
+for key in (2, 4, 5):  # another BASELINE config's full frame (static camera, tile order on)
+    if f"c{key}" not in modes:
+        continue
+    import bench  # noqa: E402
+    from gpu_raytracer_amd import scenes as S  # noqa: E402
+    cf = S.CONFIGS[key]
+    vw = S.VIEWS[cf.scene]
+    sc = bench.make_scene(R, S, cf)
+    sc.build()
+    cc = R.camera_look_at(vw.eye, vw.at, vw.up, vw.vfov, cf.w, cf.h)
+    im = torch.zeros(cf.w * cf.h, dtype=torch.int32, device="cuda")
+    hh = torch.zeros(cf.w * cf.h * cf.spp * 4, dtype=torch.float32, device="cuda")
+    f = lambda: sc.render_device(cc, cf.w, cf.h, cf.spp, d_rgba=im.data_ptr(), d_hits=hh.data_ptr(), timed=True)
+    f()
+    out[f"c{key}"] = med(f, 6)
+    out[f"crc_c{key}"] = crc(im, hh)
+    sc.close()
+    del im, hh
 if "work" in modes:  # wide records and triangle records fetched by the primary frame
     wk = s.render_work(cam, w, h, spp)
     out["records"], out["tri_records"] = float(wk[0]), float(wk[1])
