@@ -16,6 +16,7 @@ import bench  # noqa: E402
 
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+rebuild = os.environ.get("AB_REBUILD", "0") == "1"  # rebuild the BVH before every timed frame, as bench.py does
 configs = [("base", {})]
 for a in sys.argv[3:]:
     name, kv = a.split(":", 1)
@@ -27,15 +28,21 @@ scene = R.Scene.generate_soup(1_000_000, 1)
 scene.build()
 cams = [R.camera_look_at(bench.orbit_view(view, i), view.at, view.up, view.vfov, w, h) for i in range(frames + 2)]
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+hits = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
+hp = hits.data_ptr() if os.environ.get("AB_HITS", "0") == "1" else None  # the bench writes hit records too
 defaults = {}
 res = {n: [] for n, _ in configs}
 for _ in range(rounds):
     for name, kv in configs:
         for k, v in kv.items():
             R.config_set(k, v)
-        scene.render_device(cams[0], w, h, spp, d_rgba=img.data_ptr(), timed=True)  # this shape's first frame
-        scene.render_device(cams[1], w, h, spp, d_rgba=img.data_ptr(), timed=True)
-        t = [scene.render_device(cams[2 + i], w, h, spp, d_rgba=img.data_ptr(), timed=True) for i in range(frames)]
+        scene.render_device(cams[0], w, h, spp, d_rgba=img.data_ptr(), d_hits=hp, timed=True)  # this shape's first frame
+        scene.render_device(cams[1], w, h, spp, d_rgba=img.data_ptr(), d_hits=hp, timed=True)
+        t = []
+        for i in range(frames):
+            if rebuild:  # the bench's step: a build before every frame
+                scene.build()
+            t.append(scene.render_device(cams[2 + i], w, h, spp, d_rgba=img.data_ptr(), d_hits=hp, timed=True))
         res[name].append(float(np.mean(t)))
         for k in kv:  # back to the library defaults
             R.config_set(k, {"trace.coop_cap": -1, "trace.tile_order": 1, "trace.px_sort": 1, "trace.wg": 256,
