@@ -991,10 +991,30 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
     constexpr uint32_t T = kRefitT;
     extern __shared__ __attribute__((aligned(16))) unsigned char s_raw[];
     Aabb* tree = reinterpret_cast<Aabb*>(s_raw);
+    uint32_t pre[kCrossShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (uint32_t sh = 0; sh < kCrossShards; ++sh) pre[sh + 1] = pre[sh] + cross_ctr[sh];
+    const uint32_t count = pre[kCrossShards];
+    auto node_of = [&](uint32_t q) {
+        uint32_t sh = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kCrossShards; ++j) sh += (q >= pre[j]) ? 1u : 0u;
+        return cross[sh * cross_cap + (q - pre[sh])];
+    };
+    // a thread's first node is usually its only one (~20K crossing nodes at
+    // 1M): its list entry and topology word are loaded while the block builds
+    // its LDS tree, which does not depend on them (two dependent round trips
+    // off the critical path)
+    const uint32_t q0 = blockIdx.x * 256 + threadIdx.x;
+    uint32_t i0 = q0 < count ? node_of(q0) : 0u;
     uint32_t P = 1;
     while (P < m) P <<= 1;
     if (LDS_TREE) {
         for (uint32_t j = threadIdx.x; j < P; j += 256) tree[P + j] = j < m ? load_aabb(table, j) : aabb_empty();
+    }
+    uint4 tp0 = q0 < count ? topo[i0] : make_uint4(0u, 0u, 0u, 0u);
+    if (LDS_TREE) {
         __syncthreads();
         for (uint32_t len = P >> 1; len >= 1; len >>= 1) {
             for (uint32_t j = threadIdx.x; j < len; j += 256) {
@@ -1005,17 +1025,9 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
             __syncthreads();
         }
     }
-    uint32_t pre[kCrossShards + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (uint32_t sh = 0; sh < kCrossShards; ++sh) pre[sh + 1] = pre[sh] + cross_ctr[sh];
-    const uint32_t count = pre[kCrossShards];
-    for (uint32_t q = blockIdx.x * 256 + threadIdx.x; q < count; q += gridDim.x * 256) {
-        uint32_t sh = 0;
-#pragma unroll
-        for (uint32_t j = 1; j < kCrossShards; ++j) sh += (q >= pre[j]) ? 1u : 0u;
-        const uint32_t i = cross[sh * cross_cap + (q - pre[sh])];
-        const uint4 tp = topo[i];
+    for (uint32_t q = q0; q < count; q += gridDim.x * 256) {
+        const uint32_t i = q == q0 ? i0 : node_of(q);
+        const uint4 tp = q == q0 ? tp0 : topo[i];
         const uint32_t l = tp.z, r = tp.w;
         if (l >= n || r >= n || l > r) continue;  // malformed topology: never read out of bounds
         Aabb box = load_aabb(sufbuf, l);
