@@ -1215,6 +1215,17 @@ static hipError_t ensure_cross_attr() {
 #ifndef RT_WCROSS_GRID
 #define RT_WCROSS_GRID 256
 #endif
+// Crossing nodes are short chains of dependent loads, one node per thread
+// at a time: a grid that gives every node its own thread (about 11 per refit
+// block: ~2 above the block level and ~log2(kRefitT) straddling each block
+// boundary) instead of looping over them.
+#ifndef RT_XGRID_PER_BLOCK
+#define RT_XGRID_PER_BLOCK 12
+#endif
+static uint32_t cross_grid(uint32_t m, uint32_t floor_blocks) {
+    return std::min<uint32_t>(4096u, std::max<uint32_t>(floor_blocks, cdiv(RT_XGRID_PER_BLOCK * m, 256)));
+}
+
 static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
                                 hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
@@ -1231,14 +1242,14 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
         const uint32_t L = sparse_levels(m);
         RT_KLAUNCH(k_sparse_near, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table, m, L);
         if (L > kSparseNear + 1) RT_KLAUNCH(k_sparse_far, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table, m, L);
-        RT_KLAUNCH(k_refit_cross<false>, dim3(256), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
+        RT_KLAUNCH(k_refit_cross<false>, dim3(cross_grid(m, 256)), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     if (arity == 8)
-        RT_KLAUNCH(k_wide_cross<8>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+        RT_KLAUNCH(k_wide_cross<8>, dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
                            cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     else
-        RT_KLAUNCH(k_wide_cross<4>, dim3(RT_WCROSS_GRID), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
+        RT_KLAUNCH(k_wide_cross<4>, dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
                            cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
     return hipGetLastError();
 }
