@@ -436,7 +436,7 @@ __device__ __forceinline__ void msb_scatter_tile(const uint32_t* __restrict__ ki
                                                  uint32_t* s_start, uint32_t* s_gofs, uint32_t* s_sw) {
     constexpr int W = NT / 64;
     constexpr uint32_t TILE = (uint32_t)NT * P;
-    static_assert(W * kMsbBuckets <= 2 * (int)TILE, "counters and bucketed tile share one buffer");
+    // s_buf holds max(W * 1024 counters, the bucketed tile's 2 * TILE words)
     uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_buf);
     uint32_t* s_key = s_buf;
     uint32_t* s_val = s_buf + TILE;
@@ -487,21 +487,29 @@ __device__ __forceinline__ void msb_scatter_tile(const uint32_t* __restrict__ ki
     }
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_msb_scatter(const uint32_t* __restrict__ kin,
+#ifndef RT_MSB_SCATTER_NT
+#define RT_MSB_SCATTER_NT 512
+#endif
+constexpr int kMsbScatterNT = RT_MSB_SCATTER_NT;  // threads per 4096-key tile
+static_assert(kSortTile % kMsbScatterNT == 0, "a tile is whole items per thread");
+constexpr uint32_t kMsbScatterBuf = (kMsbScatterNT / 64) * kMsbBuckets > 2 * kSortTile
+                                        ? (kMsbScatterNT / 64) * kMsbBuckets : 2 * kSortTile;
+__global__ __launch_bounds__(kMsbScatterNT) void k_msb_scatter(const uint32_t* __restrict__ kin,
                                                               const uint32_t* __restrict__ vin,
                                                               uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                               uint32_t n, const uint32_t* __restrict__ offs, Gate gate = Gate{}) {
     if (gated_off(gate)) return;
-    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // ranking counters s_wc[W][1024], then the bucketed tile
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[kMsbScatterBuf];  // ranking counters s_wc[W][1024], then the bucketed tile
     __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
     __shared__ uint32_t s_gofs[kMsbBuckets];
-    __shared__ uint32_t s_sw[kSortThreads / 64];
-    msb_scatter_tile<kSortThreads, kSortItems>(kin, vin, kout, vout, n, offs, s_buf, s_start, s_gofs, s_sw);
+    __shared__ uint32_t s_sw[kMsbScatterNT / 64];
+    msb_scatter_tile<kMsbScatterNT, kSortTile / kMsbScatterNT>(kin, vin, kout, vout, n, offs, s_buf, s_start, s_gofs, s_sw);
 }
 
 constexpr int kScatterBigItems = 16;
 constexpr uint32_t kScatterBigTile = 1024u * kScatterBigItems;  // 4 sort tiles
 constexpr size_t kScatterBigLds = (size_t)2 * kScatterBigTile * 4 + (size_t)kMsbBuckets * 4 * 2 + 64;
+static_assert(16 * kMsbBuckets <= 2 * (int)kScatterBigTile, "the big scatter's counters fit its tile buffer");
 __global__ __launch_bounds__(1024) void k_msb_scatter_big(const uint32_t* __restrict__ kin,
                                                           const uint32_t* __restrict__ vin,
                                                           uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
@@ -900,7 +908,7 @@ hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, con
         RT_KLAUNCH(k_msb_chunk_apply, dim3(nch), dim3(1024), 0, s, counts, nt, scratch);
     }
     if (n <= kMsbMaxN) {
-        RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kSortThreads), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts,
+        RT_KLAUNCH(k_msb_scatter, dim3(nt), dim3(kMsbScatterNT), 0, s, keys[0], vals[0], keys[1], vals[1], n, counts,
                    g);
         RT_KLAUNCH(k_bucket_sort, dim3(kMsbBuckets), dim3(kBucketThreads), 0, s, keys[1], vals[1], keys[0], vals[0],
                    bstart, g);
