@@ -36,7 +36,7 @@ EXPORTED = [
     "rt_scene_from_soup", "rt_scene_load_obj", "rt_scene_generate_soup", "rt_scene_load_soup",
     "rt_scene_save_soup", "rt_bvh_save", "rt_bvh_load", "rt_scene_num_tris",
     "rt_scene_get_tris", "rt_scene_set_device", "rt_scene_free", "rt_camera_look_at", "rt_bvh_build",
-    "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_bvh_wide_arity", "rt_render", "rt_render_counters",
+    "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_bvh_wide_arity", "rt_render", "rt_render_timed", "rt_render_counters",
     "rt_render_work", "rt_render_device",
     "rt_render_shadow", "rt_render_shadow_device", "rt_render_shadow_work",
     "rt_render_path", "rt_render_path_device", "rt_render_path_work",
@@ -109,7 +109,8 @@ def lib() -> C.CDLL:
         "rt_bvh_read": [P, P, P, P, P, P],
         "rt_bvh_read_wide": [P, P],
         "rt_bvh_wide_arity": [P, C.POINTER(u32)],
-        "rt_render": [P, cam, u32, u32, u32, u32, P, P, C.POINTER(dbl)],
+        "rt_render": [P, cam, u32, u32, u32, u32, P, P],
+        "rt_render_timed": [P, cam, u32, u32, u32, u32, P, P, C.POINTER(dbl)],
         "rt_render_counters": [P, cam, u32, u32, u32, P],
         "rt_render_work": [P, cam, u32, u32, u32, P],
         "rt_render_shadow": [P, cam, P, C.c_float, u32, u32, u32, P, P, C.POINTER(dbl)],

@@ -1118,8 +1118,8 @@ rt_status render_tiled(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h
 
 extern "C" {
 
-rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
-                    rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
+rt_status rt_render_timed(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
+                          rt_hit* hits_out, uint8_t* rgba_out, double* ms_out) {
     RtRange range_("rt_render");
     if (!s || !cam) return fail(RT_EINVAL, "bad render arguments");
     RTR(check_frame(w, h, spp));
@@ -1153,6 +1153,13 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
     if (hits_out) HIPR(hipMemcpy(hits_out, r->d_hits, nh * 16, hipMemcpyDeviceToHost));
     if (rgba_out) HIPR(hipMemcpy(rgba_out, r->d_rgba, (size_t)w * h * 4, hipMemcpyDeviceToHost));
     return RT_OK;
+}
+
+// SURVEY.md §8(b)'s prototype exactly (SURVEY.md:291-292): the timed form
+// without its device-time output.
+rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
+                    rt_hit* hits_out, uint8_t* rgba_out) {
+    return rt_render_timed(s, cam, w, h, spp, ngpus, hits_out, rgba_out, nullptr);
 }
 
 // Shared shape of the *_device entry points: launch `fn` on the caller's

@@ -290,7 +290,7 @@ int main(int argc, char** argv) {
         uint8_t* ro = last && !a.dump.empty() ? rgba.data() : nullptr;
         double t = 0.0;
         if (a.mode == "primary")
-            RT_OR_FAIL(rt_render(s, &cam, a.w, a.h, a.spp, a.gpus, ho, ro, &t));
+            RT_OR_FAIL(rt_render_timed(s, &cam, a.w, a.h, a.spp, a.gpus, ho, ro, &t));
         else if (a.mode == "shadow")
             RT_OR_FAIL(rt_render_shadow(s, &cam, light, 0.2f, a.w, a.h, a.spp, ho, ro ? ro : rgba.data(), &t));
         else

@@ -867,12 +867,17 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                uint16_t* __restrict__ px_cost = nullptr,
                                                uint32_t coop_cap = 0, CoopQ cq = CoopQ{},
                                                OrderFold fold = OrderFold{}) {
-    __shared__ uint32_t s_ref[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
-    __shared__ uint16_t s_tn[(WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1];
+    // PX: the per-pixel order (below); its ranking borrows s_ref, so the
+    // binary instance (no stack) still sizes s_ref for tile_pixel_order
+    constexpr bool PX = !SHADOW && !COUNT && NT == 256;
+    constexpr uint32_t kStackWords = (WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1u;
+    constexpr uint32_t kRefWords = (PX && kStackWords < 144u) ? 144u : kStackWords;
+    __shared__ uint32_t s_ref[kRefWords];
+    __shared__ uint16_t s_tn[kStackWords];
     const uint32_t spp = SPPC ? (uint32_t)SPPC : spp_in;
     if constexpr (!PACKED && !SHADOW && !COUNT && NT == 256 && (WIDE || SHADOW)) {
         if (fold.out && blockIdx.x == gridDim.x - 1) {  // uniform: the extra block sorts and leaves
-            static_assert((WideFmt<WA>::stack + 1) * NT >= 256 + 16, "tile_order_block's LDS");
+            static_assert(sizeof(s_ref) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
             tile_order_block<256, kFoldPerThread>(fold.cost, fold.nb, fold.out, s_ref, s_ref + 256, fold.ema);
             return;
         }
@@ -895,10 +900,9 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     // counts, so the tile's expensive rays share a wave instead of
     // stretching all four.  Primary-ray full frames only: compiled out of the
     // shadow, counting and 64-thread variants, whose registers it would cost.
-    constexpr bool PX = !SHADOW && !COUNT && NT == 256;
     uint32_t lx = (w & 1) * 8 + (l & 7), ly = (w >> 1) * 8 + (l >> 3);
     if (PX && px_prev) {  // uniform: the whole block
-        static_assert((WideFmt<WA>::stack + 1) * NT >= 144, "tile_pixel_order's LDS");
+        static_assert(!PX || sizeof(s_ref) >= 144 * sizeof(uint32_t), "tile_pixel_order's LDS");
         const uint32_t li = tile_pixel_order(px_prev + (uint64_t)slot * 256, threadIdx.x, s_ref);
         lx = li & 15;
         ly = li >> 4;

@@ -182,7 +182,7 @@ class Scene:
         hb = np.zeros(w * h * spp, HIT_DTYPE) if hits else None
         rb = np.zeros(w * h * 4, np.uint8) if rgba else None
         ms = C.c_double()
-        call("rt_render", self._h, C.byref(cam), w, h, spp, int(ngpus), _p(hb) if hits else None,
+        call("rt_render_timed", self._h, C.byref(cam), w, h, spp, int(ngpus), _p(hb) if hits else None,
              _p(rb) if rgba else None, C.byref(ms))
         return hb, rb, ms.value
 

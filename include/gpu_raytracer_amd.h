@@ -152,9 +152,13 @@ rt_status rt_bvh_wide_arity(const rt_scene* s, uint32_t* arity_out);
  * the primary with RCCL (ncclGather over xGMI, one communicator per device
  * list, cached on the scene) and unpacked there.  ngpus > visible devices ->
  * RT_EDEVICE; RCCL failures -> RT_ECOMM.  The image and hits are identical
- * for every ngpus.  ms_out: device time of the frame (trace .. unpack). */
+ * for every ngpus.  Exactly SURVEY.md §8(b)'s prototype (SURVEY.md:291-292). */
 rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
-                    rt_hit* hits_out, uint8_t* rgba_out, double* ms_out);
+                    rt_hit* hits_out, uint8_t* rgba_out);
+/* rt_render plus ms_out (nullable): device time of the frame (trace ..
+ * unpack), from events on the stream the kernels run on. */
+rt_status rt_render_timed(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp, uint32_t ngpus,
+                          rt_hit* hits_out, uint8_t* rgba_out, double* ms_out);
 /* deterministic work counters of a render with the §9.7 binary traversal
  * (the oracle's counters): [0] nodes fetched, [1] tris tested */
 rt_status rt_render_counters(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,

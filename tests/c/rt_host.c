@@ -39,8 +39,11 @@ int main(int argc, char** argv) {
     uint8_t* rgba = (uint8_t*)malloc((size_t)w * h * 4);
     rt_hit* hits = (rt_hit*)malloc((size_t)w * h * spp * sizeof(rt_hit));
     if (!rgba || !hits) return 3;
+    /* SURVEY.md §8(b)'s rt_render; rt_render_timed (NULL outputs) then times the same frame */
+    if ((st = rt_render(s, &cam, w, h, spp, ngpus, hits, rgba)) != RT_OK) return die("rt_render", st);
     double frame_ms = 0.0;
-    if ((st = rt_render(s, &cam, w, h, spp, ngpus, hits, rgba, &frame_ms)) != RT_OK) return die("rt_render", st);
+    if ((st = rt_render_timed(s, &cam, w, h, spp, ngpus, NULL, NULL, &frame_ms)) != RT_OK)
+        return die("rt_render_timed", st);
     FILE* f = fopen(argv[7], "wb");
     if (!f || fwrite(rgba, 1, (size_t)w * h * 4, f) != (size_t)w * h * 4) return 3;
     fclose(f);

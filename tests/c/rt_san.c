@@ -171,8 +171,9 @@ static void test_no_device(void) {
     EXPECT(rt_camera_look_at(eye, at, up, 45.0, 32, 32, &cam) == RT_OK);
     rt_hit* hits = (rt_hit*)malloc(32 * 32 * sizeof(rt_hit));
     uint8_t* rgba = (uint8_t*)malloc(32 * 32 * 4);
-    EXPECT(rt_render(s, &cam, 32, 32, 1, 1, hits, rgba, &ms) != RT_OK);
-    EXPECT(rt_render(s, &cam, 32, 32, 1, 4, hits, rgba, &ms) != RT_OK);
+    EXPECT(rt_render(s, &cam, 32, 32, 1, 1, hits, rgba) != RT_OK);
+    EXPECT(rt_render_timed(s, &cam, 32, 32, 1, 1, hits, rgba, &ms) != RT_OK);
+    EXPECT(rt_render_timed(s, &cam, 32, 32, 1, 4, hits, rgba, &ms) != RT_OK);
     EXPECT(rt_bvh_save(s, path_of("x.rtbvh")) != RT_OK);
     EXPECT(rt_bvh_load(s, path_of("x.rtbvh")) != RT_OK);
     float b9[9];

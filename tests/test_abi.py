@@ -118,6 +118,31 @@ def test_invalid_arguments(rt):
         assert e.value.status == (-1 if rt.device_count() else -4)
 
 
+def test_render_prototype_is_survey_8b(rt):
+    """rt_render is exactly SURVEY.md §8(b)'s prototype (SURVEY.md:291-292):
+    (scene, cam, w, h, spp, ngpus, hits_out, rgba_out) -- 8 parameters, no
+    timing output (that is rt_render_timed's ninth)."""
+    import os
+    import re
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "gpu_raytracer_amd.h")).read()
+
+    def proto(name):
+        m = re.search(r"rt_status\s+" + name + r"\s*\(([^)]*)\)\s*;", hdr)
+        assert m, name
+        return [" ".join(a.split()) for a in m.group(1).split(",")]
+
+    assert proto("rt_render") == [
+        "rt_scene* s", "const rt_camera* cam", "uint32_t w", "uint32_t h", "uint32_t spp", "uint32_t ngpus",
+        "rt_hit* hits_out", "uint8_t* rgba_out"]
+    assert proto("rt_render_timed") == proto("rt_render") + ["double* ms_out"]
+    # called with exactly 8 arguments: without a GPU it refuses (RT_EDEVICE)
+    # before touching the NULL scene's device
+    cam = rt.camera_look_at((0, 0, -1), (0, 0, 0), (0, 1, 0), 45, 8, 8)
+    with rt.Scene.from_soup(np.zeros((3, 9), np.float32)) as s:
+        st = rt._lib.lib().rt_render(s._h, __import__("ctypes").byref(cam), 8, 8, 1, 1, None, None)
+        assert st == (-1 if rt.device_count() else -4)
+
+
 def test_render_ngpus_beyond_visible_devices(rt):
     """rt_render(ngpus > visible devices) -> RT_EDEVICE (SURVEY.md §8(b):
     multi-GPU is internal to rt_render), checked before any device work."""

@@ -387,6 +387,39 @@ def test_tile_order_successive_frames(R, oracle, px_sort):
         R.config_set("trace.px_sort", 1)
 
 
+@pytest.mark.parametrize("n", [1, 5000])
+def test_binary_variant_pixel_order_frames(R, oracle, n):
+    """The binary k_trace instance (trace.variant = 2, and every scene with
+    n < 2) has no traversal stack, yet its 256-thread full-frame blocks run the
+    per-pixel order from the 2nd frame of an unchanged camera: its ranking
+    LDS must be sized for it.  Three frames of one camera,
+    each == the oracle."""
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    if n == 1:  # one large triangle across the view: hits and misses in every tile row
+        tris = np.array([[0.1, 0.05, 0.5, 0.95, 0.3, 0.45, 0.35, 0.9, 0.55]], np.float32)
+    else:
+        tris = soup(oracle, n, 21)
+    exp = oracle.build(tris)
+    w, h, spp = 160, 96, 1
+    ocam = oracle.camera_look_at(SOUP_VIEW.eye, SOUP_VIEW.at, SOUP_VIEW.up, SOUP_VIEW.vfov, w, h)
+    eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
+    er = oracle.shade(eh, w, h, spp)
+    R.config_set("trace.variant", 2)
+    R.config_set("trace.tile_order", 1)
+    R.config_set("trace.px_sort", 1)
+    try:
+        with R.Scene.from_soup(tris) as s:
+            s.build()
+            cam = _cam(R, SOUP_VIEW, w, h)
+            for _ in range(3):
+                hits, rgba, _ = s.render(cam, w, h, spp)
+                assert np.array_equal(rgba, er)
+                assert np.array_equal(hits["prim"], eh["prim"])
+                assert np.array_equal(bits(hits["t"]), bits(eh["t"]))
+    finally:
+        R.config_set("trace.variant", 0)
+
+
 def _successive_frames(R, oracle, s_tris, exp):
     import torch
     from gpu_raytracer_amd.scenes import SOUP_VIEW
