@@ -25,6 +25,7 @@
 //                       so the result is independent of evaluation order.
 #include "rt_device.h"
 #include "rt_launch.h"
+#include "sort_device.h"
 
 #include <mutex>
 
@@ -245,6 +246,88 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
     for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) {
         const uint32_t v = hist[j];
         if (v) atomicAdd(&ghist[j], v);
+    }
+}
+
+// K1 + the first level of the gather sort (r04, sort_kernels.hip "tile-bucketed
+// gather sort"): the block's 4096 Morton keys are also sorted, stably, by
+// bucket d = key >> 20 inside the tile -- the index order is (wave, item,
+// lane), which is rank10's order -- and written bucket by bucket to
+// keys_tb/vals_tb[tile * 4096 ..], with tb[tile][d] = run start | run length
+// << 16 and the global bucket totals in ghist[1024].  No global prefix over
+// tiles exists: each bucket's block gathers its runs from every tile.
+__global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
+                                                            BuildParams* __restrict__ params,
+                                                            const float* __restrict__ partials, uint32_t nb,
+                                                            uint32_t* __restrict__ keys_tb, uint32_t* __restrict__ vals_tb,
+                                                            uint32_t* __restrict__ ghist /* [1024] */,
+                                                            uint32_t* __restrict__ tb /* [tile][1024] */) {
+    constexpr int W = kSortThreads / 64;
+    static_assert(W * kMsbBuckets <= 2 * kSortTile, "the ranking counters fit the bucketed tile's buffer");
+    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // s_wc[W][1024], then keys | vals
+    __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
+    __shared__ float red[W][6];
+    __shared__ uint32_t s_sw[W];
+    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_buf);
+    for (uint32_t j = threadIdx.x; j < W * kMsbBuckets / 4; j += kSortThreads)
+        reinterpret_cast<uint4*>(s_buf)[j] = make_uint4(0, 0, 0, 0);
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t tile = blockIdx.x, tbase = tile * (uint32_t)kSortTile;
+    const uint32_t wbase = tbase + w * 64u * kTrisPerThread;
+    float t[kTrisPerThread][9];
+    const uint32_t okm = load_tri_lanes(tris, n, wbase, t);  // in flight while the bounds are reduced
+    const BuildParams p = bounds_final<kSortThreads>(partials, nb, red);  // ends with a barrier
+    if (tile == 0 && threadIdx.x == 0) *params = p;
+    uint32_t k8[kTrisPerThread], dg[kTrisPerThread], r[kTrisPerThread];
+    bool ok[kTrisPerThread];
+#pragma unroll
+    for (uint32_t q = 0; q < kTrisPerThread; ++q) {
+        float bmin[3], bmax[3];
+        tri_bounds(t[q], bmin, bmax);
+        uint32_t qq[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
+        k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
+        dg[q] = k8[q] >> kMsbShift;  // 30-bit keys: < 1024
+        ok[q] = (okm >> q) & 1u;
+    }
+    rank10<kTrisPerThread>(dg, ok, s_wc, r);
+    __syncthreads();
+    wave_prefix4<W, kSortThreads>(s_wc, s_start);
+    __syncthreads();
+    constexpr int PER = kMsbBuckets / kSortThreads;  // buckets per thread in scan1024's layout
+    uint32_t cnt[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) cnt[j] = s_start[threadIdx.x * PER + j];
+    scan1024<kSortThreads>(s_start, s_sw);  // ends with a barrier
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t d = threadIdx.x * PER + j;
+        tb[(uint64_t)tile * kMsbBuckets + d] = s_start[d] | (cnt[j] << 16);
+        if (cnt[j]) atomicAdd(&ghist[d], cnt[j]);
+    }
+    uint32_t pos[kTrisPerThread];
+#pragma unroll
+    for (uint32_t q = 0; q < kTrisPerThread; ++q) pos[q] = s_start[dg[q]] + s_wc[w][dg[q]] + r[q];
+    __syncthreads();  // the counters are dead: the buffer becomes the bucketed tile
+    uint32_t* s_key = s_buf;
+    uint32_t* s_val = s_buf + kSortTile;
+#pragma unroll
+    for (uint32_t q = 0; q < kTrisPerThread; ++q)
+        if (ok[q]) {
+            s_key[pos[q]] = k8[q];
+            s_val[pos[q]] = wbase + q * 64u + lane;
+        }
+    __syncthreads();
+    const uint32_t trem = n - tbase;
+    const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
+#pragma unroll
+    for (uint32_t m = 0; m < kTrisPerThread; ++m) {
+        const uint32_t q = threadIdx.x + m * kSortThreads;
+        if (q < tcount) {
+            keys_tb[tbase + q] = s_key[q];
+            vals_tb[tbase + q] = s_val[q];
+        }
     }
 }
 
@@ -1346,13 +1429,21 @@ hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s) {
     return n ? launch_cross(b, n, config_snapshot().wide_collapse, b.warity, s) : hipSuccess;
 }
 
-bool build_uses_msb(const BuildBufs& b, uint32_t n) {
-    return n >= 2 && n <= kMsbBigMaxN && config_snapshot().sort_msb && b.sort_mode != 2;
+// The build's sort for this n and config: 0 = the 4-pass LSB sort, 1 = the
+// MSB scatter + bucket sort, 2 = the tile-bucketed gather sort (the default).
+// A scene whose first MSB/gather build found a bucket beyond one block's LDS
+// sort (sort_mode 2 for that sort) keeps the LSB sort.
+uint32_t build_sort_kind(const BuildBufs& b, uint32_t n, const TraceConfig& cfg) {
+    if (n < 2 || n > kMsbBigMaxN || cfg.sort_msb == 0) return 0;
+    if (cfg.sort_msb == 2 && !gather_sort_fits(n)) return 0;
+    if (b.sort_mode == 2 && b.sort_mode_of == cfg.sort_msb) return 0;
+    return cfg.sort_msb;
 }
 
-hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages) {
-    const TraceConfig cfg = config_snapshot();
+hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages,
+                        const TraceConfig& cfg, uint32_t* probed) {
     hipError_t e;
+    if (probed) *probed = 0;
     auto rec = [&](int i) -> hipError_t {
         return (ev && (stages || i == 0 || i == 6)) ? hipEventRecord(ev->e[i], s) : hipSuccess;
     };
@@ -1363,21 +1454,39 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
     if (!n) RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
-    const bool msb = n >= 2 && n <= kMsbBigMaxN && cfg.sort_msb && b.sort_mode != 2;
-    if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
-                                b.zero + kZHist, counts[0], s, msb)) != hipSuccess)
+    const uint32_t kind = build_sort_kind(b, n, cfg);
+    // the scene's first build with this sort: the verdict on its bucket sizes
+    // decides its later builds' sort (the host reads kZDense afterwards)
+    const bool probe = kind != 0 && !(b.sort_mode != 0 && b.sort_mode_of == kind);
+    if (kind == 2) {
+        if (n) RT_KLAUNCH(k_morton_tb, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params, b.partials,
+                          bounds_grid(n), b.keys[1], b.vals[1], b.zero + kZHist, b.counts);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
+                                       b.zero + kZHist, counts[0], s, kind == 1)) != hipSuccess) {
         return e;
+    }
     if ((e = rec(2)) != hipSuccess) return e;
     uint32_t* K[2] = {b.keys[0], b.keys[1]};
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
-    // scratch for the chunked tile scan (n > kMsbMaxN): the parent array, which
-    // the build does not write (ceil(tiles/32) x 1024 words <= 2n - 1)
-    if (msb && b.sort_mode == 0)  // the scene's first build: both sorts, gated on the bucket totals
+    if (kind == 2) {
+        // scratch of a bucket beyond one LDS sort: prebuf (6n words), which
+        // k_topo_refit writes only later
+        uint32_t* xk = reinterpret_cast<uint32_t*>(b.prebuf);
+        e = launch_sort_gather(K, V, n, b.zero + kZHist, b.counts, xk, xk + b.cap_n, b.counts, b.zero + kZHist4,
+                               probe ? b.zero + kZDense : nullptr, s);
+    } else if (kind == 1 && probe) {  // both sorts, gated on the bucket totals
+        // scratch for the chunked tile scan (n > kMsbMaxN): the parent array,
+        // which the build does not write (ceil(tiles/32) x 1024 words <= 2n - 1)
         e = launch_sort_probe(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, b.zero + kZHist4,
                               b.zero + kZDense, s);
-    else if (msb) e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, s);
-    else e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
+    } else if (kind == 1) {
+        e = launch_sort_msb(K, V, n, b.zero + kZHist, b.counts, b.bstart, b.parent, s);
+    } else {
+        e = launch_sort(K, V, n, b.zero + kZHist, counts, s);
+    }
     if (e != hipSuccess) return e;
+    if (probe && probed) *probed = kind;
     if ((e = rec(3)) != hipSuccess) return e;
     if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;

@@ -54,7 +54,7 @@ struct Replica {
     hipStream_t stream = nullptr;  // the replica's own stream (builds, synchronous renders)
     rt::BuildBufs bufs;
     bool uploaded = false, built = false;
-    bool msb_probe = false;  // this build decides the scene's sort (BuildBufs::sort_mode)
+    uint32_t msb_probe = 0;  // the sort (1 MSB, 2 gather) whose verdict this build wrote (BuildBufs::sort_mode)
     rt::BuildEvents ev;
     rt_build_times times{};
     // render scratch (grown on demand)
@@ -366,7 +366,11 @@ rt_status upload(const rt_scene* s, Replica& r) {
 // Build the BVH on every replica in `targets` concurrently (one stream each),
 // then wait for all; ms_out = the longest build.
 rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, double* ms_out) {
-    const bool stages = rt::config_snapshot().stage_events != 0;
+    // one config snapshot for every replica and both halves of the probe
+    // logic (a concurrent rt_config_set between two snapshots
+    // could make the host read a verdict no kernel wrote)
+    const rt::TraceConfig cfg = rt::config_snapshot();
+    const bool stages = cfg.stage_events != 0;
     for (Replica* r : targets) {
         RTR(upload(s, *r));
         HIPR(hipSetDevice(r->device));
@@ -375,8 +379,7 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         // a rebuild that fails half-way must not leave the old flag over a
         // half-written BVH: built again only after the synchronize below
         r->built = false;
-        r->msb_probe = r->bufs.sort_mode == 0 && rt::build_uses_msb(r->bufs, s->n);
-        hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages);
+        hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, &r->msb_probe);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
     }
     double worst = 0.0;
@@ -395,11 +398,12 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         float tot = 0;
         HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
         r->times.total = tot;
-        if (r->msb_probe) {  // the scene's first build ran both sorts gated on k_msb_scan's verdict: keep it
+        if (r->msb_probe) {  // the scene's first build with this sort ran both sorts gated on its verdict: keep it
             uint32_t dense = 0;
             HIPR(hipMemcpy(&dense, r->bufs.zero + rt::kZDense, 4, hipMemcpyDeviceToHost));
             r->bufs.sort_mode = dense ? 2u : 1u;
-            r->msb_probe = false;
+            r->bufs.sort_mode_of = r->msb_probe;
+            r->msb_probe = 0;
         }
         r->built = true;
         worst = std::max(worst, (double)tot);
@@ -509,7 +513,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.tile_order" && (value == 0 || value == 1)) c.tile_order = (uint32_t)value;
     else if (k == "trace.px_sort" && value >= 0 && value <= 2) c.px_sort = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
-    else if (k == "build.sort" && (value == 0 || value == 1)) c.sort_msb = (uint32_t)value;
+    else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
     else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;

@@ -41,11 +41,14 @@ struct BuildBufs {
     // sort (clustered geometry: that bucket is sorted by one block through
     // global memory, ~10x the build); a scene's triangles never change
     uint32_t sort_mode = 0;
+    uint32_t sort_mode_of = 0;  // the sort (build.sort 1 or 2) whose probe build set sort_mode
 };
 // keys one MSB bucket may hold for the LDS bucket sort at this n
 uint32_t msb_bucket_cap(uint32_t n);
-// whether launch_build(b, n) sorts with the MSB bucket sort
-bool build_uses_msb(const BuildBufs& b, uint32_t n);
+// the same for the gather sort, and whether it handles n at all
+uint32_t gather_bucket_cap(uint32_t n);
+bool gather_sort_fits(uint32_t n);
+struct TraceConfig;
 
 // zero region layout (uint32 words)
 constexpr uint32_t kZHist = 0;          // [4][256] digit histograms
@@ -65,8 +68,14 @@ struct BuildEvents { hipEvent_t e[7]; bool valid = false; };
 
 // K0..K7w on `stream` for the n tris already in b.tris.  Sorted keys/vals end
 // in keys[0]/vals[0].  With ev: e[0] and e[6] around the build, and e[1..5]
-// between the stages when `stages`.
-hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev, bool stages);
+// between the stages when `stages`.  cfg: the caller's one config snapshot.
+// probed (nullable): the sort (1 MSB, 2 gather) whose verdict this build
+// wrote to zero[kZDense] -- the caller reads it after the build to set
+// sort_mode/sort_mode_of -- else 0.
+hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev, bool stages,
+                        const TraceConfig& cfg, uint32_t* probed);
+// the sort launch_build would use: 0 LSB, 1 MSB scatter, 2 gather
+uint32_t build_sort_kind(const BuildBufs& b, uint32_t n, const TraceConfig& cfg);
 
 // K4..K7w alone (rt_stage_refit): sorted keys/vals already in keys[0]/vals[0]
 // and the soup in tris.
@@ -141,7 +150,8 @@ struct TraceConfig {
                                 // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t wide_arity = 4;    // build.wide_arity: 4 = K7w 64-B records, 8 = K7w8 96-B records (greedy cut)
-    uint32_t sort_msb = 1;      // build sort: 1 = MSB bucket sort for 2 <= n <= kMsbBigMaxN, 0 = 4-pass LSB always
+    uint32_t sort_msb = 2;      // build.sort, for 2 <= n <= kMsbBigMaxN: 2 = tile-bucketed gather sort (default),
+                                // 1 = MSB scatter + bucket sort, 0 = 4-pass LSB always
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
     uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
@@ -283,6 +293,16 @@ hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, con
 hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
                              uint32_t* counts, uint32_t* bstart, uint32_t* scratch, uint32_t* ghist4,
                              uint32_t* dense, hipStream_t s);
+// The tile-bucketed gather sort (sort_kernels.hip): keys[1]/vals[1] = K1's
+// (k_morton_tb) tile-bucketed keys, tb = its [tile][1024] run table, ghist =
+// its [1024] bucket totals -> keys[0]/vals[0].  xk/xv: n-word scratch for a
+// bucket beyond one LDS sort.  dense (a probe build): k_bucket_dense writes
+// the verdict there, the bucket kernel runs on 0 and the 4-pass LSB sort of
+// the tile-bucketed arrays on 1 (counts: the table's words, ghist4: [4][256]
+// zeroed words).
+hipError_t launch_sort_gather(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
+                              const uint32_t* tb, uint32_t* xk, uint32_t* xv, uint32_t* counts, uint32_t* ghist4,
+                              uint32_t* dense, hipStream_t s);
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
                            uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,

@@ -17,8 +17,10 @@
 // the measured chain cost ~2.5 us per hop on MI355X (tools/diag_stamps.py).
 #include "rt_device.h"
 #include "rt_launch.h"
+#include "sort_device.h"
 
 #include <algorithm>
+#include <cmath>
 #include <mutex>
 
 namespace rt {
@@ -26,10 +28,6 @@ namespace rt {
 #ifdef RT_STAMPS
 hipError_t read_stamps_sort(void* out, size_t bytes) { return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rt_stamps), bytes); }
 #endif
-
-__device__ __forceinline__ uint32_t sort_count_below(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
 
 // exclusive scan of one value per thread over threads [0,256) of a block of
 // kSortThreads (others pass 0); returns the prefix for threads < 256.
@@ -289,92 +287,6 @@ __global__ __launch_bounds__(256) void k_digit_hist(const uint32_t* __restrict__
 constexpr int kBucketThreads = 256;
 constexpr int kBucketWaves = kBucketThreads / 64;
 constexpr uint32_t kBucketCap = kBucketThreads * kSortItems;  // keys per LDS sort
-
-// Stable rank of each item among the equal 10-bit digits of its wave, in
-// (item, lane) order, on top of the wave's running digit counters s_wc[w].
-template <int P = kSortItems>
-__device__ __forceinline__ void rank10(const uint32_t (&dg)[P], const bool (&ok)[P],
-                                       uint32_t (*s_wc)[kMsbBuckets], uint32_t (&r)[P]) {
-    const uint32_t w = threadIdx.x >> 6;
-#pragma unroll
-    for (int i = 0; i < P; ++i) {
-        const uint32_t d = dg[i];
-        uint64_t peers = __ballot(ok[i]);
-        if (!peers) continue;  // wave-uniform: no item of this group (a bucket's tail)
-#pragma unroll
-        for (int b = 0; b < 10; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t bal = __ballot(ok[i] && bit);
-            peers &= bit ? bal : ~bal;
-        }
-        const uint32_t below = sort_count_below(peers);
-        const uint32_t cur = s_wc[w][d];
-        r[i] = cur + below;
-        if (ok[i] && below == 0) s_wc[w][d] = cur + (uint32_t)__popcll(peers);
-    }
-}
-
-// s_wc[w][d] -> exclusive prefix over the waves; s_cnt[d] = the digit's total.
-template <int NW, int NT>
-__device__ __forceinline__ void wave_prefix(uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt) {
-    for (uint32_t d = threadIdx.x; d < kMsbBuckets; d += NT) {
-        uint32_t acc = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t c = s_wc[w][d];
-            s_wc[w][d] = acc;
-            acc += c;
-        }
-        s_cnt[d] = acc;
-    }
-}
-
-// The same with 16-B LDS accesses (4 digits per thread and wave row);
-// s_wc rows and s_cnt 16-B aligned.
-template <int NW, int NT>
-__device__ __forceinline__ void wave_prefix4(uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt) {
-    for (uint32_t q = threadIdx.x; q < kMsbBuckets / 4; q += NT) {
-        uint4 acc = make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int w = 0; w < NW; ++w) {
-            uint4* row = reinterpret_cast<uint4*>(s_wc[w]);
-            const uint4 c = row[q];
-            row[q] = acc;
-            acc.x += c.x; acc.y += c.y; acc.z += c.z; acc.w += c.w;
-        }
-        reinterpret_cast<uint4*>(s_cnt)[q] = acc;
-    }
-}
-
-// In-place exclusive scan of a[1024] in LDS by NT threads (a written before a
-// barrier); ends with a barrier.
-template <int NT>
-__device__ __forceinline__ void scan1024(uint32_t* a, uint32_t* s_sw /* [NT / 64] */) {
-    constexpr int PER = (int)kMsbBuckets / NT;
-    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
-    uint32_t v[PER], sum = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        v[j] = a[t * PER + j];
-        sum += v[j];
-    }
-    uint32_t x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (l >= (uint32_t)o) x += y;
-    }
-    if (l == 63) s_sw[w] = x;
-    __syncthreads();
-    uint32_t pre = x - sum;
-    for (uint32_t k = 0; k < w; ++k) pre += s_sw[k];
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-        a[t * PER + j] = pre;
-        pre += v[j];
-    }
-    __syncthreads();
-}
 
 // counts[t][d] (t < nt <= 512) -> exclusive destinations bucket start +
 // sum_{t' < t} counts[t'][d], in place; bstart[0..1024] = bucket starts.
@@ -818,6 +730,234 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
     }
 }
 
+// ================================================================ tile-bucketed gather sort (r04)
+// The build's MSB sort without a global prefix or a first-level scatter
+// launch.  K1 (k_morton_tb, build_kernels.hip) already sorts each 4096-key
+// tile stably by bucket d = key >> 20 and writes it bucket by bucket, with
+// tb[tile][d] = run start | run length << 16 and the bucket totals ghist[d].
+// k_bucket_gather then owns bucket d: its start is the sum of ghist below d,
+// its keys are the d-runs of every tile in tile order -- an index-ordered
+// stream, since tiles are index ranges and each run is in index order -- so
+// the two stable 10-bit LSB passes over key bits 0..19 in LDS give §9.4's
+// unique (key, index) order.  Two launches (K1 + this) instead of four
+// (K1, k_msb_scan, k_msb_scatter, k_bucket_sort), and the keys cross HBM
+// twice less.
+// Blocks are dealt to buckets XCD by XCD (dispatch order is round-robin over
+// the 8 XCDs, so block b runs on XCD b mod 8): XCD x owns buckets
+// [128x, 128x + 128), i.e. one contiguous eighth of every tile's runs and of
+// every table row, which its own L2 then serves to its 128 blocks.
+constexpr uint32_t kGatherMaxTilesPerThread = 4;  // nt <= NT * 4 (n <= NT * 16384)
+constexpr uint32_t kGatherChunk = 8;              // run words loaded per round trip (a run: ~n / 4M keys)
+
+// LDS words of k_bucket_gather<NT, P>: the bucket (keys | vals, 2 x NT*P;
+// first the ranking counters), s_cnt, s_run, two [16] reduction rows
+constexpr size_t gather_lds_bytes(int nt, int p) { return ((size_t)2 * nt * p + 2 * kMsbBuckets + 32) * 4; }
+
+// The two stable 10-bit passes over key bits 0..19 of m > NT*P keys through
+// global memory, chunk by chunk: (sk, sv) -> (dk, dv) -> (sk, sv), then the
+// copy to (dk, dv).  The block owns [s, s + m) of all four arrays.
+template <int NT, int P>
+__device__ void bucket_sort_global(uint32_t* sk, uint32_t* sv, uint32_t* dk, uint32_t* dv, uint32_t s, uint32_t m,
+                                   uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt, uint32_t* s_run, uint32_t* s_sw) {
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    uint32_t* const ok0 = dk;
+    uint32_t* const ov0 = dv;
+    uint32_t k[P], v[P], dg[P], r[P];
+    bool ok[P];
+    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+        for (uint32_t j = tid; j < kMsbBuckets; j += NT) s_run[j] = 0u;
+        __syncthreads();
+        for (uint32_t j = tid; j < m; j += NT) atomicAdd(&s_run[(sk[s + j] >> shift) & (kMsbBuckets - 1)], 1u);
+        __syncthreads();
+        scan1024<NT>(s_run, s_sw);
+        for (uint32_t c0 = 0; c0 < m; c0 += (uint32_t)NT * P) {
+#pragma unroll
+            for (int i = 0; i < P; ++i) {
+                const uint32_t j = c0 + w * (64u * P) + i * 64u + l;
+                ok[i] = j < m;
+                k[i] = ok[i] ? sk[s + j] : 0u;
+                v[i] = ok[i] ? sv[s + j] : 0u;
+            }
+            bucket_rank<NT, P>(k, ok, shift, s_wc, s_cnt, dg, r);
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+                if (ok[i]) {
+                    const uint32_t o = s_run[dg[i]] + r[i];
+                    dk[s + o] = k[i];
+                    dv[s + o] = v[i];
+                }
+            __syncthreads();  // s_run and s_wc reads done
+            for (uint32_t d = tid; d < kMsbBuckets; d += NT) s_run[d] += s_cnt[d];
+            __syncthreads();
+        }
+        // this pass's stores before the next pass's loads by the block's other
+        // waves (one CU: a workgroup-scope fence, not an L2 writeback)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+        uint32_t* t0 = sk;
+        sk = dk;
+        dk = t0;
+        t0 = sv;
+        sv = dv;
+        dv = t0;
+    }
+    for (uint32_t j = tid; j < m; j += NT) {  // two passes: the result is back in the source arrays
+        ok0[s + j] = sk[s + j];
+        ov0[s + j] = sv[s + j];
+    }
+}
+
+// xk/xv: scratch of n words each, used only by a bucket over NT*P keys (the
+// scene's first build, before its verdict; later builds of a dense scene run
+// the LSB sort).
+template <int NT, int P>
+__global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict__ keys_tb,
+                                                      const uint32_t* __restrict__ vals_tb,
+                                                      const uint32_t* __restrict__ tb, uint32_t nt,
+                                                      const uint32_t* __restrict__ ghist,
+                                                      uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
+                                                      uint32_t* __restrict__ xk, uint32_t* __restrict__ xv,
+                                                      Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
+    constexpr int NW = NT / 64;
+    constexpr uint32_t CAP = (uint32_t)NT * P;
+    static_assert(NW * kMsbBuckets <= 2 * CAP, "the ranking counters fit the bucket's buffer");
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
+    uint32_t* s_key = s_dyn;
+    uint32_t* s_val = s_dyn + CAP;
+    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_dyn);
+    uint32_t* s_cnt = s_dyn + 2 * CAP;
+    uint32_t* s_run = s_cnt + kMsbBuckets;
+    uint32_t* s_sw = s_run + kMsbBuckets;  // [16]
+    uint32_t* s_sw2 = s_sw + 16;           // [16]
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const uint32_t b = blockIdx.x;
+    const uint32_t d = (b & 7u) * (kMsbBuckets / 8) + (b >> 3);  // XCD x: buckets [128x, 128x + 128)
+    // this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K)
+    const uint32_t K = (nt + NT - 1) / NT;
+    uint32_t e[kGatherMaxTilesPerThread], csum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherMaxTilesPerThread; ++k) {
+        const uint32_t t = tid * K + k;
+        e[k] = (k < K && t < nt) ? tb[(uint64_t)t * kMsbBuckets + d] : 0u;
+        csum += e[k] >> 16;
+    }
+    // the bucket's start: the totals of the buckets below it
+    uint32_t gs = 0;
+    for (uint32_t j = tid; j < d; j += NT) gs += ghist[j];
+    const uint32_t m = ghist[d];
+    uint32_t x = csum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) gs += __shfl_xor(gs, o, 64);
+    if (l == 63) s_sw[w] = x;
+    if (l == 0) s_sw2[w] = gs;
+    __syncthreads();
+    uint32_t off = x - csum, s = 0;
+    for (uint32_t q = 0; q < (uint32_t)NW; ++q) {
+        if (q < w) off += s_sw[q];
+        s += s_sw2[q];
+    }
+    if (m == 0) return;  // block-uniform
+    const bool fits = m <= CAP;
+    uint32_t* gk = fits ? s_key : xk + s;  // the gathered bucket: LDS, or scratch beyond one LDS sort
+    uint32_t* gv = fits ? s_val : xv + s;
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherMaxTilesPerThread; ++k) {
+        const uint32_t c = e[k] >> 16;
+        if (c) {
+            const uint32_t src = (tid * K + k) * (uint32_t)kSortTile + (e[k] & 0xFFFFu);
+            for (uint32_t i0 = 0; i0 < c; i0 += kGatherChunk) {
+                uint32_t kk[kGatherChunk], vv[kGatherChunk];
+#pragma unroll
+                for (uint32_t i = 0; i < kGatherChunk; ++i) {
+                    kk[i] = i0 + i < c ? keys_tb[src + i0 + i] : 0u;
+                    vv[i] = i0 + i < c ? vals_tb[src + i0 + i] : 0u;
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < kGatherChunk; ++i)
+                    if (i0 + i < c) {
+                        gk[off + i0 + i] = kk[i];
+                        gv[off + i0 + i] = vv[i];
+                    }
+            }
+            off += c;
+        }
+    }
+    if (!fits) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+        bucket_sort_global<NT, P>(xk, xv, kout, vout, s, m, s_wc, s_cnt, s_run, s_sw);
+        return;
+    }
+    __syncthreads();
+    // per items per lane: wave w holds [64 per w, 64 per (w + 1)), index order =
+    // (wave, item, lane), the ranking's order
+    const uint32_t per = (m + NT - 1) / NT;
+    uint32_t k[P], v[P], dg[P], r[P];
+    bool ok[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const uint32_t j = w * (64u * per) + i * 64u + l;
+        ok[i] = (uint32_t)i < per && j < m;
+        k[i] = ok[i] ? s_key[j] : 0u;
+        v[i] = ok[i] ? s_val[j] : 0u;
+    }
+    __syncthreads();  // every item in registers before the counters overwrite the buffer
+    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+        bucket_rank<NT, P>(k, ok, shift, s_wc, s_cnt, dg, r);
+        scan1024<NT>(s_cnt, s_sw);  // its barriers also end every counter read
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            if (ok[i]) {
+                const uint32_t p = s_cnt[dg[i]] + r[i];
+                s_key[p] = k[i];
+                s_val[p] = v[i];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            const uint32_t j = w * (64u * per) + i * 64u + l;
+            if (ok[i]) {
+                k[i] = s_key[j];
+                v[i] = s_val[j];
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const uint32_t j = w * (64u * per) + i * 64u + l;
+        if (ok[i]) {
+            kout[s + j] = k[i];
+            vout[s + j] = v[i];
+        }
+    }
+}
+
+// A probe build's verdict for the gather sort: 1 when some bucket holds more
+// than cap keys (the LSB sort then runs), else 0.
+__global__ __launch_bounds__(1024) void k_bucket_dense(const uint32_t* __restrict__ ghist, uint32_t cap,
+                                                       uint32_t* __restrict__ dense) {
+    const int big = __syncthreads_or(ghist[threadIdx.x] > cap);
+    if (threadIdx.x == 0) dense[0] = big ? 1u : 0u;
+}
+
+// copies n words of two arrays (the probe build's LSB leg ends in buffer 1)
+__global__ __launch_bounds__(256) void k_copy2(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
+                                               uint32_t* __restrict__ ao, uint32_t* __restrict__ bo, uint32_t n,
+                                               Gate gate) {
+    if (gated_off(gate)) return;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        ao[i] = a[i];
+        bo[i] = b[i];
+    }
+}
+
 // ================================================================ launchers
 static inline uint32_t sdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
@@ -937,6 +1077,83 @@ hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, c
     if ((e = digit_hist(keys[0], n, ghist4, s, g)) != hipSuccess) return e;
     if ((e = tile_hist0(keys[0], n, c4[0], s, g)) != hipSuccess) return e;
     return sort_lsb(keys, vals, n, ghist4, c4, s, g);
+}
+
+// ---- the gather sort's launchers.  Block shape by n: the smallest bucket
+// block whose LDS sort holds a uniform soup's n/1024 keys with a wide margin
+// (mean + 16 sigma + 64), so a uniform scene never takes the global path
+// (a fixed 2048-key cap up to 2^21 sent uniform 2M soups to the
+// LSB sort for good).
+struct GatherShape { int nt, p; };
+static GatherShape gather_shape(uint32_t n) {
+    const double mean = (double)n / kMsbBuckets;
+    const double need = mean + 16.0 * std::sqrt(mean) + 64.0;
+    if (need <= 256 * 8) return {256, 8};
+    if (need <= 512 * 8) return {512, 8};
+    if (need <= 1024 * 12) return {1024, 12};
+    return {1024, 16};
+}
+uint32_t gather_bucket_cap(uint32_t n) {
+    const GatherShape g = gather_shape(n);
+    return (uint32_t)(g.nt * g.p);
+}
+bool gather_sort_fits(uint32_t n) {  // tiles per bucket-block thread, and 16-bit run starts
+    return n >= 2 && sort_tiles(n) <= (uint32_t)gather_shape(n).nt * kGatherMaxTilesPerThread;
+}
+
+template <int NT, int P>
+static hipError_t gather_launch(const uint32_t* ktb, const uint32_t* vtb, const uint32_t* tb, uint32_t nt,
+                                const uint32_t* ghist, uint32_t* ko, uint32_t* vo, uint32_t* xk, uint32_t* xv,
+                                hipStream_t s, Gate g) {
+    static std::once_flag once[kMaxDevices];
+    static hipError_t err[kMaxDevices];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    constexpr size_t lds = gather_lds_bytes(NT, P);
+    std::call_once(once[dev], [dev] {
+        err[dev] = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bucket_gather<NT, P>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    });
+    if (err[dev] != hipSuccess) return err[dev];
+    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, ktb, vtb, tb, nt, ghist, ko, vo, xk, xv,
+               g);
+    return hipGetLastError();
+}
+
+hipError_t launch_sort_gather(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
+                              const uint32_t* tb, uint32_t* xk, uint32_t* xv, uint32_t* counts, uint32_t* ghist4,
+                              uint32_t* dense, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    if (!gather_sort_fits(n)) return hipErrorInvalidValue;
+    const uint32_t nt = sort_tiles(n);
+    const GatherShape gs = gather_shape(n);
+    hipError_t e;
+    if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), dense);
+    const Gate g{dense, 0u};
+    // keys[1]/vals[1]: K1's tile-bucketed keys -> keys[0]/vals[0]
+    if (gs.nt == 256) e = gather_launch<256, 8>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
+    else if (gs.nt == 512) e = gather_launch<512, 8>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
+    else if (gs.p == 12) e = gather_launch<1024, 12>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
+    else e = gather_launch<1024, 16>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
+    if (e != hipSuccess || !dense) return e;
+    // dense (a probe build whose verdict is 1): the 4-pass LSB sort of the
+    // tile-bucketed arrays -- equal keys share a bucket, and a bucket's keys
+    // are in index order there, so the stable passes still give §9.4's order
+    // -- from buffer 1 (ending there), then copied to buffer 0.  The table is
+    // spent, so the LSB passes reuse its words ([4][tile][256] = [tile][1024]).
+    const Gate g1{dense, 1u};
+    const uint64_t cs = (uint64_t)nt * 256;
+    uint32_t* c4[4] = {counts, counts + cs, counts + 2 * cs, counts + 3 * cs};
+    uint32_t* K1[2] = {keys[1], keys[0]};
+    uint32_t* V1[2] = {vals[1], vals[0]};
+    if ((e = digit_hist(keys[1], n, ghist4, s, g1)) != hipSuccess) return e;
+    if ((e = tile_hist0(keys[1], n, c4[0], s, g1)) != hipSuccess) return e;
+    if ((e = sort_lsb(K1, V1, n, ghist4, c4, s, g1)) != hipSuccess) return e;
+    RT_KLAUNCH(k_copy2, dim3(std::min<uint32_t>(2048, sdiv(n, 256))), dim3(256), 0, s, keys[1], vals[1], keys[0], vals[0],
+               n, g1);
+    return hipGetLastError();
 }
 
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,

@@ -342,6 +342,11 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
  * 0/1: timing events of scenes created afterwards record with the
  * system-scope fence (default 0: no L2 writeback at each record).
+ * "build.sort" (n in 2..12M): 2 = the tile-bucketed gather sort (default:
+ * K1 sorts each 4096-key tile by the top 10 key bits, then one block per
+ * bucket gathers its runs and sorts them in LDS), 1 = the r01-r03 MSB
+ * scatter + bucket sort, 0 = the 4-pass LSB radix sort; a scene whose first
+ * build finds a bucket beyond one block's LDS sort keeps the LSB sort.
  * "debug.poison" 0/1: every device buffer the library allocates from then on
  * is filled with 0xFF bytes before first use, so reading a byte no kernel
  * wrote gives the same (wrong) value every run instead of allocator luck.

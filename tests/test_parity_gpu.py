@@ -179,26 +179,34 @@ def test_build_degenerate_inputs(R, oracle):
     _compare_build(R, oracle, neg)
 
 
+SORT_DEFAULT = 2  # build.sort: the tile-bucketed gather sort
+
+
 def _compare_sorts(R, tris):
-    """The build with the MSB bucket sort (default for 2 <= n <= 12M) and with
-    the 4-pass LSB sort (build.sort = 0) must give the same BVH."""
+    """The build with the tile-bucketed gather sort (build.sort = 2, the
+    default for 2 <= n <= 12M), the MSB scatter + bucket sort (1) and the
+    4-pass LSB sort (0) must give the same BVH; each scene's first build (the
+    probe) and a second build alike."""
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     outs = []
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             R.config_set("build.sort", mode)
             with R.Scene.from_soup(tris) as s:
-                s.build()
-                outs.append(s.read_bvh())
+                for _ in range(2):
+                    s.build()
+                    outs.append(s.read_bvh())
     finally:
-        R.config_set("build.sort", 1)
-    a, b = outs
-    assert np.array_equal(a["keys"], b["keys"])
-    assert np.array_equal(a["vals"], b["vals"])
-    assert np.array_equal(a["nodes"].view(np.uint32), b["nodes"].view(np.uint32))
+        R.config_set("build.sort", SORT_DEFAULT)
+    a = outs[0]
+    for b in outs[1:]:
+        assert np.array_equal(a["keys"], b["keys"])
+        assert np.array_equal(a["vals"], b["vals"])
+        assert np.array_equal(a["nodes"].view(np.uint32), b["nodes"].view(np.uint32))
 
 
-@pytest.mark.parametrize("n", [2, 3, 4097, 70000, 1000000, 2097152, 2097153, 3000017, 10000000])
+@pytest.mark.parametrize("n", [2, 3, 4097, 70000, 1000000, 1400000, 2097152, 2097153, 3000017, 6000000, 10000000,
+                               12000000])
 def test_build_sort_paths_agree(R, oracle, n):
     _compare_sorts(R, soup(oracle, n, 11))
 
@@ -220,8 +228,9 @@ def test_build_sort_paths_agree_clustered(R, oracle):
     _compare_sorts(R, big)
 
 
+@pytest.mark.parametrize("sort", [1, 2])
 @pytest.mark.parametrize("n", [1_000_000, 3_000_000])  # LDS bucket sort / the _big kernels (n > kMsbMaxN)
-def test_clustered_scene_switches_sort(R, oracle, n):
+def test_clustered_scene_switches_sort(R, oracle, n, sort):
     """A scene whose first build finds an MSB bucket beyond one LDS sort -- a
     quarter of the soup in one tiny cell -- is sorted by the gated 4-pass LSB
     leg of that same build (launch_sort_probe) and by the LSB sort from then
@@ -231,16 +240,20 @@ def test_clustered_scene_switches_sort(R, oracle, n):
     t = rng.random((n, 9), dtype=np.float32)
     t[: n // 4] = 0.5 + rng.random((n // 4, 9), dtype=np.float32) * np.float32(1e-4)
     exp = oracle.build(t)
-    with R.Scene.from_soup(rng.random((n, 9), dtype=np.float32)) as w:  # every build kernel loaded
-        w.build()
-    ms = []
-    with R.Scene.from_soup(t) as s:
-        for _ in range(3):
-            ms.append(s.build())
-            got = s.read_bvh()
-            assert np.array_equal(got["keys"], exp["keys"])
-            assert np.array_equal(got["vals"], exp["vals"])
-            assert np.array_equal(got["nodes"].view(np.uint32), exp["nodes"].view(np.uint32))
+    R.config_set("build.sort", sort)
+    try:
+        with R.Scene.from_soup(rng.random((n, 9), dtype=np.float32)) as w:  # every build kernel loaded
+            w.build()
+        ms = []
+        with R.Scene.from_soup(t) as s:
+            for _ in range(3):
+                ms.append(s.build())
+                got = s.read_bvh()
+                assert np.array_equal(got["keys"], exp["keys"])
+                assert np.array_equal(got["vals"], exp["vals"])
+                assert np.array_equal(got["nodes"].view(np.uint32), exp["nodes"].view(np.uint32))
+    finally:
+        R.config_set("build.sort", SORT_DEFAULT)
     assert max(ms) < 1.0 * n / 1e6, ms
 
 

@@ -9,7 +9,11 @@
 #   bench:<tag>[:<bench.py args, ',' for ' '>]  -> gpurun_out/bench_<tag>.json/.err
 #   profile:<tag>:<config>:<steps>   kernel trace + FETCH/WRITE/SQ PMC passes of the
 #                                    timed bench steps -> gpurun_out/prof_<tag>/
+#   pmclds:<tag>:<config>:<steps>    the LDS counter pass (SQ_INSTS_LDS, bank conflicts, ...)
+#                                    -> gpurun_out/prof_<tag>/lds/
 #   py:<tag>:<script>[:<args, "~" for " ">]  a tools/ script -> gpurun_out/<tag>.log
+#   kstats:<tag>:<script>:<args>[:<counters>]  the script under rocprofv3 (kernel trace + stats,
+#                                    or one --pmc pass) -> gpurun_out/ks_<tag>/
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -48,6 +52,36 @@ run_profile() {  # tag config steps
     echo "[gpu_run] profile $tag done"
 }
 
+run_pmclds() {  # tag config steps: the LDS/issue counter pass (its own step, so a counter
+                # the box lacks ends only this step) -> gpurun_out/prof_<tag>/lds
+    local tag=$1 cfg=${2:-3} steps=${3:-20}
+    local out=gpurun_out/prof_$tag
+    local B="bench.py --only-timed --no-cpu-baseline --no-extra --config $cfg --steps $steps --warmup 3"
+    echo "[gpu_run] pmclds $tag: config $cfg, $steps steps"
+    mkdir -p $out
+    timeout -k 10 -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS \
+        SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY --output-format csv -d $out/lds -- python3 $B \
+        > $out/lds.log 2>&1 || { tail -20 $out/lds.log; return 1; }
+    echo "[gpu_run] pmclds $tag done"
+}
+
+run_kstats() {  # tag script args [pmc counters, "~" for " "]: a tools/ script under rocprofv3
+                # (kernel trace + stats; with counters, one --pmc pass instead) -> gpurun_out/ks_<tag>/
+    local tag=$1 script=$2 args=${3//\~/ } pmc=${4//\~/ }
+    local out=gpurun_out/ks_$tag
+    mkdir -p $out
+    if [ -z "$pmc" ]; then
+        echo "[gpu_run] kstats $tag: $script $args"
+        timeout -k 10 -s KILL 600 rocprofv3 --kernel-trace --stats --output-format csv -d $out -- python3 $script $args \
+            > $out/run.log 2>&1 || { tail -20 $out/run.log; return 1; }
+    else
+        echo "[gpu_run] kstats $tag (pmc $pmc): $script $args"
+        timeout -k 10 -s KILL 600 rocprofv3 --pmc $pmc --output-format csv -d $out -- python3 $script $args \
+            > $out/run.log 2>&1 || { tail -20 $out/run.log; return 1; }
+    fi
+    tail -3 $out/run.log
+}
+
 run_py() {  # tag script args
     local tag=$1 script=$2 args=${3//\~/ }
     echo "[gpu_run] py $tag: $script $args"
@@ -56,12 +90,14 @@ run_py() {  # tag script args
 }
 
 for step in "$@"; do
-    IFS=':' read -r kind a b c <<< "$step"
+    IFS=':' read -r kind a b c d <<< "$step"
     case $kind in
         tests) run_tests "$a" "$b" || exit 1 ;;
         bench) run_bench "$a" "$b" || exit 1 ;;
         profile) run_profile "$a" "$b" "$c" || exit 1 ;;
+        pmclds) run_pmclds "$a" "$b" "$c" || exit 1 ;;
         py) run_py "$a" "$b" "$c" || exit 1 ;;
+        kstats) run_kstats "$a" "$b" "$c" "$d" || exit 1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
 done

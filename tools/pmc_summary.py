@@ -168,6 +168,29 @@ def main():
         L.append(f"| {k} | {len(v)} | {mean(v):.2f} | {min(v):.2f} | {max(v):.2f} | "
                  f"{f if f is None else round(f, 1)} | {w if w is None else round(w, 1)} | {hb} | "
                  f"{'-' if va is None else f'{va:.4g}'} |")
+    # the LDS/issue pass (gpu_run.sh pmclds), when it ran
+    LDSC = ("SQ_INSTS_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE", "SQ_WAIT_INST_LDS", "SQ_BUSY_CYCLES",
+            "SQ_INSTS_SALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY")
+    if glob.glob(os.path.join(d, "lds", "**", "*counter_collection.csv"), recursive=True):
+        lp = {}
+        for c in LDSC:
+            acc = defaultdict(list)
+            for _, k, v in dispatches(os.path.join(d, "lds", "**", "*counter_collection.csv"), c):
+                acc[k].append(v)
+            lp[c] = {k: mean(v) for k, v in acc.items()}
+        L += ["", "## LDS / issue counters per dispatch (gpu_run.sh pmclds; SQ cycle counters in quad-cycles)", "",
+              "| kernel | LDS insts | bank-conflict cycles | LDS array cycles | conflict frac | WAIT_INST_LDS | "
+              "SALU insts | WAIT_ANY / WAVE_CYCLES |", "|---|---|---|---|---|---|---|---|"]
+        for k, v in sorted(dur.items(), key=lambda kv: -sum(kv[1])):
+            g = {c: lp[c].get(k) for c in LDSC}
+            if g["SQ_INSTS_LDS"] is None:
+                continue
+            cf = g["SQ_LDS_BANK_CONFLICT"] / g["SQ_LDS_IDX_ACTIVE"] if g["SQ_LDS_IDX_ACTIVE"] else None
+            wf = g["SQ_WAIT_ANY"] / g["SQ_WAVE_CYCLES"] if g["SQ_WAVE_CYCLES"] else None
+            fmt = lambda x: "-" if x is None else f"{x:.4g}"
+            L.append(f"| {k} | {fmt(g['SQ_INSTS_LDS'])} | {fmt(g['SQ_LDS_BANK_CONFLICT'])} | "
+                     f"{fmt(g['SQ_LDS_IDX_ACTIVE'])} | {fmt(cf)} | {fmt(g['SQ_WAIT_INST_LDS'])} | "
+                     f"{fmt(g['SQ_INSTS_SALU'])} | {fmt(wf)} |")
     open(os.path.join("profiles", f"rocprof_{tag}.md"), "w").write("\n".join(x for x in L if x is not None) + "\n")
     print(json.dumps(entry, indent=1))
 
