@@ -32,15 +32,14 @@ GPU, before any of them touches the GPU); under torch.distributed.run the
 ranks come from the environment.
 
 roofline: the trace launch (k_trace, then k_trace_coop for the rays past the heavy-ray cap, whose block 0
-  sorts the next frame's tile order) -- the bytes the kernels
-  request (64 B per K7w record + 48 B per triangle record fetched, its own
-  deterministic counters, + 16 B hit + 4 B RGBA written per ray) over its
-  event-timed duration, against the 8.0 TB/s HBM peak (frac) and the
-  aggregate L2 bandwidth (l2_frac); beside it the PMC-measured HBM bytes
-  (hbm_frac) and VALU issue (issue_frac) of the same kernel from the committed
-  profile (profiles/pmc_summary.json, tools/gpu_run.sh profile); `limiter`
-  names the largest MEASURED fraction (HBM traffic, L2 requests, VALU issue).
-  other_configs.config5 (soup-10M, the config whose trace structures exceed
+  sorts the next frame's tile order), priced against the resource that
+  measurably bounds it (`bound`, roofline_of): HBM (PMC bytes), L2 (the bytes
+  the kernels request: 64 B per K7w record + 48 B per triangle record fetched,
+  their own deterministic counters, + 16 B hit + 4 B RGBA per ray -- served
+  by L2/MALL, so never priced against HBM) or VALU issue (SQ_INSTS_VALU over
+  the issue capacity), the PMC figures from the committed profile of the same
+  command (profiles/pmc_summary.json, tools/gpu_run.sh profile).  Every frac
+  is <= 1.  other_configs.config5 (soup-10M, the config whose trace structures exceed
   the MALL) carries the same block from its own profile entry.  The SURVEY.md §8(d) binary-traversal byte model
   is kept as algo_bytes_binary_model (it charges node visits the wide kernel
   does not make, so its fraction is not a roofline of this kernel).
@@ -282,30 +281,48 @@ def make_scene(R, S, cfg):
     return R.Scene.from_soup(S.tris_for(cfg.scene))
 
 
+VALU_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md: nominal shader clock
+
+
 def roofline_of(kernel_bytes, trace_ms, pmc):
-    """The trace kernel's roofline block: `frac` = the bytes it requests over
-    its event-timed launch against the HBM peak (the contract's memory
-    roofline); `hbm_frac` / `issue_frac` = the MEASURED HBM traffic and VALU
-    issue (PMC, from the committed profile of the same command); `limiter` =
-    the largest of the measured fractions only (HBM traffic, L2 requests,
-    VALU issue) -- the requested-bytes fraction is a model, not a resource."""
-    achieved = kernel_bytes / (trace_ms * 1e-3) / 1e9
+    """The trace kernel's roofline block, priced against the resource that
+    MEASURABLY bounds it:
+      hbm_frac   = PMC HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE) over
+                   the event-timed launch, against the 8 TB/s HBM peak;
+      l2_frac    = the bytes the kernel requests (its own record/triangle
+                   counters + outputs) against the aggregate L2 bandwidth --
+                   every request passes L2, and most are served there or from
+                   the MALL, so they are never priced against HBM;
+      issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 x GRBM_GUI_ACTIVE/8), the
+                   VALU issue share, from the committed profile of the same
+                   command.
+    `bound` is the largest of these; achieved/peak/unit/frac are that
+    resource's.  Without a PMC entry only l2_frac is known and bound = l2."""
+    t = trace_ms * 1e-3
+    req_gbs = kernel_bytes / t / 1e9
     hbm_frac = issue_frac = traffic = None
     if pmc:
         traffic = pmc.get("hbm_bytes_per_launch")
         if traffic:
-            hbm_frac = traffic / (trace_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+            hbm_frac = traffic / t / 1e9 / HBM_PEAK_GBS
         if pmc.get("valu_insts_per_launch") and pmc.get("cycles_per_launch"):
             issue_frac = pmc["valu_insts_per_launch"] / (VALU_ISSUE_PER_CYCLE * pmc["cycles_per_launch"])
-    l2_frac = achieved / L2_PEAK_GBS
-    cands = {"hbm_measured": hbm_frac, "l2_requests": l2_frac, "valu_issue": issue_frac}
-    limiter = max((k for k in cands if cands[k] is not None), key=lambda k: cands[k])
-    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "bytes_per_launch": kernel_bytes,
+    l2_frac = req_gbs / L2_PEAK_GBS
+    fr = {"hbm": hbm_frac, "l2": l2_frac, "valu_issue": issue_frac}
+    bound = max((k for k in fr if fr[k] is not None), key=lambda k: fr[k])
+    if bound == "hbm":
+        achieved, peak, unit = traffic / t / 1e9, HBM_PEAK_GBS, "GB/s"
+    elif bound == "l2":
+        achieved, peak, unit = req_gbs, L2_PEAK_GBS, "GB/s"
+    else:
+        peak = VALU_ISSUE_PER_CYCLE * VALU_CLOCK_GHZ
+        achieved, unit = issue_frac * peak, "G VALU wave-instructions/s"
+    return {"bound": bound, "achieved": round(achieved, 1), "peak": peak, "unit": unit,
+            "frac": round(fr[bound], 4), "traffic": traffic,
             "hbm_frac": round(hbm_frac, 4) if hbm_frac is not None else None,
             "l2_frac": round(l2_frac, 4), "l2_peak": L2_PEAK_GBS,
             "issue_frac": round(issue_frac, 4) if issue_frac is not None else None,
-            "limiter": limiter,
+            "requested_bytes_per_launch": kernel_bytes, "requested_gbs": round(req_gbs, 1),
             "pmc_trace_kernel_us": pmc.get("trace_kernel_avg_us") if pmc else None}
 
 
@@ -628,15 +645,15 @@ def main():
                              pmc_source=(os.path.relpath(args.pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]")
                              if pmc else None,
                              algo_bytes_binary_model=algo_bytes,
-                             note="achieved = bytes the wide kernel requests per launch (64 B per K7w record + "
-                                  "48 B per triangle record, its own counters, + 16 B hit + 4 B RGBA per ray) over "
-                                  "the event-timed launch, priced against HBM (frac) and the aggregate L2 (l2_frac: "
-                                  "every request passes L2); traffic = PMC HBM bytes per launch (2*FETCH_SIZE + "
-                                  "WRITE_SIZE, gfx950 correction), hbm_frac = traffic over the same time; "
-                                  "issue_frac = SQ_INSTS_VALU / (1024 SIMDs x 0.5 x GRBM_GUI_ACTIVE/8); limiter = "
-                                  "the largest MEASURED fraction (hbm_measured, l2_requests, valu_issue); "
-                                  "algo_bytes_binary_model = SURVEY.md §8(d) 32/node + 36/tri + 16/ray over the "
-                                  "§9.7 binary traversal (not what this kernel fetches)"),
+                             note="bound = the resource with the largest measured fraction: hbm (PMC HBM bytes "
+                                  "2*FETCH_SIZE + WRITE_SIZE per launch, gfx950 correction, over the event-timed "
+                                  "launch vs 8 TB/s), l2 (the bytes the wide kernel requests -- 64 B per K7w record "
+                                  "+ 48 B per triangle record, its own counters, + 16 B hit + 4 B RGBA per ray -- vs "
+                                  "the aggregate L2; they are served by L2/MALL, so never priced against HBM) or "
+                                  "valu_issue (SQ_INSTS_VALU / (1024 SIMDs x 0.5 x GRBM_GUI_ACTIVE/8), committed "
+                                  "profile); achieved/peak/frac are that resource's. algo_bytes_binary_model = "
+                                  "SURVEY.md §8(d) 32/node + 36/tri + 16/ray over the §9.7 binary traversal (node "
+                                  "visits the wide kernel does not make: not a roofline of this kernel)"),
             "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM,
