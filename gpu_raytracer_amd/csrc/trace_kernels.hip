@@ -2040,8 +2040,19 @@ hipError_t dev_alloc(void** p, size_t bytes) {
     hipError_t e = hipMalloc(p, bytes ? bytes : 16);
     if (e != hipSuccess || !config_snapshot().poison) return e;
     // debug.poison: 0xFF in every byte (a NaN float, RT_SENT index, 255 plane),
-    // finished before any stream can use the buffer
-    if ((e = hipMemset(*p, 0xFF, bytes ? bytes : 16)) == hipSuccess) e = hipDeviceSynchronize();
+    // finished before any stream can use the buffer.  The fill runs on a
+    // private non-blocking stream of the current device and only that stream
+    // is waited for (a device-wide synchronize here would also
+    // wait for -- and hide the ordering of -- other scenes' in-flight work).
+    static std::once_flag once[kMaxDevices];
+    static hipStream_t fill[kMaxDevices];
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) == hipSuccess && (dev < 0 || dev >= kMaxDevices)) e = hipErrorInvalidDevice;
+    if (e == hipSuccess) {
+        std::call_once(once[dev], [dev] { (void)hipStreamCreateWithFlags(&fill[dev], hipStreamNonBlocking); });
+        e = fill[dev] ? hipMemsetAsync(*p, 0xFF, bytes ? bytes : 16, fill[dev]) : hipErrorInvalidResourceHandle;
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(fill[dev]);
     if (e != hipSuccess) {
         (void)hipFree(*p);
         *p = nullptr;
