@@ -192,7 +192,9 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals,
                                                          uint32_t* __restrict__ ghist /* [4][256] */,
                                                          uint32_t* __restrict__ counts0 /* [tile][256] */,
-                                                         uint32_t vbase = 0 /* vals = vbase + index */) {
+                                                         uint32_t vbase = 0 /* vals = vbase + index */,
+                                                         Gate gate = Gate{}) {
+    if (gated_off(gate)) return;
     __shared__ uint32_t hist[4 * 256];
     __shared__ float red[kSortThreads / 64][6];
     for (uint32_t j = threadIdx.x; j < 1024; j += kSortThreads) hist[j] = 0u;
@@ -249,37 +251,154 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
     }
 }
 
+// A grid-wide barrier of co-resident blocks (the fused K0 + K1 below; the
+// pattern of tools/calib_barrier.hip, 2.4 us on MI355X): the data handed over
+// is stored with agent-scope relaxed atomic stores (write-through, no L2
+// writeback), the block drains them (workgroup release = s_waitcnt) and
+// arrives on one agent-scope counter, and readers use agent-scope atomic
+// loads.  The counter holds generation << 16 | arrivals, so it resets itself
+// for the next build: the last arrival bumps the generation and zeroes the
+// count, the others wait for the generation to change.  A wait gives up
+// after ~100 ms (s_memrealtime) and sets *err -- a grid that is not
+// co-resident must not hang the GPU (the host reads *err after the build).
+__device__ __forceinline__ bool grid_sync(uint32_t* bar, uint32_t nblocks, uint32_t* err) {
+    __shared__ uint32_t s_ok;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t ok = 1;
+        if ((old & 0xFFFFu) == nblocks - 1) {
+            __hip_atomic_fetch_add(bar, 0x10000u - nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            while ((__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == (old >> 16)) {
+                __builtin_amdgcn_s_sleep(1);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
+                    ok = 0;
+                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
 // K1 + the first level of the gather sort (r04, sort_kernels.hip "tile-bucketed
-// gather sort"): the block's 4096 Morton keys are also sorted, stably, by
-// bucket d = key >> 20 inside the tile -- the index order is (wave, item,
-// lane), which is rank10's order -- and written bucket by bucket to
-// keys_tb/vals_tb[tile * 4096 ..], with tb[tile][d] = run start | run length
-// << 16 and the global bucket totals in ghist[1024].  No global prefix over
-// tiles exists: each bucket's block gathers its runs from every tile.
+// gather sort"): the block's 4096 Morton keys are also grouped by bucket
+// d = key >> 20 inside the tile (LDS atomics: the order inside a bucket is
+// free, since the second level orders by the whole (key, index) pair) and
+// written bucket by bucket as ONE word per key, key bits 0..19 << 12 | the
+// key's index inside the tile (the bucket is the run's, the tile the
+// table row's), with tb[tile][d] = run start | run length << 16 and the
+// global bucket totals in ghist[1024].  No global prefix over tiles exists:
+// each bucket's block gathers its runs from every tile.
+// FUSED (the grid must be co-resident, launch_build
+// checks): K0 in the same launch -- the block's triangles, loaded once, give
+// its partial centroid box (published for the grid barrier) and then its
+// keys; the zero words K0 clears are cleared here before the barrier.  One
+// soup read and one launch instead of two.
+struct FuseArgs {
+    uint32_t* zero = nullptr;  // per-build control words (K0's)
+    uint32_t nzero = 0;
+    uint32_t* bar = nullptr;   // grid barrier counter (never zeroed: self-resetting)
+    uint32_t* err = nullptr;   // set on a barrier timeout
+};
+static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
+template <bool FUSED>
 __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
                                                             BuildParams* __restrict__ params,
-                                                            const float* __restrict__ partials, uint32_t nb,
-                                                            uint32_t* __restrict__ keys_tb, uint32_t* __restrict__ vals_tb,
+                                                            float* __restrict__ partials, uint32_t nb,
+                                                            uint32_t* __restrict__ words_tb,
                                                             uint32_t* __restrict__ ghist /* [1024] */,
-                                                            uint32_t* __restrict__ tb /* [tile][1024] */) {
+                                                            uint32_t* __restrict__ tb /* [tile][1024] */,
+                                                            FuseArgs fu = FuseArgs{}) {
     constexpr int W = kSortThreads / 64;
-    static_assert(W * kMsbBuckets <= 2 * kSortTile, "the ranking counters fit the bucketed tile's buffer");
-    __shared__ __attribute__((aligned(16))) uint32_t s_buf[2 * kSortTile];  // s_wc[W][1024], then keys | vals
+    __shared__ uint32_t s_word[kSortTile];  // the bucketed tile
     __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
     __shared__ float red[W][6];
     __shared__ uint32_t s_sw[W];
-    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_buf);
-    for (uint32_t j = threadIdx.x; j < W * kMsbBuckets / 4; j += kSortThreads)
-        reinterpret_cast<uint4*>(s_buf)[j] = make_uint4(0, 0, 0, 0);
+    for (uint32_t j = threadIdx.x; j < kMsbBuckets; j += kSortThreads) s_start[j] = 0u;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x, tbase = tile * (uint32_t)kSortTile;
     const uint32_t wbase = tbase + w * 64u * kTrisPerThread;
     float t[kTrisPerThread][9];
     const uint32_t okm = load_tri_lanes(tris, n, wbase, t);  // in flight while the bounds are reduced
-    const BuildParams p = bounds_final<kSortThreads>(partials, nb, red);  // ends with a barrier
+    BuildParams p;
+    if constexpr (FUSED) {
+        // K0: the zero words, then this tile's partial centroid box, published
+        for (uint32_t j = tile * kSortThreads + threadIdx.x; j < fu.nzero; j += gridDim.x * kSortThreads)
+            __hip_atomic_store(fu.zero + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        float lo[3], hi[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
+#pragma unroll
+        for (uint32_t q = 0; q < kTrisPerThread; ++q) {
+            if ((okm >> q) & 1u) {
+                float bmin[3], bmax[3];
+                tri_bounds(t[q], bmin, bmax);
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    const float cc = (bmin[c] + bmax[c]) * 0.5f;
+                    lo[c] = fminf(lo[c], cc);
+                    hi[c] = fmaxf(hi[c], cc);
+                }
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { lo[c] = wave_min(lo[c]); hi[c] = wave_max(hi[c]); }
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { red[w][c] = lo[c]; red[w][3 + c] = hi[c]; }
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) {
+            const int c = threadIdx.x;
+            float v = red[0][c];
+#pragma unroll
+            for (int k = 1; k < W; ++k) v = c < 3 ? fminf(v, red[k][c]) : fmaxf(v, red[k][c]);
+            __hip_atomic_store(partials + tile * 6 + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        grid_sync(fu.bar, gridDim.x, fu.err);
+        // the second level, as bounds_final: every block reduces all partials
+        // (exact min/max: the same box in every block and as K0 + K1 give)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
+        for (uint32_t b = threadIdx.x; b < gridDim.x; b += kSortThreads) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) {
+                lo[c] = fminf(lo[c], __hip_atomic_load(partials + b * 6 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                hi[c] = fmaxf(hi[c], __hip_atomic_load(partials + b * 6 + 3 + c, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT));
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { lo[c] = wave_min(lo[c]); hi[c] = wave_max(hi[c]); }
+        __syncthreads();  // red[] reads of the partial box done
+        if (lane == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; ++c) { red[w][c] = lo[c]; red[w][3 + c] = hi[c]; }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            float a = red[0][c], b = red[0][3 + c];
+#pragma unroll
+            for (int k = 1; k < W; ++k) { a = fminf(a, red[k][c]); b = fmaxf(b, red[k][3 + c]); }
+            p.lo[c] = a;
+            p.hi[c] = b;
+            p.inv[c] = (b > a) ? 1.0f / (b - a) : 0.0f;  // §9.2, correctly rounded
+        }
+#pragma unroll
+        for (int c = 0; c < 7; ++c) p.pad[c] = 0u;
+    } else {
+        p = bounds_final<kSortThreads>(partials, nb, red);  // ends with a barrier
+    }
     if (tile == 0 && threadIdx.x == 0) *params = p;
-    uint32_t k8[kTrisPerThread], dg[kTrisPerThread], r[kTrisPerThread];
-    bool ok[kTrisPerThread];
+    uint32_t k8[kTrisPerThread];
 #pragma unroll
     for (uint32_t q = 0; q < kTrisPerThread; ++q) {
         float bmin[3], bmax[3];
@@ -288,35 +407,26 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
 #pragma unroll
         for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
         k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
-        dg[q] = k8[q] >> kMsbShift;  // 30-bit keys: < 1024
-        ok[q] = (okm >> q) & 1u;
+        if ((okm >> q) & 1u) atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);  // 30-bit keys: bucket < 1024
     }
-    rank10<kTrisPerThread>(dg, ok, s_wc, r);
-    __syncthreads();
-    wave_prefix4<W, kSortThreads>(s_wc, s_start);
     __syncthreads();
     constexpr int PER = kMsbBuckets / kSortThreads;  // buckets per thread in scan1024's layout
     uint32_t cnt[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) cnt[j] = s_start[threadIdx.x * PER + j];
-    scan1024<kSortThreads>(s_start, s_sw);  // ends with a barrier
+    scan1024<kSortThreads>(s_start, s_sw);  // exclusive starts; ends with a barrier
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t d = threadIdx.x * PER + j;
         tb[(uint64_t)tile * kMsbBuckets + d] = s_start[d] | (cnt[j] << 16);
         if (cnt[j]) atomicAdd(&ghist[d], cnt[j]);
     }
-    uint32_t pos[kTrisPerThread];
-#pragma unroll
-    for (uint32_t q = 0; q < kTrisPerThread; ++q) pos[q] = s_start[dg[q]] + s_wc[w][dg[q]] + r[q];
-    __syncthreads();  // the counters are dead: the buffer becomes the bucketed tile
-    uint32_t* s_key = s_buf;
-    uint32_t* s_val = s_buf + kSortTile;
+    __syncthreads();  // every start read: the starts become the bucket cursors
 #pragma unroll
     for (uint32_t q = 0; q < kTrisPerThread; ++q)
-        if (ok[q]) {
-            s_key[pos[q]] = k8[q];
-            s_val[pos[q]] = wbase + q * 64u + lane;
+        if ((okm >> q) & 1u) {
+            const uint32_t pos = atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);
+            s_word[pos] = (k8[q] << 12) | (w * 64u * kTrisPerThread + q * 64u + lane);  // key bits 0..19, index
         }
     __syncthreads();
     const uint32_t trem = n - tbase;
@@ -324,10 +434,7 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
 #pragma unroll
     for (uint32_t m = 0; m < kTrisPerThread; ++m) {
         const uint32_t q = threadIdx.x + m * kSortThreads;
-        if (q < tcount) {
-            keys_tb[tbase + q] = s_key[q];
-            vals_tb[tbase + q] = s_val[q];
-        }
+        if (q < tcount) words_tb[tbase + q] = s_word[q];
     }
 }
 
@@ -1214,9 +1321,9 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.bstart, (kMsbBuckets + 4) * 4);
     RT_ALLOC(b.partials, (uint64_t)bounds_grid((uint32_t)N) * 24);
     RT_ALLOC(b.params, sizeof(BuildParams));
-    RT_ALLOC(b.zero, (uint64_t)b.nzero * 4);
+    RT_ALLOC(b.zero, (uint64_t)kZAlloc * 4);
 #undef RT_ALLOC
-    if ((e = hipMemset(b.zero, 0, (uint64_t)b.nzero * 4)) != hipSuccess) { free_build(b); return e; }
+    if ((e = hipMemset(b.zero, 0, (uint64_t)kZAlloc * 4)) != hipSuccess) { free_build(b); return e; }
     return hipSuccess;
 }
 
@@ -1440,27 +1547,64 @@ uint32_t build_sort_kind(const BuildBufs& b, uint32_t n, const TraceConfig& cfg)
     return cfg.sort_msb;
 }
 
+std::mutex& fused_gate(int device) {
+    static std::mutex m[kMaxDevices];
+    return m[device >= 0 && device < kMaxDevices ? device : 0];
+}
+
+// Co-residency of k_morton_tb<true>'s grid (one block per sort tile): the
+// occupancy API's blocks per CU, less one (MI355X_MICROARCH.md: the API can
+// be one block per CU high), times the CUs, must hold every tile -- the grid
+// barrier would otherwise wait for blocks that cannot start (it gives up
+// after ~100 ms and flags it rather than hang).
+bool fused_k01_fits(uint32_t n) {
+    static std::once_flag once[kMaxDevices];
+    static uint32_t cap[kMaxDevices];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return false;
+    std::call_once(once[dev], [dev] {
+        int per_cu = 0, cus = 0;
+        cap[dev] = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_morton_tb<true>),
+                                                         kSortThreads, 0) != hipSuccess)
+            return;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
+        cap[dev] = per_cu > 1 ? (uint32_t)(per_cu - 1) * (uint32_t)cus : 0u;
+    });
+    return n >= 2 && sort_tiles(n) <= cap[dev];
+}
+
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages,
-                        const TraceConfig& cfg, uint32_t* probed) {
+                        const TraceConfig& cfg, uint32_t* probed, bool allow_fused, bool* fused_out) {
     hipError_t e;
     if (probed) *probed = 0;
+    if (fused_out) *fused_out = false;
     auto rec = [&](int i) -> hipError_t {
         return (ev && (stages || i == 0 || i == 6)) ? hipEventRecord(ev->e[i], s) : hipSuccess;
     };
+    const uint32_t kind = build_sort_kind(b, n, cfg);
+    const bool fused = kind == 2 && allow_fused && cfg.fuse_k01 && fused_k01_fits(n);
     if ((e = rec(0)) != hipSuccess) return e;
-    RT_KLAUNCH(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.zero, kZEnd);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (!fused) {
+        RT_KLAUNCH(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.zero, kZEnd);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if ((e = rec(1)) != hipSuccess) return e;
     const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* counts[4] = {b.counts, b.counts + cs, b.counts + 2 * cs, b.counts + 3 * cs};
     if (!n) RT_KLAUNCH(k_bounds_final, dim3(1), dim3(256), 0, s, b.partials, 1u, b.params);
-    const uint32_t kind = build_sort_kind(b, n, cfg);
     // the scene's first build with this sort: the verdict on its bucket sizes
     // decides its later builds' sort (the host reads kZDense afterwards)
     const bool probe = kind != 0 && !(b.sort_mode != 0 && b.sort_mode_of == kind);
-    if (kind == 2) {
-        if (n) RT_KLAUNCH(k_morton_tb, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params, b.partials,
-                          bounds_grid(n), b.keys[1], b.vals[1], b.zero + kZHist, b.counts);
+    if (kind == 2 && fused) {
+        const FuseArgs fu{b.zero, kZEnd, b.zero + kZBar, b.zero + kZFuseErr};
+        RT_KLAUNCH(k_morton_tb<true>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params, b.partials,
+                   sort_tiles(n), b.keys[1], b.zero + kZHist, b.counts, fu);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (fused_out) *fused_out = true;
+    } else if (kind == 2) {
+        if (n) RT_KLAUNCH(k_morton_tb<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params,
+                          b.partials, bounds_grid(n), b.keys[1], b.zero + kZHist, b.counts, FuseArgs{});
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
                                        b.zero + kZHist, counts[0], s, kind == 1)) != hipSuccess) {
@@ -1470,11 +1614,17 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     uint32_t* K[2] = {b.keys[0], b.keys[1]};
     uint32_t* V[2] = {b.vals[0], b.vals[1]};
     if (kind == 2) {
-        // scratch of a bucket beyond one LDS sort: prebuf (6n words), which
-        // k_topo_refit writes only later
-        uint32_t* xk = reinterpret_cast<uint32_t*>(b.prebuf);
-        e = launch_sort_gather(K, V, n, b.zero + kZHist, b.counts, xk, xk + b.cap_n, b.counts, b.zero + kZHist4,
-                               probe ? b.zero + kZDense : nullptr, s);
+        // keys[1] = K1's tile-bucketed words -> keys[0]/vals[0]
+        uint32_t* dense = probe ? b.zero + kZDense : nullptr;
+        e = launch_sort_gather(b.keys[1], b.counts, n, b.zero + kZHist, b.keys[0], b.vals[0], b.zero + kZGatherFlags,
+                               dense, s);
+        if (e == hipSuccess && dense) {  // the LSB leg of a dense probe build: K1 again, in index order
+            RT_KLAUNCH(k_morton<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params,
+                       (const float*)nullptr, 0u, b.keys[0], b.vals[0], b.zero + kZHist4, counts[0], 0u,
+                       Gate{dense, 1u});
+            if ((e = hipGetLastError()) == hipSuccess)
+                e = launch_sort_lsb_gated(K, V, n, b.zero + kZHist4, b.counts, dense, s);
+        }
     } else if (kind == 1 && probe) {  // both sorts, gated on the bucket totals
         // scratch for the chunked tile scan (n > kMsbMaxN): the parent array,
         // which the build does not write (ceil(tiles/32) x 1024 words <= 2n - 1)

@@ -55,6 +55,8 @@ struct Replica {
     rt::BuildBufs bufs;
     bool uploaded = false, built = false;
     uint32_t msb_probe = 0;  // the sort (1 MSB, 2 gather) whose verdict this build wrote (BuildBufs::sort_mode)
+    bool fused = false;      // this build ran K0 + K1 fused (its barrier's timeout flag is in h_flag)
+    uint32_t* h_flag = nullptr;  // pinned host copy of zero[kZDense .. kZDense + 8): the build's verdict words
     rt::BuildEvents ev;
     rt_build_times times{};
     // render scratch (grown on demand)
@@ -286,6 +288,8 @@ void replica_free(Replica& r) {
     (void)hipEventDestroy(r.r0);
     (void)hipEventDestroy(r.r1);
     (void)hipEventDestroy(r.last);
+    if (r.h_flag) (void)hipHostFree(r.h_flag);
+    r.h_flag = nullptr;
     (void)hipStreamDestroy(r.stream);
     r.stream = nullptr;
 }
@@ -371,6 +375,11 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
     // could make the host read a verdict no kernel wrote)
     const rt::TraceConfig cfg = rt::config_snapshot();
     const bool stages = cfg.stage_events != 0;
+    // K0 + K1 fused (a grid barrier over co-resident blocks): only for a
+    // replica alone on its device in this call that also wins its device's
+    // fused gate, held until the build has finished -- two fused grids that
+    // share a device could each wait for blocks the other holds
+    std::vector<std::unique_lock<std::mutex>> gates;
     for (Replica* r : targets) {
         RTR(upload(s, *r));
         HIPR(hipSetDevice(r->device));
@@ -379,8 +388,22 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         // a rebuild that fails half-way must not leave the old flag over a
         // half-written BVH: built again only after the synchronize below
         r->built = false;
-        hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, &r->msb_probe);
+        bool alone = true;
+        for (Replica* o : targets) alone = alone && (o == r || o->device != r->device);
+        bool allow = false;
+        if (alone && cfg.fuse_k01) {
+            std::unique_lock<std::mutex> g(rt::fused_gate(r->device), std::try_to_lock);
+            if (g.owns_lock()) {
+                gates.push_back(std::move(g));
+                allow = true;
+            }
+        }
+        if (!r->h_flag) HIPR(hipHostMalloc(reinterpret_cast<void**>(&r->h_flag), 32, hipHostMallocDefault));
+        hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, &r->msb_probe, allow,
+                                        &r->fused);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
+        // the build's verdict words, read after the synchronize below (no extra sync)
+        HIPR(hipMemcpyAsync(r->h_flag, r->bufs.zero + rt::kZDense, 32, hipMemcpyDeviceToHost, r->stream));
     }
     double worst = 0.0;
     for (Replica* r : targets) {
@@ -398,10 +421,27 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         float tot = 0;
         HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
         r->times.total = tot;
-        if (r->msb_probe) {  // the scene's first build with this sort ran both sorts gated on its verdict: keep it
-            uint32_t dense = 0;
-            HIPR(hipMemcpy(&dense, r->bufs.zero + rt::kZDense, 4, hipMemcpyDeviceToHost));
-            r->bufs.sort_mode = dense ? 2u : 1u;
+        const uint32_t* hf = r->h_flag;  // [0] dense, [1] clustered bins, [2] bucket overflow, [5] barrier timeout
+        if (r->fused && hf[rt::kZFuseErr - rt::kZDense]) {  // a block of the fused grid gave up at the barrier
+            HIPR(hipMemset(r->bufs.zero + rt::kZFuseErr, 0, 4));
+            return fail(RT_EDEVICE, "fused bounds+Morton: grid barrier timed out (grid not co-resident)");
+        }
+        const uint32_t kind = rt::build_sort_kind(r->bufs, s->n, cfg);
+        if (kind == 2 && hf[rt::kZGatherFlags + 1 - rt::kZDense]) {
+            // a bucket outgrew its block's LDS (the verdict should have sent
+            // this scene to the LSB sort): that bucket is unsorted -- keep
+            // the LSB sort for this scene and build again with it
+            r->bufs.sort_mode = 2;
+            r->bufs.sort_mode_of = kind;
+            r->msb_probe = 0;
+            hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, nullptr, false, &r->fused);
+            if (e != hipSuccess) return hip_fail(e, "launch_build (LSB)");
+            HIPR(hipStreamSynchronize(r->stream));
+            HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
+            r->times.total = tot;
+        } else if (r->msb_probe) {  // the scene's first build with this sort ran both sorts gated on its verdict
+            const bool lsb = hf[0] != 0 || (r->msb_probe == 2 && hf[rt::kZGatherFlags - rt::kZDense] != 0);
+            r->bufs.sort_mode = lsb ? 2u : 1u;
             r->bufs.sort_mode_of = r->msb_probe;
             r->msb_probe = 0;
         }
@@ -514,6 +554,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.px_sort" && value >= 0 && value <= 2) c.px_sort = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
+    else if (k == "build.fuse_k01" && (value == 0 || value == 1)) c.fuse_k01 = (uint32_t)value;
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
     else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;

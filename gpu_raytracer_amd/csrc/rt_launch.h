@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <mutex>
+
 namespace rt {
 
 struct BuildParams;
@@ -57,8 +59,14 @@ constexpr uint32_t kZErr = 1028;        // sticky error bits (reserved)
 constexpr uint32_t kZCrossCtr = 1040;   // [kCrossShards] crossing-list shard lengths
 constexpr uint32_t kCrossShards = 16;
 constexpr uint32_t kZHist4 = 1056;      // [4][256] digit histograms of a probe build's LSB leg
-constexpr uint32_t kZDense = 2080;      // a probe build's verdict (k_msb_scan writes it)
+constexpr uint32_t kZDense = 2080;      // a probe build's verdict (k_msb_scan / k_bucket_dense write it)
+constexpr uint32_t kZGatherFlags = 2081;  // [2] k_bucket_gather: clustered bins, bucket overflow
 constexpr uint32_t kZEnd = 2084;        // words zeroed by K0 every build
+// past kZEnd, never zeroed by a build: the fused K0+K1's grid barrier
+// (self-resetting) and its timeout flag (cleared by the host when it sees it)
+constexpr uint32_t kZBar = 2084;
+constexpr uint32_t kZFuseErr = 2085;
+constexpr uint32_t kZAlloc = 2088;      // words of the zero region
 
 
 hipError_t alloc_build(BuildBufs& b, uint32_t n);
@@ -72,8 +80,16 @@ struct BuildEvents { hipEvent_t e[7]; bool valid = false; };
 // probed (nullable): the sort (1 MSB, 2 gather) whose verdict this build
 // wrote to zero[kZDense] -- the caller reads it after the build to set
 // sort_mode/sort_mode_of -- else 0.
+// allow_fused: the caller holds fused_gate(device) for this build (no other
+// fused build can be in flight on the device); launch_build then runs K0 + K1
+// as one launch with a grid barrier when the gather sort is used and the
+// grid fits the device at once (fused_k01_fits).  *fused_out: whether it did
+// (the caller then checks zero[kZFuseErr] after the build).
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev, bool stages,
-                        const TraceConfig& cfg, uint32_t* probed);
+                        const TraceConfig& cfg, uint32_t* probed, bool allow_fused = false,
+                        bool* fused_out = nullptr);
+bool fused_k01_fits(uint32_t n);  // every sort tile's block co-resident on the current device
+std::mutex& fused_gate(int device);
 // the sort launch_build would use: 0 LSB, 1 MSB scatter, 2 gather
 uint32_t build_sort_kind(const BuildBufs& b, uint32_t n, const TraceConfig& cfg);
 
@@ -150,6 +166,8 @@ struct TraceConfig {
                                 // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t wide_arity = 4;    // build.wide_arity: 4 = K7w 64-B records, 8 = K7w8 96-B records (greedy cut)
+    uint32_t fuse_k01 = 1;      // build.fuse_k01: 1 = K0 + K1 as one launch with a grid barrier when the grid
+                                // is co-resident and no other fused build runs on the device (gather sort)
     uint32_t sort_msb = 2;      // build.sort, for 2 <= n <= kMsbBigMaxN: 2 = tile-bucketed gather sort (default),
                                 // 1 = MSB scatter + bucket sort, 0 = 4-pass LSB always
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
@@ -293,16 +311,20 @@ hipError_t launch_sort_msb(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, con
 hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
                              uint32_t* counts, uint32_t* bstart, uint32_t* scratch, uint32_t* ghist4,
                              uint32_t* dense, hipStream_t s);
-// The tile-bucketed gather sort (sort_kernels.hip): keys[1]/vals[1] = K1's
-// (k_morton_tb) tile-bucketed keys, tb = its [tile][1024] run table, ghist =
-// its [1024] bucket totals -> keys[0]/vals[0].  xk/xv: n-word scratch for a
-// bucket beyond one LDS sort.  dense (a probe build): k_bucket_dense writes
-// the verdict there, the bucket kernel runs on 0 and the 4-pass LSB sort of
-// the tile-bucketed arrays on 1 (counts: the table's words, ghist4: [4][256]
-// zeroed words).
-hipError_t launch_sort_gather(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
-                              const uint32_t* tb, uint32_t* xk, uint32_t* xv, uint32_t* counts, uint32_t* ghist4,
-                              uint32_t* dense, hipStream_t s);
+// The tile-bucketed gather sort (sort_kernels.hip): words = K1's
+// (k_morton_tb) tile-bucketed words, tb = its [tile][1024] run table, ghist =
+// its [1024] bucket totals -> kout/vout sorted by (key, index).  flags: [0]
+// set when a bin of 2^10 keys' low bits held more than 64 keys (clustered:
+// exact, but the scene's later builds should use the LSB sort), [1] set when
+// a bucket did not fit one block's LDS (that bucket is NOT sorted: rebuild
+// with the LSB sort).  dense (a probe build): k_bucket_dense writes 1 there
+// when a bucket exceeds the LDS capacity, and the bucket kernel runs on 0.
+hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_t n, const uint32_t* ghist,
+                              uint32_t* kout, uint32_t* vout, uint32_t* flags, uint32_t* dense, hipStream_t s);
+// the 4-pass LSB sort of keys[0]/vals[0] (index order), every launch gated on
+// *dense == 1; ghist4 and counts[0] from k_morton<false>
+hipError_t launch_sort_lsb_gated(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist4,
+                                 uint32_t* counts, const uint32_t* dense, hipStream_t s);
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,
                            uint32_t digits, uint32_t* out_buf, hipStream_t s);
 hipError_t launch_unpack(const void* slabs, uint32_t tiles_per_slab, uint32_t w, uint32_t h, uint32_t nranks,

@@ -731,109 +731,71 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
 }
 
 // ================================================================ tile-bucketed gather sort (r04)
-// The build's MSB sort without a global prefix or a first-level scatter
-// launch.  K1 (k_morton_tb, build_kernels.hip) already sorts each 4096-key
-// tile stably by bucket d = key >> 20 and writes it bucket by bucket, with
-// tb[tile][d] = run start | run length << 16 and the bucket totals ghist[d].
-// k_bucket_gather then owns bucket d: its start is the sum of ghist below d,
-// its keys are the d-runs of every tile in tile order -- an index-ordered
-// stream, since tiles are index ranges and each run is in index order -- so
-// the two stable 10-bit LSB passes over key bits 0..19 in LDS give §9.4's
-// unique (key, index) order.  Two launches (K1 + this) instead of four
-// (K1, k_msb_scan, k_msb_scatter, k_bucket_sort), and the keys cross HBM
-// twice less.
+// The build's MSB sort without a global prefix, a first-level scatter launch
+// or any stability requirement.  K1 (k_morton_tb, build_kernels.hip) groups
+// each 4096-key tile by bucket d = key >> 20 and writes it bucket by bucket,
+// one word per key (key bits 0..19 << 12 | the key's index in its tile),
+// with tb[tile][d] = run start | run length << 16 and the bucket totals
+// ghist[d].  k_bucket_gather then owns bucket d:
+//   1. its start = the totals of the buckets below it; its runs = column d
+//      of the table, their offsets a block scan over the tiles;
+//   2. element j of the bucket (any order will do) is found by a binary
+//      search over the run offsets in LDS, so consecutive lanes read
+//      consecutive words of one run (coalesced), and decoded to (key, index);
+//   3. the bucket is grouped by bin b = key bits 10..19 (LDS atomics: one
+//      histogram pass, a scan, one scatter pass -- again in any order);
+//   4. each element's rank in its bin is the number of bin elements whose
+//      (key, index) pair is smaller: the sorted position is bin start +
+//      rank, i.e. §9.4's unique (key, index) order by construction, whatever
+//      order the atomics left -- so neither level needs a stable ranking;
+//   5. the bin-sorted bucket is written back coalesced.
+// A uniform soup's bins hold n / 2^20 keys on average, so step 4 is a short
+// loop; a bin beyond kGatherBinFast keys (clustered geometry) is still
+// exact, at O(bin^2 / 64) LDS broadcasts, and flags the scene (*slow) so its
+// later builds use the LSB sort.  A bucket beyond the block's LDS (a probe
+// build's verdict normally prevents this) flags *overflow and is left
+// unsorted: the host then rebuilds with the LSB sort.
 // Blocks are dealt to buckets XCD by XCD (dispatch order is round-robin over
 // the 8 XCDs, so block b runs on XCD b mod 8): XCD x owns buckets
 // [128x, 128x + 128), i.e. one contiguous eighth of every tile's runs and of
 // every table row, which its own L2 then serves to its 128 blocks.
-constexpr uint32_t kGatherMaxTilesPerThread = 4;  // nt <= NT * 4 (n <= NT * 16384)
-constexpr uint32_t kGatherChunk = 8;              // run words loaded per round trip (a run: ~n / 4M keys)
+constexpr uint32_t kGatherMaxTilesPerThread = 4;  // runs (tiles) per thread in step 1
+constexpr uint32_t kGatherBinFast = 64;           // bins above this many keys flag the scene as clustered
 
-// LDS words of k_bucket_gather<NT, P>: the bucket (keys | vals, 2 x NT*P;
-// first the ranking counters), s_cnt, s_run, two [16] reduction rows
-constexpr size_t gather_lds_bytes(int nt, int p) { return ((size_t)2 * nt * p + 2 * kMsbBuckets + 32) * 4; }
-
-// The two stable 10-bit passes over key bits 0..19 of m > NT*P keys through
-// global memory, chunk by chunk: (sk, sv) -> (dk, dv) -> (sk, sv), then the
-// copy to (dk, dv).  The block owns [s, s + m) of all four arrays.
-template <int NT, int P>
-__device__ void bucket_sort_global(uint32_t* sk, uint32_t* sv, uint32_t* dk, uint32_t* dv, uint32_t s, uint32_t m,
-                                   uint32_t (*s_wc)[kMsbBuckets], uint32_t* s_cnt, uint32_t* s_run, uint32_t* s_sw) {
-    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    uint32_t* const ok0 = dk;
-    uint32_t* const ov0 = dv;
-    uint32_t k[P], v[P], dg[P], r[P];
-    bool ok[P];
-    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
-        for (uint32_t j = tid; j < kMsbBuckets; j += NT) s_run[j] = 0u;
-        __syncthreads();
-        for (uint32_t j = tid; j < m; j += NT) atomicAdd(&s_run[(sk[s + j] >> shift) & (kMsbBuckets - 1)], 1u);
-        __syncthreads();
-        scan1024<NT>(s_run, s_sw);
-        for (uint32_t c0 = 0; c0 < m; c0 += (uint32_t)NT * P) {
-#pragma unroll
-            for (int i = 0; i < P; ++i) {
-                const uint32_t j = c0 + w * (64u * P) + i * 64u + l;
-                ok[i] = j < m;
-                k[i] = ok[i] ? sk[s + j] : 0u;
-                v[i] = ok[i] ? sv[s + j] : 0u;
-            }
-            bucket_rank<NT, P>(k, ok, shift, s_wc, s_cnt, dg, r);
-#pragma unroll
-            for (int i = 0; i < P; ++i)
-                if (ok[i]) {
-                    const uint32_t o = s_run[dg[i]] + r[i];
-                    dk[s + o] = k[i];
-                    dv[s + o] = v[i];
-                }
-            __syncthreads();  // s_run and s_wc reads done
-            for (uint32_t d = tid; d < kMsbBuckets; d += NT) s_run[d] += s_cnt[d];
-            __syncthreads();
-        }
-        // this pass's stores before the next pass's loads by the block's other
-        // waves (one CU: a workgroup-scope fence, not an L2 writeback)
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __syncthreads();
-        uint32_t* t0 = sk;
-        sk = dk;
-        dk = t0;
-        t0 = sv;
-        sv = dv;
-        dv = t0;
-    }
-    for (uint32_t j = tid; j < m; j += NT) {  // two passes: the result is back in the source arrays
-        ok0[s + j] = sk[s + j];
-        ov0[s + j] = sv[s + j];
-    }
+// tiles (runs per bucket) the block's LDS holds: NT * 4, less for the
+// 16-key-per-thread shape, whose bucket takes 128 KB (n <= 12.05M)
+constexpr uint32_t gather_max_tiles(int nt, int p) { return p == 16 ? 2944u : (uint32_t)nt * kGatherMaxTilesPerThread; }
+// LDS words of k_bucket_gather<NT, P>: the bucket as (key, index) pairs
+// (2 x NT*P), the bin starts and cursors (2 x 1025), the run offsets and
+// entries (2 x tiles + 1), two [16] reduction rows
+constexpr size_t gather_lds_bytes(int nt, int p) {
+    return ((size_t)2 * nt * p + 2 * (kMsbBuckets + 1) + 2 * (size_t)gather_max_tiles(nt, p) + 1 + 32) * 4;
 }
 
-// xk/xv: scratch of n words each, used only by a bucket over NT*P keys (the
-// scene's first build, before its verdict; later builds of a dense scene run
-// the LSB sort).
 template <int NT, int P>
-__global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict__ keys_tb,
-                                                      const uint32_t* __restrict__ vals_tb,
+__global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict__ words_tb,
                                                       const uint32_t* __restrict__ tb, uint32_t nt,
                                                       const uint32_t* __restrict__ ghist,
                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
-                                                      uint32_t* __restrict__ xk, uint32_t* __restrict__ xv,
+                                                      uint32_t* __restrict__ flags /* [0] slow, [1] overflow */,
                                                       Gate gate = Gate{}) {
     if (gated_off(gate)) return;
     constexpr int NW = NT / 64;
     constexpr uint32_t CAP = (uint32_t)NT * P;
-    static_assert(NW * kMsbBuckets <= 2 * CAP, "the ranking counters fit the bucket's buffer");
+    constexpr uint32_t TMAX = gather_max_tiles(NT, P);
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    uint32_t* s_key = s_dyn;
-    uint32_t* s_val = s_dyn + CAP;
-    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_dyn);
-    uint32_t* s_cnt = s_dyn + 2 * CAP;
-    uint32_t* s_run = s_cnt + kMsbBuckets;
-    uint32_t* s_sw = s_run + kMsbBuckets;  // [16]
-    uint32_t* s_sw2 = s_sw + 16;           // [16]
+    uint2* s_kv = reinterpret_cast<uint2*>(s_dyn);              // [CAP] (key, index)
+    uint32_t* s_bin = s_dyn + 2 * CAP;                          // [1025] bin counts, then starts
+    uint32_t* s_cur = s_bin + kMsbBuckets + 1;                  // [1025] bin cursors
+    uint32_t* s_off = s_cur + kMsbBuckets + 1;                  // [TMAX + 1] run offsets in the bucket
+    uint32_t* s_ent = s_off + TMAX + 1;                         // [TMAX] run entries start | len << 16
+    uint32_t* s_sw = s_ent + TMAX;                              // [16]
+    uint32_t* s_sw2 = s_sw + 16;                                // [16]
     const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t d = (b & 7u) * (kMsbBuckets / 8) + (b >> 3);  // XCD x: buckets [128x, 128x + 128)
-    // this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K)
+    for (uint32_t j = tid; j <= kMsbBuckets; j += NT) s_bin[j] = 0u;
+    // 1. this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K)
     const uint32_t K = (nt + NT - 1) / NT;
     uint32_t e[kGatherMaxTilesPerThread], csum = 0;
 #pragma unroll
@@ -842,8 +804,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
         e[k] = (k < K && t < nt) ? tb[(uint64_t)t * kMsbBuckets + d] : 0u;
         csum += e[k] >> 16;
     }
-    // the bucket's start: the totals of the buckets below it
-    uint32_t gs = 0;
+    uint32_t gs = 0;  // the bucket's start: the totals of the buckets below it
     for (uint32_t j = tid; j < d; j += NT) gs += ghist[j];
     const uint32_t m = ghist[d];
     uint32_t x = csum;
@@ -863,79 +824,82 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
         s += s_sw2[q];
     }
     if (m == 0) return;  // block-uniform
-    const bool fits = m <= CAP;
-    uint32_t* gk = fits ? s_key : xk + s;  // the gathered bucket: LDS, or scratch beyond one LDS sort
-    uint32_t* gv = fits ? s_val : xv + s;
-#pragma unroll
-    for (uint32_t k = 0; k < kGatherMaxTilesPerThread; ++k) {
-        const uint32_t c = e[k] >> 16;
-        if (c) {
-            const uint32_t src = (tid * K + k) * (uint32_t)kSortTile + (e[k] & 0xFFFFu);
-            for (uint32_t i0 = 0; i0 < c; i0 += kGatherChunk) {
-                uint32_t kk[kGatherChunk], vv[kGatherChunk];
-#pragma unroll
-                for (uint32_t i = 0; i < kGatherChunk; ++i) {
-                    kk[i] = i0 + i < c ? keys_tb[src + i0 + i] : 0u;
-                    vv[i] = i0 + i < c ? vals_tb[src + i0 + i] : 0u;
-                }
-#pragma unroll
-                for (uint32_t i = 0; i < kGatherChunk; ++i)
-                    if (i0 + i < c) {
-                        gk[off + i0 + i] = kk[i];
-                        gv[off + i0 + i] = vv[i];
-                    }
-            }
-            off += c;
-        }
-    }
-    if (!fits) {
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-        __syncthreads();
-        bucket_sort_global<NT, P>(xk, xv, kout, vout, s, m, s_wc, s_cnt, s_run, s_sw);
+    if (m > CAP) {       // block-uniform: beyond one LDS sort
+        if (tid == 0) atomicOr(flags + 1, 1u);
         return;
     }
+#pragma unroll
+    for (uint32_t k = 0; k < kGatherMaxTilesPerThread; ++k) {
+        const uint32_t t = tid * K + k;
+        if (k < K && t < nt) {
+            s_off[t] = off;
+            s_ent[t] = e[k];
+            off += e[k] >> 16;
+        }
+    }
+    if (tid == 0) s_off[nt] = m;
     __syncthreads();
-    // per items per lane: wave w holds [64 per w, 64 per (w + 1)), index order =
-    // (wave, item, lane), the ranking's order
-    const uint32_t per = (m + NT - 1) / NT;
-    uint32_t k[P], v[P], dg[P], r[P];
-    bool ok[P];
+    // 2. gather: element j = tid + i*NT; its run = the last tile t with
+    // s_off[t] <= j (empty runs share their successor's offset, so the
+    // search lands on the run that holds j); decode (key, index)
+    uint32_t key[P], val[P], bin[P];
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-        const uint32_t j = w * (64u * per) + i * 64u + l;
-        ok[i] = (uint32_t)i < per && j < m;
-        k[i] = ok[i] ? s_key[j] : 0u;
-        v[i] = ok[i] ? s_val[j] : 0u;
-    }
-    __syncthreads();  // every item in registers before the counters overwrite the buffer
-    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
-        bucket_rank<NT, P>(k, ok, shift, s_wc, s_cnt, dg, r);
-        scan1024<NT>(s_cnt, s_sw);  // its barriers also end every counter read
-#pragma unroll
-        for (int i = 0; i < P; ++i)
-            if (ok[i]) {
-                const uint32_t p = s_cnt[dg[i]] + r[i];
-                s_key[p] = k[i];
-                s_val[p] = v[i];
+        const uint32_t j = tid + (uint32_t)i * NT;
+        if (j < m) {
+            uint32_t lo = 0, hi = nt;  // s_off[lo] <= j < s_off[hi]
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_off[mid] <= j) lo = mid;
+                else hi = mid;
             }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-            const uint32_t j = w * (64u * per) + i * 64u + l;
-            if (ok[i]) {
-                k[i] = s_key[j];
-                v[i] = s_val[j];
-            }
+            const uint32_t en = s_ent[lo];
+            const uint32_t wd = words_tb[lo * (uint32_t)kSortTile + (en & 0xFFFFu) + (j - s_off[lo])];
+            key[i] = (d << kMsbShift) | (wd >> 12);
+            val[i] = lo * (uint32_t)kSortTile + (wd & 0xFFFu);
+            bin[i] = (key[i] >> 10) & (kMsbBuckets - 1);
+            atomicAdd(&s_bin[bin[i]], 1u);
         }
-        __syncthreads();
     }
+    __syncthreads();
+    // 3. bin starts (s_bin[1024] = m) and cursors, then the bin grouping
+    {
+        uint32_t mx = 0;
+        for (uint32_t j = tid; j < kMsbBuckets; j += NT) mx = max(mx, s_bin[j]);
+        if (__syncthreads_or(mx > kGatherBinFast) && tid == 0) atomicOr(flags, 1u);
+    }
+    scan1024<NT>(s_bin, s_sw);  // ends with a barrier
+    for (uint32_t j = tid; j < kMsbBuckets; j += NT) s_cur[j] = s_bin[j];
+    if (tid == 0) s_bin[kMsbBuckets] = m;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+        if (tid + (uint32_t)i * NT < m) s_kv[atomicAdd(&s_cur[bin[i]], 1u)] = make_uint2(key[i], val[i]);
+    __syncthreads();
+    // 4. rank in the bin by the (key, index) pair
+    uint32_t pos[P];
 #pragma unroll
     for (int i = 0; i < P; ++i) {
-        const uint32_t j = w * (64u * per) + i * 64u + l;
-        if (ok[i]) {
-            kout[s + j] = k[i];
-            vout[s + j] = v[i];
+        if (tid + (uint32_t)i * NT < m) {
+            const uint32_t b0 = s_bin[bin[i]], b1 = s_bin[bin[i] + 1];
+            uint32_t r = b0;
+            for (uint32_t q = b0; q < b1; ++q) {
+                const uint2 o = s_kv[q];
+                r += (o.x < key[i] || (o.x == key[i] && o.y < val[i])) ? 1u : 0u;
+            }
+            pos[i] = r;
         }
+    }
+    __syncthreads();  // every bin read
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+        if (tid + (uint32_t)i * NT < m) s_kv[pos[i]] = make_uint2(key[i], val[i]);
+    __syncthreads();
+    // 5. the sorted bucket, coalesced
+    for (uint32_t j = tid; j < m; j += NT) {
+        const uint2 o = s_kv[j];
+        kout[s + j] = o.x;
+        vout[s + j] = o.y;
     }
 }
 
@@ -945,17 +909,6 @@ __global__ __launch_bounds__(1024) void k_bucket_dense(const uint32_t* __restric
                                                        uint32_t* __restrict__ dense) {
     const int big = __syncthreads_or(ghist[threadIdx.x] > cap);
     if (threadIdx.x == 0) dense[0] = big ? 1u : 0u;
-}
-
-// copies n words of two arrays (the probe build's LSB leg ends in buffer 1)
-__global__ __launch_bounds__(256) void k_copy2(const uint32_t* __restrict__ a, const uint32_t* __restrict__ b,
-                                               uint32_t* __restrict__ ao, uint32_t* __restrict__ bo, uint32_t n,
-                                               Gate gate) {
-    if (gated_off(gate)) return;
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
-        ao[i] = a[i];
-        bo[i] = b[i];
-    }
 }
 
 // ================================================================ launchers
@@ -1080,10 +1033,10 @@ hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, c
 }
 
 // ---- the gather sort's launchers.  Block shape by n: the smallest bucket
-// block whose LDS sort holds a uniform soup's n/1024 keys with a wide margin
-// (mean + 16 sigma + 64), so a uniform scene never takes the global path
-// (a fixed 2048-key cap up to 2^21 sent uniform 2M soups to the
-// LSB sort for good).
+// block whose LDS holds a uniform soup's n/1024 keys with a wide margin
+// (mean + 16 sigma + 64), so a uniform scene never overflows one (ADVICE r03:
+// a fixed 2048-key cap up to 2^21 sent uniform 2M soups to the LSB sort for
+// good).
 struct GatherShape { int nt, p; };
 static GatherShape gather_shape(uint32_t n) {
     const double mean = (double)n / kMsbBuckets;
@@ -1097,14 +1050,14 @@ uint32_t gather_bucket_cap(uint32_t n) {
     const GatherShape g = gather_shape(n);
     return (uint32_t)(g.nt * g.p);
 }
-bool gather_sort_fits(uint32_t n) {  // tiles per bucket-block thread, and 16-bit run starts
-    return n >= 2 && sort_tiles(n) <= (uint32_t)gather_shape(n).nt * kGatherMaxTilesPerThread;
+bool gather_sort_fits(uint32_t n) {  // every run of a bucket in its block's LDS
+    const GatherShape g = gather_shape(n);
+    return n >= 2 && sort_tiles(n) <= gather_max_tiles(g.nt, g.p);
 }
 
 template <int NT, int P>
-static hipError_t gather_launch(const uint32_t* ktb, const uint32_t* vtb, const uint32_t* tb, uint32_t nt,
-                                const uint32_t* ghist, uint32_t* ko, uint32_t* vo, uint32_t* xk, uint32_t* xv,
-                                hipStream_t s, Gate g) {
+static hipError_t gather_launch(const uint32_t* words, const uint32_t* tb, uint32_t nt, const uint32_t* ghist,
+                                uint32_t* ko, uint32_t* vo, uint32_t* flags, hipStream_t s, Gate g) {
     static std::once_flag once[kMaxDevices];
     static hipError_t err[kMaxDevices];
     int dev = 0;
@@ -1112,48 +1065,39 @@ static hipError_t gather_launch(const uint32_t* ktb, const uint32_t* vtb, const 
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
     constexpr size_t lds = gather_lds_bytes(NT, P);
+    static_assert(lds <= 160 * 1024, "one block's LDS");
     std::call_once(once[dev], [dev] {
         err[dev] = hipFuncSetAttribute(reinterpret_cast<const void*>(k_bucket_gather<NT, P>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (err[dev] != hipSuccess) return err[dev];
-    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, ktb, vtb, tb, nt, ghist, ko, vo, xk, xv,
-               g);
+    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, words, tb, nt, ghist, ko, vo, flags, g);
     return hipGetLastError();
 }
 
-hipError_t launch_sort_gather(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist,
-                              const uint32_t* tb, uint32_t* xk, uint32_t* xv, uint32_t* counts, uint32_t* ghist4,
-                              uint32_t* dense, hipStream_t s) {
+hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_t n, const uint32_t* ghist,
+                              uint32_t* kout, uint32_t* vout, uint32_t* flags, uint32_t* dense, hipStream_t s) {
     if (n <= 1) return hipSuccess;
     if (!gather_sort_fits(n)) return hipErrorInvalidValue;
     const uint32_t nt = sort_tiles(n);
     const GatherShape gs = gather_shape(n);
-    hipError_t e;
     if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), dense);
     const Gate g{dense, 0u};
-    // keys[1]/vals[1]: K1's tile-bucketed keys -> keys[0]/vals[0]
-    if (gs.nt == 256) e = gather_launch<256, 8>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
-    else if (gs.nt == 512) e = gather_launch<512, 8>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
-    else if (gs.p == 12) e = gather_launch<1024, 12>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
-    else e = gather_launch<1024, 16>(keys[1], vals[1], tb, nt, ghist, keys[0], vals[0], xk, xv, s, g);
-    if (e != hipSuccess || !dense) return e;
-    // dense (a probe build whose verdict is 1): the 4-pass LSB sort of the
-    // tile-bucketed arrays -- equal keys share a bucket, and a bucket's keys
-    // are in index order there, so the stable passes still give §9.4's order
-    // -- from buffer 1 (ending there), then copied to buffer 0.  The table is
-    // spent, so the LSB passes reuse its words ([4][tile][256] = [tile][1024]).
-    const Gate g1{dense, 1u};
-    const uint64_t cs = (uint64_t)nt * 256;
+    if (gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, ghist, kout, vout, flags, s, g);
+    if (gs.nt == 512) return gather_launch<512, 8>(words, tb, nt, ghist, kout, vout, flags, s, g);
+    if (gs.p == 12) return gather_launch<1024, 12>(words, tb, nt, ghist, kout, vout, flags, s, g);
+    return gather_launch<1024, 16>(words, tb, nt, ghist, kout, vout, flags, s, g);
+}
+
+// The probe build's LSB leg when the verdict is dense (*dense == 1): K1 again
+// in index order (k_morton<false>: the keys, their 4 digit histograms and
+// pass 0's tile counts) and the 4-pass LSB sort, every launch gated.
+hipError_t launch_sort_lsb_gated(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist4,
+                                 uint32_t* counts, const uint32_t* dense, hipStream_t s) {
+    if (n <= 1) return hipSuccess;
+    const uint64_t cs = (uint64_t)sort_tiles(n) * 256;
     uint32_t* c4[4] = {counts, counts + cs, counts + 2 * cs, counts + 3 * cs};
-    uint32_t* K1[2] = {keys[1], keys[0]};
-    uint32_t* V1[2] = {vals[1], vals[0]};
-    if ((e = digit_hist(keys[1], n, ghist4, s, g1)) != hipSuccess) return e;
-    if ((e = tile_hist0(keys[1], n, c4[0], s, g1)) != hipSuccess) return e;
-    if ((e = sort_lsb(K1, V1, n, ghist4, c4, s, g1)) != hipSuccess) return e;
-    RT_KLAUNCH(k_copy2, dim3(std::min<uint32_t>(2048, sdiv(n, 256))), dim3(256), 0, s, keys[1], vals[1], keys[0], vals[0],
-               n, g1);
-    return hipGetLastError();
+    return sort_lsb(keys, vals, n, ghist4, c4, s, Gate{dense, 1u});
 }
 
 hipError_t launch_sort_top(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist, uint32_t* counts,

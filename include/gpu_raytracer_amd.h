@@ -347,6 +347,10 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * bucket gathers its runs and sorts them in LDS), 1 = the r01-r03 MSB
  * scatter + bucket sort, 0 = the 4-pass LSB radix sort; a scene whose first
  * build finds a bucket beyond one block's LDS sort keeps the LSB sort.
+ * "build.fuse_k01" 1 (default) / 0: with the gather sort, K0 (bounds) and K1
+ * (Morton) as one launch whose blocks meet at a grid barrier, when every sort
+ * tile's block fits the device at once (n up to ~2M) and no other such build
+ * runs on the device; else two launches.
  * "debug.poison" 0/1: every device buffer the library allocates from then on
  * is filled with 0xFF bytes before first use, so reading a byte no kernel
  * wrote gives the same (wrong) value every run instead of allocator luck.

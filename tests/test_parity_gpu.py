@@ -190,14 +190,16 @@ def _compare_sorts(R, tris):
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     outs = []
     try:
-        for mode in (0, 1, 2):
+        for mode, fuse in ((0, 1), (1, 1), (2, 1), (2, 0)):  # (2, 1): K0 + K1 fused where the grid fits
             R.config_set("build.sort", mode)
+            R.config_set("build.fuse_k01", fuse)
             with R.Scene.from_soup(tris) as s:
                 for _ in range(2):
                     s.build()
                     outs.append(s.read_bvh())
     finally:
         R.config_set("build.sort", SORT_DEFAULT)
+        R.config_set("build.fuse_k01", 1)
     a = outs[0]
     for b in outs[1:]:
         assert np.array_equal(a["keys"], b["keys"])
