@@ -84,6 +84,29 @@ __device__ __forceinline__ uint32_t load_tri_lanes(const float* __restrict__ tri
     return mask;
 }
 
+// the same for triangles q0 .. q0 + Q - 1 of the lane's 8 (t[q - q0])
+template <uint32_t Q>
+__device__ __forceinline__ uint32_t load_tri_lanes_part(const float* __restrict__ tris, uint32_t n, uint32_t base,
+                                                        uint32_t q0, float (&t)[Q][9]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const Vtx* p = reinterpret_cast<const Vtx*>(tris);
+    uint32_t mask = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < Q; ++q) {
+        const uint32_t k = base + (q0 + q) * 64u + lane;
+        const bool ok = k < n;
+        mask |= (ok ? 1u : 0u) << (q0 + q);
+#pragma unroll
+        for (uint32_t j = 0; j < 3; ++j) {
+            const Vtx v = ok ? p[(uint64_t)k * 3 + j] : Vtx{0.0f, 0.0f, 0.0f};
+            t[q][3 * j] = v.x;
+            t[q][3 * j + 1] = v.y;
+            t[q][3 * j + 2] = v.z;
+        }
+    }
+    return mask;
+}
+
 // ---------------------------------------------------------------- K0
 __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, uint32_t n,
                                                 float* __restrict__ partials,
@@ -308,6 +331,9 @@ struct FuseArgs {
     uint32_t* err = nullptr;   // set on a barrier timeout
 };
 static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
+#ifndef RT_K1TB_HALVES
+#define RT_K1TB_HALVES 0
+#endif
 template <bool FUSED>
 __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
                                                             BuildParams* __restrict__ params,
@@ -325,8 +351,14 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t tile = blockIdx.x, tbase = tile * (uint32_t)kSortTile;
     const uint32_t wbase = tbase + w * 64u * kTrisPerThread;
-    float t[kTrisPerThread][9];
-    const uint32_t okm = load_tri_lanes(tris, n, wbase, t);  // in flight while the bounds are reduced
+    // HALVES (the unfused kernel): the lane's 8 triangles in two batches of 4,
+    // so it holds 36 instead of 72 triangle registers -- more resident blocks
+    // per CU to overlap one block's LDS phases with the others' loads
+    constexpr bool HALVES = !FUSED && RT_K1TB_HALVES;
+    constexpr uint32_t QL = HALVES ? kTrisPerThread / 2 : kTrisPerThread;
+    float t[QL][9];
+    uint32_t okm = HALVES ? load_tri_lanes_part<QL>(tris, n, wbase, 0u, t)
+                          : load_tri_lanes(tris, n, wbase, reinterpret_cast<float(&)[kTrisPerThread][9]>(t));
     BuildParams p;
     if constexpr (FUSED) {
         // K0: the zero words, then this tile's partial centroid box, published
@@ -400,14 +432,19 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
     if (tile == 0 && threadIdx.x == 0) *params = p;
     uint32_t k8[kTrisPerThread];
 #pragma unroll
-    for (uint32_t q = 0; q < kTrisPerThread; ++q) {
-        float bmin[3], bmax[3];
-        tri_bounds(t[q], bmin, bmax);
-        uint32_t qq[3];
+    for (uint32_t h = 0; h < kTrisPerThread / QL; ++h) {
+        if (h > 0) okm |= load_tri_lanes_part<QL>(tris, n, wbase, h * QL, t);
 #pragma unroll
-        for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
-        k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
-        if ((okm >> q) & 1u) atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);  // 30-bit keys: bucket < 1024
+        for (uint32_t qi = 0; qi < QL; ++qi) {
+            const uint32_t q = h * QL + qi;
+            float bmin[3], bmax[3];
+            tri_bounds(t[qi], bmin, bmax);
+            uint32_t qq[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
+            k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
+            if ((okm >> q) & 1u) atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);  // 30-bit keys: bucket < 1024
+        }
     }
     __syncthreads();
     constexpr int PER = kMsbBuckets / kSortThreads;  // buckets per thread in scan1024's layout
@@ -1000,8 +1037,13 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         float* __restrict__ totals, uint32_t* __restrict__ cross,
                                                         uint32_t* cross_ctr, uint32_t cross_cap,
                                                         uint4* __restrict__ wnodes, uint32_t collapse,
-                                                        uint32_t block0 = 0) {
+                                                        uint32_t block0 = 0,
+                                                        const uint32_t* __restrict__ flags_src = nullptr,
+                                                        uint32_t* __restrict__ flags_dst = nullptr) {
     constexpr int T = kRefitT, NW = T / 64, KW = RT_REFIT_KEY_MARGIN;
+    // the build's verdict words (zero[kZDense ..]), final once the sort
+    // kernels have run, to the host's mapped pinned copy: no copy launch
+    if (flags_dst && blockIdx.x == 0 && threadIdx.x < 8) flags_dst[threadIdx.x] = flags_src[threadIdx.x];
     static_assert((T + 2 * KW) * 4 <= T * (int)sizeof(Aabb), "key window must fit the table buffer");
     static_assert(sizeof(uint4) <= sizeof(Aabb), "topology words must fit the table buffer");
     __shared__ Aabb s_tab[T];          // key window first (uint32), then the odd sparse-table levels
@@ -1447,23 +1489,25 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
 // K4 + K5 + K6-local + K7w-local (k_topo_refit) over sorted keys/vals in
 // keys[0]/vals[0]; expects the crossing-list counters zeroed (K0 does it).
 static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
-                                     uint32_t block0, uint32_t nblocks, hipStream_t s) {
+                                     uint32_t block0, uint32_t nblocks, hipStream_t s,
+                                     uint32_t* host_flags = nullptr) {
+    const uint32_t* fsrc = host_flags ? b.zero + kZDense : nullptr;
     const uint32_t m = cdiv(n, kRefitT);
     if (arity == 8)
         RT_KLAUNCH(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags);
     else
         RT_KLAUNCH(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags);
     return hipGetLastError();
 }
 
 static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
-                                    hipStream_t s) {
+                                    hipStream_t s, uint32_t* host_flags = nullptr) {
     if (!n) return hipSuccess;
-    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s);
+    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s, host_flags);
 }
 
 hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
@@ -1575,7 +1619,8 @@ bool fused_k01_fits(uint32_t n) {
 }
 
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEvents* ev, bool stages,
-                        const TraceConfig& cfg, uint32_t* probed, bool allow_fused, bool* fused_out) {
+                        const TraceConfig& cfg, uint32_t* probed, bool allow_fused, bool* fused_out,
+                        uint32_t* host_flags) {
     hipError_t e;
     if (probed) *probed = 0;
     if (fused_out) *fused_out = false;
@@ -1638,7 +1683,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     if (e != hipSuccess) return e;
     if (probe && probed) *probed = kind;
     if ((e = rec(3)) != hipSuccess) return e;
-    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
+    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s, host_flags)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
     if (n && (e = launch_cross(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;

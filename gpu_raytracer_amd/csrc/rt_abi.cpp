@@ -56,7 +56,8 @@ struct Replica {
     bool uploaded = false, built = false;
     uint32_t msb_probe = 0;  // the sort (1 MSB, 2 gather) whose verdict this build wrote (BuildBufs::sort_mode)
     bool fused = false;      // this build ran K0 + K1 fused (its barrier's timeout flag is in h_flag)
-    uint32_t* h_flag = nullptr;  // pinned host copy of zero[kZDense .. kZDense + 8): the build's verdict words
+    uint32_t* h_flag = nullptr;  // mapped pinned host copy of zero[kZDense .. kZDense + 8): the build's verdict words
+    uint32_t* d_flag = nullptr;  // its device-side address
     rt::BuildEvents ev;
     rt_build_times times{};
     // render scratch (grown on demand)
@@ -398,12 +399,16 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
                 allow = true;
             }
         }
-        if (!r->h_flag) HIPR(hipHostMalloc(reinterpret_cast<void**>(&r->h_flag), 32, hipHostMallocDefault));
+        if (!r->h_flag) {
+            HIPR(hipHostMalloc(reinterpret_cast<void**>(&r->h_flag), 32, hipHostMallocMapped));
+            HIPR(hipHostGetDevicePointer(reinterpret_cast<void**>(&r->d_flag), r->h_flag, 0));
+        }
+        for (int i = 0; i < 8; ++i) r->h_flag[i] = 0;
+        // the build's verdict words land in h_flag (written by its last
+        // kernels, read after the synchronize below: no copy launch)
         hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, &r->msb_probe, allow,
-                                        &r->fused);
+                                        &r->fused, r->d_flag);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
-        // the build's verdict words, read after the synchronize below (no extra sync)
-        HIPR(hipMemcpyAsync(r->h_flag, r->bufs.zero + rt::kZDense, 32, hipMemcpyDeviceToHost, r->stream));
     }
     double worst = 0.0;
     for (Replica* r : targets) {

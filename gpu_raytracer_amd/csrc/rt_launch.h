@@ -85,9 +85,13 @@ struct BuildEvents { hipEvent_t e[7]; bool valid = false; };
 // as one launch with a grid barrier when the gather sort is used and the
 // grid fits the device at once (fused_k01_fits).  *fused_out: whether it did
 // (the caller then checks zero[kZFuseErr] after the build).
+// host_flags (nullable): device pointer of 8 mapped pinned host words that
+// receive zero[kZDense .. kZDense + 8) at the end of the build (k_topo_refit
+// block 0 writes them; n >= 1), the verdict words the caller reads after its
+// synchronize.
 hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t stream, BuildEvents* ev, bool stages,
                         const TraceConfig& cfg, uint32_t* probed, bool allow_fused = false,
-                        bool* fused_out = nullptr);
+                        bool* fused_out = nullptr, uint32_t* host_flags = nullptr);
 bool fused_k01_fits(uint32_t n);  // every sort tile's block co-resident on the current device
 std::mutex& fused_gate(int device);
 // the sort launch_build would use: 0 LSB, 1 MSB scatter, 2 gather

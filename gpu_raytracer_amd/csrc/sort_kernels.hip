@@ -839,28 +839,38 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     }
     if (tid == 0) s_off[nt] = m;
     __syncthreads();
-    // 2. gather: element j = tid + i*NT; its run = the last tile t with
+    // 2. gather: element j = tid + i*NT; its run = the last tile t < nt with
     // s_off[t] <= j (empty runs share their successor's offset, so the
-    // search lands on the run that holds j); decode (key, index)
-    uint32_t key[P], val[P], bin[P];
+    // search lands on the run that holds j), by a fixed-depth search run
+    // step-major over the thread's items (P independent LDS reads in
+    // flight per step); then decode (key, index)
+    uint32_t key[P], val[P], bin[P], lo[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) lo[i] = 0;
+    for (uint32_t step = 1u << (31 - __clz((int)nt)); step; step >>= 1) {
+#pragma unroll
+        for (int i = 0; i < P; ++i) {
+            const uint32_t j = tid + (uint32_t)i * NT;
+            const uint32_t c = lo[i] + step;
+            if (j < m && c < nt && s_off[c] <= j) lo[i] = c;
+        }
+    }
 #pragma unroll
     for (int i = 0; i < P; ++i) {
         const uint32_t j = tid + (uint32_t)i * NT;
         if (j < m) {
-            uint32_t lo = 0, hi = nt;  // s_off[lo] <= j < s_off[hi]
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (s_off[mid] <= j) lo = mid;
-                else hi = mid;
-            }
-            const uint32_t en = s_ent[lo];
-            const uint32_t wd = words_tb[lo * (uint32_t)kSortTile + (en & 0xFFFFu) + (j - s_off[lo])];
+            const uint32_t t = lo[i], en = s_ent[t];
+            const uint32_t wd = words_tb[t * (uint32_t)kSortTile + (en & 0xFFFFu) + (j - s_off[t])];
             key[i] = (d << kMsbShift) | (wd >> 12);
-            val[i] = lo * (uint32_t)kSortTile + (wd & 0xFFFu);
+            val[i] = t * (uint32_t)kSortTile + (wd & 0xFFFu);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+        if (tid + (uint32_t)i * NT < m) {
             bin[i] = (key[i] >> 10) & (kMsbBuckets - 1);
             atomicAdd(&s_bin[bin[i]], 1u);
         }
-    }
     __syncthreads();
     // 3. bin starts (s_bin[1024] = m) and cursors, then the bin grouping
     {
@@ -876,20 +886,32 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     for (int i = 0; i < P; ++i)
         if (tid + (uint32_t)i * NT < m) s_kv[atomicAdd(&s_cur[bin[i]], 1u)] = make_uint2(key[i], val[i]);
     __syncthreads();
-    // 4. rank in the bin by the (key, index) pair
-    uint32_t pos[P];
+    // 4. rank in the bin by the (key, index) pair; item-interleaved, so the
+    // thread's P bin reads of one step are in flight together
+    uint32_t pos[P], len[P], kmax = 0;
 #pragma unroll
     for (int i = 0; i < P; ++i) {
+        pos[i] = 0;
+        len[i] = 0;
         if (tid + (uint32_t)i * NT < m) {
-            const uint32_t b0 = s_bin[bin[i]], b1 = s_bin[bin[i] + 1];
-            uint32_t r = b0;
-            for (uint32_t q = b0; q < b1; ++q) {
-                const uint2 o = s_kv[q];
-                r += (o.x < key[i] || (o.x == key[i] && o.y < val[i])) ? 1u : 0u;
-            }
-            pos[i] = r;
+            pos[i] = s_bin[bin[i]];
+            len[i] = s_bin[bin[i] + 1] - pos[i];
+            kmax = max(kmax, len[i]);
         }
     }
+    uint32_t r[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) r[i] = 0;
+    for (uint32_t k = 0; k < kmax; ++k) {
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            if (k < len[i]) {
+                const uint2 o = s_kv[pos[i] + k];
+                r[i] += (o.x < key[i] || (o.x == key[i] && o.y < val[i])) ? 1u : 0u;
+            }
+    }
+#pragma unroll
+    for (int i = 0; i < P; ++i) pos[i] += r[i];
     __syncthreads();  // every bin read
 #pragma unroll
     for (int i = 0; i < P; ++i)

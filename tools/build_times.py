@@ -1,21 +1,31 @@
 """Median build-stage times (hipEvents) of rt_bvh_build on the soup.
-usage: RT_LIB=<lib.so> [RT_CFG=key=v,key=v] python tools/build_times.py [n] [reps] [key=v,key=v]"""
+usage: python tools/build_times.py [n] [reps] [key=v,key=v,...]
+  keys are rt_config_set knobs, plus lib=<path> (a librtamd variant, e.g.
+  from tools/build_exp.sh; default: the in-tree library, or $RT_LIB).
+  $RT_CFG adds knobs the same way."""
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-import numpy as np  # noqa: E402
-import gpu_raytracer_amd as R  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+cfgs = [kv for kv in (os.environ.get("RT_CFG", "") + "," + (sys.argv[3] if len(sys.argv) > 3 else "")).split(",") if kv]
+knobs = []
+for kv in cfgs:
+    k, v = kv.split("=", 1)
+    if k == "lib":
+        os.environ["RT_LIB"] = os.path.abspath(os.path.join(ROOT, v) if not os.path.isabs(v) else v)
+    else:
+        knobs.append((k, int(v)))
+
+import numpy as np  # noqa: E402
+import gpu_raytracer_amd as R  # noqa: E402
+
 R.config_set("timing.event_fence", int(os.environ.get("RT_EVENT_FENCE", "0")))
-cfgs = os.environ.get("RT_CFG", "") + ("," + sys.argv[3] if len(sys.argv) > 3 else "")
-os.environ["RT_CFG"] = cfgs.strip(",")
-for kv in filter(None, cfgs.split(",")):
-    k, v = kv.split("=")
-    R.config_set(k, int(v))
+for k, v in knobs:
+    R.config_set(k, v)
 s = R.Scene.generate_soup(n, 1)
 rows, tot = [], []
 R.config_set("build.stage_events", 1)
@@ -31,6 +41,6 @@ for i in range(reps + 3):
         tot.append(ms)
 m = np.median(np.array(rows), 0) * 1e3
 lib = os.path.basename(os.environ.get("RT_LIB", "librtamd.so")) + (" fence" if os.environ.get("RT_EVENT_FENCE") == "1" else "")
-lib += (" " + os.environ["RT_CFG"]) if os.environ.get("RT_CFG") else ""
+lib += " " + ",".join(f"{k}={v}" for k, v in knobs) if knobs else ""
 print(f"{lib:<24s} n={n} us: bounds {m[0]:6.1f} morton {m[1]:6.1f} sort {m[2]:6.1f} topo {m[3]:6.1f} "
       f"refit {m[4]:6.1f} wide {m[5]:5.1f} total(stage events) {m[6]:6.1f}  total {np.median(tot) * 1e3:6.1f}")
