@@ -763,13 +763,47 @@ constexpr uint32_t kGatherMaxTilesPerThread = 4;  // runs (tiles) per thread in 
 constexpr uint32_t kGatherBinFast = 64;           // bins above this many keys flag the scene as clustered
 
 // tiles (runs per bucket) the block's LDS holds: NT * 4, less for the
-// 16-key-per-thread shape, whose bucket takes 128 KB (n <= 12.05M)
-constexpr uint32_t gather_max_tiles(int nt, int p) { return p == 16 ? 2944u : (uint32_t)nt * kGatherMaxTilesPerThread; }
+// 12- and 16-key-per-thread shapes, whose buckets take 96 / 128 KB (n <= 12.05M)
+constexpr uint32_t gather_max_tiles(int nt, int p) { return p >= 12 ? 2944u : (uint32_t)nt * kGatherMaxTilesPerThread; }
+// bin width by shape: key bits [20 - BB, 20), so a uniform soup's bins hold
+// ~1-2 keys (1M: 977 keys per bucket over 1024 bins; 10M: 9766 over 4096)
+constexpr int gather_bin_bits(int nt, int p) { return nt * p >= 12288 && p < 16 ? 12 : nt * p >= 4096 && p < 16 ? 11 : 10; }
 // LDS words of k_bucket_gather<NT, P>: the bucket as (key, index) pairs
-// (2 x NT*P), the bin starts and cursors (2 x 1025), the run offsets and
-// entries (2 x tiles + 1), two [16] reduction rows
+// (2 x NT*P; first the run marks), the bin starts and cursors (2 x (2^BB +
+// 1)), the run offsets and entries (2 x tiles + 1), two [16] reduction rows
 constexpr size_t gather_lds_bytes(int nt, int p) {
-    return ((size_t)2 * nt * p + 2 * (kMsbBuckets + 1) + 2 * (size_t)gather_max_tiles(nt, p) + 1 + 32) * 4;
+    return ((size_t)2 * nt * p + 2 * ((1u << gather_bin_bits(nt, p)) + 1) + 2 * (size_t)gather_max_tiles(nt, p) + 1 +
+            32) * 4;
+}
+
+// In-place exclusive scan of a[N] in LDS by NT threads (N a multiple of NT;
+// a written before a barrier); thread t owns a[t * N/NT ..].  Ends with a barrier.
+template <int NT, int N>
+__device__ __forceinline__ void scan_lds(uint32_t* a, uint32_t* s_sw /* [NT / 64] */) {
+    constexpr int PER = N / NT;
+    const uint32_t t = threadIdx.x, l = t & 63, w = t >> 6;
+    uint32_t v[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        v[j] = a[t * PER + j];
+        sum += v[j];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (l >= (uint32_t)o) x += y;
+    }
+    if (l == 63) s_sw[w] = x;
+    __syncthreads();
+    uint32_t pre = x - sum;
+    for (uint32_t k = 0; k < w; ++k) pre += s_sw[k];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        a[t * PER + j] = pre;
+        pre += v[j];
+    }
+    __syncthreads();
 }
 
 template <int NT, int P>
@@ -783,18 +817,22 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     constexpr int NW = NT / 64;
     constexpr uint32_t CAP = (uint32_t)NT * P;
     constexpr uint32_t TMAX = gather_max_tiles(NT, P);
+    constexpr int BB = gather_bin_bits(NT, P);
+    constexpr uint32_t NB = 1u << BB;
+    constexpr uint32_t BSH = kMsbShift - BB;  // bin = key bits [BSH, 20)
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dyn[];
-    uint2* s_kv = reinterpret_cast<uint2*>(s_dyn);              // [CAP] (key, index)
-    uint32_t* s_bin = s_dyn + 2 * CAP;                          // [1025] bin counts, then starts
-    uint32_t* s_cur = s_bin + kMsbBuckets + 1;                  // [1025] bin cursors
-    uint32_t* s_off = s_cur + kMsbBuckets + 1;                  // [TMAX + 1] run offsets in the bucket
+    uint2* s_kv = reinterpret_cast<uint2*>(s_dyn);              // [CAP] (key, index); first the run marks
+    uint32_t* s_mark = s_dyn;                                   // [CAP] run index of each bucket position
+    uint32_t* s_bin = s_dyn + 2 * CAP;                          // [NB + 1] bin counts, then starts
+    uint32_t* s_cur = s_bin + NB + 1;                           // [NB + 1] bin cursors
+    uint32_t* s_off = s_cur + NB + 1;                           // [TMAX + 1] run offsets in the bucket
     uint32_t* s_ent = s_off + TMAX + 1;                         // [TMAX] run entries start | len << 16
     uint32_t* s_sw = s_ent + TMAX;                              // [16]
     uint32_t* s_sw2 = s_sw + 16;                                // [16]
     const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t d = (b & 7u) * (kMsbBuckets / 8) + (b >> 3);  // XCD x: buckets [128x, 128x + 128)
-    for (uint32_t j = tid; j <= kMsbBuckets; j += NT) s_bin[j] = 0u;
+    for (uint32_t j = tid; j <= NB; j += NT) s_bin[j] = 0u;
     // 1. this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K)
     const uint32_t K = (nt + NT - 1) / NT;
     uint32_t e[kGatherMaxTilesPerThread], csum = 0;
@@ -828,65 +866,84 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
         if (tid == 0) atomicOr(flags + 1, 1u);
         return;
     }
+    // 2. run index of every bucket position: each non-empty run marks its
+    // first position with its tile, then an inclusive max-scan fills the
+    // rest (tiles increase along the bucket); thread tid scans the
+    // contiguous positions [tid*per, tid*per + per)
+    const uint32_t per = (m + NT - 1) / NT;
+    for (uint32_t j = tid; j < m; j += NT) s_mark[j] = 0u;
+    __syncthreads();
 #pragma unroll
     for (uint32_t k = 0; k < kGatherMaxTilesPerThread; ++k) {
         const uint32_t t = tid * K + k;
         if (k < K && t < nt) {
             s_off[t] = off;
             s_ent[t] = e[k];
+            if (e[k] >> 16) s_mark[off] = t;
             off += e[k] >> 16;
         }
     }
-    if (tid == 0) s_off[nt] = m;
     __syncthreads();
-    // 2. gather: element j = tid + i*NT; its run = the last tile t < nt with
-    // s_off[t] <= j (empty runs share their successor's offset, so the
-    // search lands on the run that holds j), by a fixed-depth search run
-    // step-major over the thread's items (P independent LDS reads in
-    // flight per step); then decode (key, index)
-    uint32_t key[P], val[P], bin[P], lo[P];
+    {
+        uint32_t run = 0;
+        for (uint32_t i = 0; i < per; ++i) {
+            const uint32_t j = tid * per + i;
+            if (j < m) run = max(run, s_mark[j]);
+        }
+        uint32_t y = run;  // inclusive max-scan over the threads' chunks
 #pragma unroll
-    for (int i = 0; i < P; ++i) lo[i] = 0;
-    for (uint32_t step = 1u << (31 - __clz((int)nt)); step; step >>= 1) {
-#pragma unroll
-        for (int i = 0; i < P; ++i) {
-            const uint32_t j = tid + (uint32_t)i * NT;
-            const uint32_t c = lo[i] + step;
-            if (j < m && c < nt && s_off[c] <= j) lo[i] = c;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t z = __shfl_up(y, o, 64);
+            if (l >= (uint32_t)o) y = max(y, z);
+        }
+        if (l == 63) s_sw2[w] = y;
+        __syncthreads();
+        uint32_t carry = __shfl_up(y, 1, 64);
+        carry = l ? carry : 0u;
+        for (uint32_t q = 0; q < w; ++q) carry = max(carry, s_sw2[q]);
+        for (uint32_t i = 0; i < per; ++i) {
+            const uint32_t j = tid * per + i;
+            if (j < m) {
+                carry = max(carry, s_mark[j]);
+                s_mark[j] = carry;
+            }
         }
     }
+    __syncthreads();
+    // 3. gather: element j = tid + i*NT (consecutive lanes read consecutive
+    // words of a run) and decode (key, index)
+    uint32_t key[P], val[P], bin[P];
 #pragma unroll
     for (int i = 0; i < P; ++i) {
         const uint32_t j = tid + (uint32_t)i * NT;
         if (j < m) {
-            const uint32_t t = lo[i], en = s_ent[t];
+            const uint32_t t = s_mark[j], en = s_ent[t];
             const uint32_t wd = words_tb[t * (uint32_t)kSortTile + (en & 0xFFFFu) + (j - s_off[t])];
             key[i] = (d << kMsbShift) | (wd >> 12);
             val[i] = t * (uint32_t)kSortTile + (wd & 0xFFFu);
+            bin[i] = (key[i] >> BSH) & (NB - 1);
         }
     }
 #pragma unroll
     for (int i = 0; i < P; ++i)
-        if (tid + (uint32_t)i * NT < m) {
-            bin[i] = (key[i] >> 10) & (kMsbBuckets - 1);
-            atomicAdd(&s_bin[bin[i]], 1u);
-        }
+        if (tid + (uint32_t)i * NT < m) atomicAdd(&s_bin[bin[i]], 1u);
     __syncthreads();
-    // 3. bin starts (s_bin[1024] = m) and cursors, then the bin grouping
+    // 4. bin starts (s_bin[NB] = m) and cursors, then the bin grouping (the
+    // marks are dead: s_kv takes their words)
     {
         uint32_t mx = 0;
-        for (uint32_t j = tid; j < kMsbBuckets; j += NT) mx = max(mx, s_bin[j]);
+        for (uint32_t j = tid; j < NB; j += NT) mx = max(mx, s_bin[j]);
         if (__syncthreads_or(mx > kGatherBinFast) && tid == 0) atomicOr(flags, 1u);
     }
-    scan1024<NT>(s_bin, s_sw);  // ends with a barrier
-    for (uint32_t j = tid; j < kMsbBuckets; j += NT) s_cur[j] = s_bin[j];
-    if (tid == 0) s_bin[kMsbBuckets] = m;
+    scan_lds<NT, (int)NB>(s_bin, s_sw);  // ends with a barrier
+    for (uint32_t j = tid; j < NB; j += NT) s_cur[j] = s_bin[j];
+    if (tid == 0) s_bin[NB] = m;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < P; ++i)
         if (tid + (uint32_t)i * NT < m) s_kv[atomicAdd(&s_cur[bin[i]], 1u)] = make_uint2(key[i], val[i]);
     __syncthreads();
-    // 4. rank in the bin by the (key, index) pair; item-interleaved, so the
+    // 5. rank in the bin by the (key, index) pair; item-interleaved, so the
     // thread's P bin reads of one step are in flight together
     uint32_t pos[P], len[P], kmax = 0;
 #pragma unroll
@@ -917,7 +974,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     for (int i = 0; i < P; ++i)
         if (tid + (uint32_t)i * NT < m) s_kv[pos[i]] = make_uint2(key[i], val[i]);
     __syncthreads();
-    // 5. the sorted bucket, coalesced
+    // 6. the sorted bucket, coalesced
     for (uint32_t j = tid; j < m; j += NT) {
         const uint2 o = s_kv[j];
         kout[s + j] = o.x;
