@@ -619,10 +619,26 @@ __device__ __forceinline__ LeafTri gather_leaf(uint32_t prim, const float* __res
     return t;
 }
 
+// The end, in direction d, of the run of sorted positions whose keys share
+// their top L bits with key ki (ki's bucket bid = ki >> 20), when L <= 12:
+// such a prefix covers only bucket bits (bits 31..30 of a 30-bit key are 0),
+// so the run is a range of whole buckets and its ends are bucket starts
+// (bstart[1025]).  This answers §9.5's searches for the long ranges of the
+// top tree levels -- whose keys differ in the bucket bits -- with two loads
+// instead of a wave-wide search through global memory.
+__device__ __forceinline__ uint32_t bucket_run_end(const uint32_t* __restrict__ bstart, uint32_t ki, int L, int d,
+                                                   uint32_t n) {
+    const int shift = 12 - L;  // bucket bits below the prefix
+    if (shift >= 10) return d > 0 ? n - 1 : 0u;
+    const uint32_t g = (ki >> kMsbShift) >> shift;
+    return d > 0 ? bstart[(g + 1) << shift] - 1 : bstart[g << shift];
+}
+
 __device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafTri& lt, uint32_t n, uint32_t i32,
                                                  uint4* __restrict__ topo, uint32_t* __restrict__ parent,
                                                  void* __restrict__ nodes, float4* __restrict__ tri_s, uint4& tp_out,
-                                                 Aabb& box, bool allow_defer, bool& deferred, bool leaf_node = false) {
+                                                 Aabb& box, bool allow_defer, bool& deferred, bool leaf_node = false,
+                                                 const uint32_t* __restrict__ bstart = nullptr) {
     const int64_t i = i32, N = n;
     const uint32_t L0 = n - 1;
     if (i32 == 0 && parent) parent[0] = RT_SENT;  // root: internal 0, or leaf 0 when n == 1
@@ -646,7 +662,22 @@ __device__ __forceinline__ void karras_node_leaf(const KeyWin& keys, const LeafT
             if (!(kdelta32(keys, n, i32, ki, q) > dmin)) break;
             lmax <<= 1;
         }
-        if (!deferred) {
+        if (deferred && bstart && dmin <= 11) {
+            // the range leaves the key window: its end is a bucket boundary
+            // (dmin + 1 <= 12 prefix bits); so is the split when the range's
+            // ends differ in their bucket (dnode <= 11)
+            const uint32_t j = bucket_run_end(bstart, ki, dmin + 1, d, n);
+            const int dnode = kdelta32(keys, n, i32, ki, j);
+            if (dnode <= 11) {
+                const uint32_t l = d > 0 ? j - i32 : i32 - j;
+                const uint32_t g = bucket_run_end(bstart, ki, dnode + 1, d, n);
+                const uint32_t sp = d > 0 ? g - i32 : i32 - g;
+                tp_out = karras_finish(keys, N, i, d, (int64_t)l, (int64_t)sp, topo, parent);
+                deferred = false;
+            } else {
+                tp_out = make_uint4(0, 0, d > 0 ? i32 : 0u, d > 0 ? RT_SENT - 1 : i32);
+            }
+        } else if (!deferred) {
             uint32_t l = 0;
             for (uint32_t t = lmax >> 1; t >= 1; t >>= 1)
                 if (kdelta32(keys, n, i32, ki, i32 + (l + t) * ud) > dmin) l += t;
@@ -1039,7 +1070,8 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         uint4* __restrict__ wnodes, uint32_t collapse,
                                                         uint32_t block0 = 0,
                                                         const uint32_t* __restrict__ flags_src = nullptr,
-                                                        uint32_t* __restrict__ flags_dst = nullptr) {
+                                                        uint32_t* __restrict__ flags_dst = nullptr,
+                                                        const uint32_t* __restrict__ bstart = nullptr) {
     constexpr int T = kRefitT, NW = T / 64, KW = RT_REFIT_KEY_MARGIN;
     // the build's verdict words (zero[kZDense ..]), final once the sort
     // kernels have run, to the host's mapped pinned copy: no copy launch
@@ -1075,7 +1107,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         bool deferred = false;
         // topology words stay in registers/LDS: only the crossing nodes' go to
         // global memory (step 2), for k_refit_cross / k_wide_cross
-        if (valid) karras_node_leaf(keys, lt, n, k, nullptr, parent, nodes, tri_s, tp, box, true, deferred);
+        if (valid) karras_node_leaf(keys, lt, n, k, nullptr, parent, nodes, tri_s, tp, box, true, deferred, false, bstart);
         karras_wave_search(keys, n, k, deferred, nullptr, parent, tp);
     }
     s_box[tid] = box;
@@ -1490,24 +1522,26 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
 // keys[0]/vals[0]; expects the crossing-list counters zeroed (K0 does it).
 static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
                                      uint32_t block0, uint32_t nblocks, hipStream_t s,
-                                     uint32_t* host_flags = nullptr) {
+                                     uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr) {
     const uint32_t* fsrc = host_flags ? b.zero + kZDense : nullptr;
     const uint32_t m = cdiv(n, kRefitT);
     if (arity == 8)
         RT_KLAUNCH(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart);
     else
         RT_KLAUNCH(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart);
     return hipGetLastError();
 }
 
+// bstart (nullable): the [1025] bucket starts of the keys' top 10 bits (an
+// MSB or gather sort wrote them), for the long-range nodes' closed form
 static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
-                                    hipStream_t s, uint32_t* host_flags = nullptr) {
+                                    hipStream_t s, uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr) {
     if (!n) return hipSuccess;
-    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s, host_flags);
+    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s, host_flags, bstart);
 }
 
 hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
@@ -1662,7 +1696,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
         // keys[1] = K1's tile-bucketed words -> keys[0]/vals[0]
         uint32_t* dense = probe ? b.zero + kZDense : nullptr;
         e = launch_sort_gather(b.keys[1], b.counts, n, b.zero + kZHist, b.keys[0], b.vals[0], b.zero + kZGatherFlags,
-                               dense, s);
+                               b.bstart, dense, s);
         if (e == hipSuccess && dense) {  // the LSB leg of a dense probe build: K1 again, in index order
             RT_KLAUNCH(k_morton<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params,
                        (const float*)nullptr, 0u, b.keys[0], b.vals[0], b.zero + kZHist4, counts[0], 0u,
@@ -1683,7 +1717,10 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     if (e != hipSuccess) return e;
     if (probe && probed) *probed = kind;
     if ((e = rec(3)) != hipSuccess) return e;
-    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s, host_flags)) != hipSuccess) return e;
+    // bucket starts: written by the MSB/gather sort (a dense probe build's LSB
+    // leg leaves them stale: that build searches as before)
+    const uint32_t* bst = (kind != 0 && !probe) ? b.bstart : nullptr;
+    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s, host_flags, bst)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
     if (n && (e = launch_cross(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;

@@ -323,8 +323,10 @@ hipError_t launch_sort_probe(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, c
 // a bucket did not fit one block's LDS (that bucket is NOT sorted: rebuild
 // with the LSB sort).  dense (a probe build): k_bucket_dense writes 1 there
 // when a bucket exceeds the LDS capacity, and the bucket kernel runs on 0.
+// bstart: [1025] bucket starts written by the bucket blocks.
 hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_t n, const uint32_t* ghist,
-                              uint32_t* kout, uint32_t* vout, uint32_t* flags, uint32_t* dense, hipStream_t s);
+                              uint32_t* kout, uint32_t* vout, uint32_t* flags, uint32_t* bstart, uint32_t* dense,
+                              hipStream_t s);
 // the 4-pass LSB sort of keys[0]/vals[0] (index order), every launch gated on
 // *dense == 1; ghist4 and counts[0] from k_morton<false>
 hipError_t launch_sort_lsb_gated(uint32_t* keys[2], uint32_t* vals[2], uint32_t n, const uint32_t* ghist4,

@@ -812,6 +812,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ ghist,
                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                       uint32_t* __restrict__ flags /* [0] slow, [1] overflow */,
+                                                      uint32_t* __restrict__ bstart /* [1025] bucket starts */,
                                                       Gate gate = Gate{}) {
     if (gated_off(gate)) return;
     constexpr int NW = NT / 64;
@@ -860,6 +861,10 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     for (uint32_t q = 0; q < (uint32_t)NW; ++q) {
         if (q < w) off += s_sw[q];
         s += s_sw2[q];
+    }
+    if (tid == 0) {  // the bucket starts, for k_topo_refit's long-range nodes
+        bstart[d] = s;
+        if (d == kMsbBuckets - 1) bstart[kMsbBuckets] = s + m;
     }
     if (m == 0) return;  // block-uniform
     if (m > CAP) {       // block-uniform: beyond one LDS sort
@@ -1136,7 +1141,7 @@ bool gather_sort_fits(uint32_t n) {  // every run of a bucket in its block's LDS
 
 template <int NT, int P>
 static hipError_t gather_launch(const uint32_t* words, const uint32_t* tb, uint32_t nt, const uint32_t* ghist,
-                                uint32_t* ko, uint32_t* vo, uint32_t* flags, hipStream_t s, Gate g) {
+                                uint32_t* ko, uint32_t* vo, uint32_t* flags, uint32_t* bstart, hipStream_t s, Gate g) {
     static std::once_flag once[kMaxDevices];
     static hipError_t err[kMaxDevices];
     int dev = 0;
@@ -1150,22 +1155,24 @@ static hipError_t gather_launch(const uint32_t* words, const uint32_t* tb, uint3
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (err[dev] != hipSuccess) return err[dev];
-    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, words, tb, nt, ghist, ko, vo, flags, g);
+    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, words, tb, nt, ghist, ko, vo, flags, bstart,
+               g);
     return hipGetLastError();
 }
 
 hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_t n, const uint32_t* ghist,
-                              uint32_t* kout, uint32_t* vout, uint32_t* flags, uint32_t* dense, hipStream_t s) {
+                              uint32_t* kout, uint32_t* vout, uint32_t* flags, uint32_t* bstart, uint32_t* dense,
+                              hipStream_t s) {
     if (n <= 1) return hipSuccess;
     if (!gather_sort_fits(n)) return hipErrorInvalidValue;
     const uint32_t nt = sort_tiles(n);
     const GatherShape gs = gather_shape(n);
     if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), dense);
     const Gate g{dense, 0u};
-    if (gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, ghist, kout, vout, flags, s, g);
-    if (gs.nt == 512) return gather_launch<512, 8>(words, tb, nt, ghist, kout, vout, flags, s, g);
-    if (gs.p == 12) return gather_launch<1024, 12>(words, tb, nt, ghist, kout, vout, flags, s, g);
-    return gather_launch<1024, 16>(words, tb, nt, ghist, kout, vout, flags, s, g);
+    if (gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
+    if (gs.nt == 512) return gather_launch<512, 8>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
+    if (gs.p == 12) return gather_launch<1024, 12>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
+    return gather_launch<1024, 16>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
 }
 
 // The probe build's LSB leg when the verdict is dense (*dense == 1): K1 again
