@@ -25,7 +25,8 @@ from collections import defaultdict
 
 BUILD = ("k_bounds", "k_morton", "k_msb_scan", "k_msb_scatter", "k_bucket_sort", "k_tile_hist", "k_scatter",
          "k_scan_tiles", "k_topo_refit", "k_refit_cross", "k_wide_cross", "k_sparse_level", "k_sparse_near", "k_sparse_far", "k_bounds_final",
-         "k_msb_chunk_sum", "k_msb_chunk_apply", "k_msb_scatter_big", "k_bucket_sort_big")
+         "k_msb_chunk_sum", "k_msb_chunk_apply", "k_msb_scatter_big", "k_bucket_sort_big",
+         "k_morton_tb", "k_bucket_gather", "k_bucket_dense", "k_digit_hist")
 
 
 def short(name):
