@@ -316,8 +316,10 @@ __device__ __forceinline__ bool grid_sync(uint32_t* bar, uint32_t nblocks, uint3
 // free, since the second level orders by the whole (key, index) pair) and
 // written bucket by bucket as ONE word per key, key bits 0..19 << 12 | the
 // key's index inside the tile (the bucket is the run's, the tile the
-// table row's), with tb[tile][d] = run start | run length << 16 and the
-// global bucket totals in ghist[1024].  No global prefix over tiles exists:
+// table row's), with tb[tile][d] = run start | run length << 16 (the
+// bucket's total and start are sums over the table's column); ghist
+// (nullable: a scene's first build only, for its verdict) gets the global
+// bucket totals.  No global prefix over tiles exists:
 // each bucket's block gathers its runs from every tile.
 // FUSED (the grid must be co-resident, launch_build
 // checks): K0 in the same launch -- the block's triangles, loaded once, give
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
     for (int j = 0; j < PER; ++j) {
         const uint32_t d = threadIdx.x * PER + j;
         tb[(uint64_t)tile * kMsbBuckets + d] = s_start[d] | (cnt[j] << 16);
-        if (cnt[j]) atomicAdd(&ghist[d], cnt[j]);
+        if (ghist && cnt[j]) atomicAdd(&ghist[d], cnt[j]);  // a probe build's verdict needs the totals
     }
     __syncthreads();  // every start read: the starts become the bucket cursors
 #pragma unroll
@@ -1678,12 +1680,13 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     if (kind == 2 && fused) {
         const FuseArgs fu{b.zero, kZEnd, b.zero + kZBar, b.zero + kZFuseErr};
         RT_KLAUNCH(k_morton_tb<true>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params, b.partials,
-                   sort_tiles(n), b.keys[1], b.zero + kZHist, b.counts, fu);
+                   sort_tiles(n), b.keys[1], probe ? b.zero + kZHist : nullptr, b.counts, fu);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (fused_out) *fused_out = true;
     } else if (kind == 2) {
         if (n) RT_KLAUNCH(k_morton_tb<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params,
-                          b.partials, bounds_grid(n), b.keys[1], b.zero + kZHist, b.counts, FuseArgs{});
+                          b.partials, bounds_grid(n), b.keys[1], probe ? b.zero + kZHist : nullptr, b.counts,
+                          FuseArgs{});
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if ((e = launch_morton_impl(b.tris, n, b.params, b.partials, bounds_grid(n), b.keys[0], b.vals[0],
                                        b.zero + kZHist, counts[0], s, kind == 1)) != hipSuccess) {

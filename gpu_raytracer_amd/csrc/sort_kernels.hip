@@ -735,13 +735,14 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
 // or any stability requirement.  K1 (k_morton_tb, build_kernels.hip) groups
 // each 4096-key tile by bucket d = key >> 20 and writes it bucket by bucket,
 // one word per key (key bits 0..19 << 12 | the key's index in its tile),
-// with tb[tile][d] = run start | run length << 16 and the bucket totals
-// ghist[d].  k_bucket_gather then owns bucket d:
-//   1. its start = the totals of the buckets below it; its runs = column d
-//      of the table, their offsets a block scan over the tiles;
-//   2. element j of the bucket (any order will do) is found by a binary
-//      search over the run offsets in LDS, so consecutive lanes read
-//      consecutive words of one run (coalesced), and decoded to (key, index);
+// with tb[tile][d] = run start | run length << 16.  k_bucket_gather then
+// owns bucket d:
+//   1. its runs = column d of the table, their offsets a block scan over
+//      the tiles; its size = the sum of the run lengths and its start = the
+//      sum of the runs' tile-local starts (no global histogram);
+//   2. each run marks its first bucket position and a max-scan gives every
+//      position its run, so element j is read by lane j (consecutive lanes
+//      read consecutive words of one run), and decoded to (key, index);
 //   3. the bucket is grouped by bin b = key bits 10..19 (LDS atomics: one
 //      histogram pass, a scan, one scatter pass -- again in any order);
 //   4. each element's rank in its bin is the number of bin elements whose
@@ -809,7 +810,6 @@ __device__ __forceinline__ void scan_lds(uint32_t* a, uint32_t* s_sw /* [NT / 64
 template <int NT, int P>
 __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict__ words_tb,
                                                       const uint32_t* __restrict__ tb, uint32_t nt,
-                                                      const uint32_t* __restrict__ ghist,
                                                       uint32_t* __restrict__ kout, uint32_t* __restrict__ vout,
                                                       uint32_t* __restrict__ flags /* [0] slow, [1] overflow */,
                                                       uint32_t* __restrict__ bstart /* [1025] bucket starts */,
@@ -834,18 +834,19 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     const uint32_t b = blockIdx.x;
     const uint32_t d = (b & 7u) * (kMsbBuckets / 8) + (b >> 3);  // XCD x: buckets [128x, 128x + 128)
     for (uint32_t j = tid; j <= NB; j += NT) s_bin[j] = 0u;
-    // 1. this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K)
+    // 1. this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K).
+    // The bucket's size m is the sum of its runs, and its start the sum of
+    // the runs' tile-local starts (a run starts after its tile's keys of the
+    // lower buckets): no global histogram is needed
     const uint32_t K = (nt + NT - 1) / NT;
-    uint32_t e[kGatherMaxTilesPerThread], csum = 0;
+    uint32_t e[kGatherMaxTilesPerThread], csum = 0, gs = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kGatherMaxTilesPerThread; ++k) {
         const uint32_t t = tid * K + k;
         e[k] = (k < K && t < nt) ? tb[(uint64_t)t * kMsbBuckets + d] : 0u;
         csum += e[k] >> 16;
+        gs += e[k] & 0xFFFFu;
     }
-    uint32_t gs = 0;  // the bucket's start: the totals of the buckets below it
-    for (uint32_t j = tid; j < d; j += NT) gs += ghist[j];
-    const uint32_t m = ghist[d];
     uint32_t x = csum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -857,10 +858,11 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     if (l == 63) s_sw[w] = x;
     if (l == 0) s_sw2[w] = gs;
     __syncthreads();
-    uint32_t off = x - csum, s = 0;
+    uint32_t off = x - csum, s = 0, m = 0;
     for (uint32_t q = 0; q < (uint32_t)NW; ++q) {
         if (q < w) off += s_sw[q];
         s += s_sw2[q];
+        m += s_sw[q];
     }
     if (tid == 0) {  // the bucket starts, for k_topo_refit's long-range nodes
         bstart[d] = s;
@@ -1140,8 +1142,8 @@ bool gather_sort_fits(uint32_t n) {  // every run of a bucket in its block's LDS
 }
 
 template <int NT, int P>
-static hipError_t gather_launch(const uint32_t* words, const uint32_t* tb, uint32_t nt, const uint32_t* ghist,
-                                uint32_t* ko, uint32_t* vo, uint32_t* flags, uint32_t* bstart, hipStream_t s, Gate g) {
+static hipError_t gather_launch(const uint32_t* words, const uint32_t* tb, uint32_t nt, uint32_t* ko, uint32_t* vo,
+                                uint32_t* flags, uint32_t* bstart, hipStream_t s, Gate g) {
     static std::once_flag once[kMaxDevices];
     static hipError_t err[kMaxDevices];
     int dev = 0;
@@ -1155,8 +1157,7 @@ static hipError_t gather_launch(const uint32_t* words, const uint32_t* tb, uint3
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     });
     if (err[dev] != hipSuccess) return err[dev];
-    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, words, tb, nt, ghist, ko, vo, flags, bstart,
-               g);
+    RT_KLAUNCH((k_bucket_gather<NT, P>), dim3(kMsbBuckets), dim3(NT), lds, s, words, tb, nt, ko, vo, flags, bstart, g);
     return hipGetLastError();
 }
 
@@ -1169,10 +1170,10 @@ hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_
     const GatherShape gs = gather_shape(n);
     if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), dense);
     const Gate g{dense, 0u};
-    if (gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
-    if (gs.nt == 512) return gather_launch<512, 8>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
-    if (gs.p == 12) return gather_launch<1024, 12>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
-    return gather_launch<1024, 16>(words, tb, nt, ghist, kout, vout, flags, bstart, s, g);
+    if (gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, kout, vout, flags, bstart, s, g);
+    if (gs.nt == 512) return gather_launch<512, 8>(words, tb, nt, kout, vout, flags, bstart, s, g);
+    if (gs.p == 12) return gather_launch<1024, 12>(words, tb, nt, kout, vout, flags, bstart, s, g);
+    return gather_launch<1024, 16>(words, tb, nt, kout, vout, flags, bstart, s, g);
 }
 
 // The probe build's LSB leg when the verdict is dense (*dense == 1): K1 again
