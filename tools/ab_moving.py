@@ -2,7 +2,7 @@
 headline workload: soup-1M 1080p, eye orbiting 0.25 deg per frame), full
 frames on one GPU; each configuration renders the whole sequence in turn,
 interleaved over rounds; reports the mean event-timed trace per frame.
-usage: python tools/ab_moving.py [rounds] [frames] name:knob=v,knob=v ..."""
+usage: python tools/ab_moving.py [rounds] [frames] name:knob=v,knob=v ...  (or name@knob=v,...)"""
 import os
 import sys
 
@@ -19,7 +19,7 @@ frames = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 rebuild = os.environ.get("AB_REBUILD", "0") == "1"  # rebuild the BVH before every timed frame, as bench.py does
 configs = [("base", {})]
 for a in sys.argv[3:]:
-    name, kv = a.split(":", 1)
+    name, kv = a.split(":", 1) if ":" in a else a.split("@", 1)
     configs.append((name, {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}))
 cfg = S.CONFIGS[3]
 view = S.VIEWS[cfg.scene]
