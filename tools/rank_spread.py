@@ -6,6 +6,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+for _a in [x for x in sys.argv[1:] if x.startswith("lib=")]:  # a librtamd variant (tools/build_exp.sh)
+    os.environ["RT_LIB"] = os.path.join(ROOT, _a[4:])
+    sys.argv.remove(_a)
+    print("lib", os.environ["RT_LIB"], flush=True)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import gpu_raytracer_amd as R  # noqa: E402
