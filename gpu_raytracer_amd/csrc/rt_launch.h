@@ -185,8 +185,6 @@ struct TraceConfig {
                                   // auto (default): coop_cap_for_tiles (tools/coop_sweep.py,
                                   // profiles/coop_sweep_r02b.log, profiles/coop_sweep_hi_r02.log)
     uint32_t coop_lanes = 32;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
-    uint32_t coop_predict = 0;    // > 0: pixels whose previous-frame wide-step count reached this go to the
-                                  // heavy-ray queue at once (with the queue on); 0 = off
     uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
     uint32_t poison = 0;          // debug.poison: fill every new device allocation with 0xFF bytes, so a

@@ -841,12 +841,6 @@ struct OrderFold {
     uint32_t nb = 0;
 };
 constexpr uint32_t kFoldPerThread = 32;  // 256 threads: up to 8192 tiles (a 1080p frame has 8160)
-// Heavy-ray prediction (trace.coop_predict): pixels whose previous-frame step
-// count (the frame's step map) reached thr go straight to the heavy-ray queue.
-struct PredQ {
-    const uint16_t* pred = nullptr;
-    uint32_t thr = 0;
-};
 #ifndef RT_ORDER_FOLD
 #define RT_ORDER_FOLD 1  // 0: k_tile_order at the head of every frame (A/B)
 #endif
@@ -872,13 +866,10 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                const uint16_t* __restrict__ px_prev = nullptr,
                                                uint16_t* __restrict__ px_cost = nullptr,
                                                uint32_t coop_cap = 0, CoopQ cq = CoopQ{},
-                                               OrderFold fold = OrderFold{}, PredQ pq = PredQ{}) {
+                                               OrderFold fold = OrderFold{}) {
     // PX: the per-pixel order (below); its ranking borrows s_ref, so the
-    // binary instance (no stack) still sizes s_ref for tile_pixel_order.
-    // PXW: the per-pixel step map is recorded (px_cost), for the order or
-    // for the heavy-ray prediction (trace.coop_predict)
+    // binary instance (no stack) still sizes s_ref for tile_pixel_order
     constexpr bool PX = !SHADOW && !COUNT && NT == 256;
-    constexpr bool PXW = !SHADOW && !COUNT;
     constexpr uint32_t kStackWords = (WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1u;
     constexpr uint32_t kRefWords = (PX && kStackWords < 144u) ? 144u : kStackWords;
     __shared__ uint32_t s_ref[kRefWords];
@@ -948,16 +939,6 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                 WRay R;
                 wray_init(cam.eye, d, R, sb);
                 int st = R.fin ? 0 : 2;
-                if (CQ && !SHADOW && pq.pred && s == 0 && st == 0 && coop_on) {
-                    // predicted heavy (the previous frame's step map): queued
-                    // for k_trace_coop at once, from the root, instead of
-                    // holding this wave for coop_cap steps first
-                    const uint32_t pv = pq.pred[(uint64_t)slot * 256 + ly * 16 + lx];
-                    if (pv >= pq.thr) {
-                        st = coop_defer(cq, gw, qslot);
-                        if (PXW && st == 3) steps = pv - (pv >> 3);  // carried, decaying, into this frame's map
-                    }
-                }
                 const char* nd = reinterpret_cast<const char*>(nodes);
                 const WideMem M = wide_mem<WA>(wnodes, tri_s, n);
                 while (st == 0) {
@@ -966,7 +947,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                         false, &M);
                     if (coop_on && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
                 }
-                if (PXW) steps += R.steps;
+                if (PX) steps += R.steps;
                 if (st == 3) {  // heavy: k_trace_coop finishes this pixel from here on
                     coop_store<NT>(cq, qslot, x, y, s, PACKED ? slot * 256 + ly * 16 + lx : y * W + x, r, g, b, R,
                                    s_ref + threadIdx.x, s_tn + threadIdx.x);
@@ -979,7 +960,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                           R.tb, R.hu, R.hv, R.hp, cn, ct);
                 }
                 tb = R.tb; hu = R.hu; hv = R.hv; hp = R.hp;
-                if (PXW && st == 2) steps += 64u;  // a binary finish: a nominal charge
+                if (PX && st == 2) steps += 64u;  // a binary finish: a nominal charge
             } else {
                 trace_ray<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d, tb, hu, hv, hp, cn, ct);
             }
@@ -1047,7 +1028,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             atomicAdd(&counters[1], bsum);
         }
     }
-    if (PXW && px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
+    if (PX && px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
     if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
         atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
@@ -2091,9 +2072,6 @@ static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity) {
 #ifndef RT_SPP1
 #define RT_SPP1 1  // 0: 1-spp full frames run the generic kernel (A/B)
 #endif
-#ifndef RT_SPP1_TILES
-#define RT_SPP1_TILES 1  // one rank's 1-spp tiles on the SPPC = 1 instance as well
-#endif
 template <bool C, bool P, bool WI, int NT, typename... A>
 static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t grid, hipStream_t s, A... a) {
     if constexpr (WI) {
@@ -2103,10 +2081,9 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t g
             return;
         }
         if (buf) {
-            // (one rank's tiles used to keep the generic kernel: its 1-spp instance, 77 VGPRs /
-            // 6 waves instead of 96 / 5, measured no faster per rank, profiles/ab_occupancy_r03.log;
-            // RT_SPP1_TILES runs them on it -- the generic instance spills with the step map)
-            if (cq && RT_SPP1 && !C && (RT_SPP1_TILES || !P) && spp1)  // 1-spp frames with the queue (trace.coop_cap)
+            // (one rank's tiles keep the generic kernel: its 1-spp instance, 77 VGPRs / 6 waves
+            // instead of 96 / 5, measured no faster per rank, profiles/ab_occupancy_r03.log)
+            if (cq && RT_SPP1 && !C && !P && NT == 256 && spp1)  // full frames with the queue (trace.coop_cap)
                 RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true, 1>), dim3(grid), dim3(NT), 0, s, a...);
             else if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true>), dim3(grid), dim3(NT), 0, s, a...);
             else if (RT_SPP1 && !C && !P && NT == 256 && spp1)  // the headline kernel: 1 spp full frames
@@ -2245,16 +2222,6 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         sched->prev_cam = c;
         sched->prev_cam_valid = true;
     }
-    // trace.coop_predict: the previous frame's step map picks the pixels
-    // queued at once (the map is recorded for every frame of the shape)
-    PredQ pq;
-    if (coop_cap && cfg.coop_predict && cost_out && sched->px_cur) {
-        px_cost = sched->px_cur;
-        if (sched->have_prev) {
-            pq.pred = sched->px_prev;
-            pq.thr = cfg.coop_predict;
-        }
-    }
     CoopQ cq;
     if (coop_cap) {
         if (sched->coop_fresh) {
@@ -2273,7 +2240,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, spp == 1, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, \
                              wnodes, cap, tris, n,                                                                       \
                              cam, w, h, spp, rank, nranks, tilesX, H, R, counters, (const float*)nullptr, Light{},      \
-                             order, cost_out, px_prev, px_cost, coop_cap, cq, fold, pq)
+                             order, cost_out, px_prev, px_cost, coop_cap, cq, fold)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \

@@ -274,7 +274,6 @@ CONFIG_KEYS = {
     "trace.coop_cap_tiles": ([-1, 0, 1, 96, 1 << 20], [-2, (1 << 20) + 1], -1),
     "trace.buf_loads": ([0, 1], [2, -1], 1),
     "trace.coop_lanes": ([16, 32, 64], [0, 8, 48, 128], 32),
-    "trace.coop_predict": ([0, 1, 80, 65535], [-1, 65536], 0),
     "trace.coop_max": ([1, 64, 65536, 1 << 24], [0, -1, (1 << 24) + 1], 65536),
     "debug.poison": ([0, 1], [2, -1], 0),
     "debug.lds_scribble": ([0, 1], [2, -1], 0),

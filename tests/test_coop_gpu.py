@@ -163,38 +163,3 @@ def test_coop_headline_1m(R, oracle, cfg):
             hits, rgba, _ = s.render(cam, w, h, 1)
             assert np.array_equal(rgba, er), frame
             assert _same_hits(hits, eh), frame
-
-
-def _cam_pair(R, oracle, V, step, w, h):
-    import math
-    a = math.radians(2.0 * step)
-    ex, ey, ez = (e - c for e, c in zip(V.eye, V.at))
-    eye = (V.at[0] + ex * math.cos(a) + ez * math.sin(a), V.at[1] + ey, V.at[2] - ex * math.sin(a) + ez * math.cos(a))
-    return (R.camera_look_at(eye, V.at, V.up, V.vfov, w, h), oracle.camera_look_at(eye, V.at, V.up, V.vfov, w, h))
-
-
-@pytest.mark.parametrize("P,spp", [(1, 1), (1, 2), (2, 1), (8, 1), (3, 2)])
-@pytest.mark.parametrize("thr", [1, 3, 6])
-def test_coop_predict(R, oracle, cfg, P, spp, thr):
-    """trace.coop_predict: pixels whose previous-frame step count reached
-    `thr` are queued before their first step and traced from the root by the
-    lane groups.  Four frames of a camera that moves every frame (the maps are
-    one frame stale) and two of a fixed one, full frames and P-rank tiles:
-    every frame == the oracle."""
-    V = _soup_view()
-    tris = oracle.soup(30000, 15).reshape(-1, 9)
-    exp = oracle.build(tris)
-    w, h = 160, 96
-    cfg("render.emulate", 1, 0)
-    cfg("trace.coop_cap", 8, -1)
-    cfg("trace.coop_cap_tiles", 8, -1)
-    cfg("trace.coop_predict", thr, 0)
-    with R.Scene.from_soup(tris) as s:
-        s.build()
-        for frame, step in enumerate([0, 1, 2, 3, 3, 3]):
-            cam, ocam = _cam_pair(R, oracle, V, step, w, h)
-            eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
-            er = oracle.shade(eh, w, h, spp)
-            hits, rgba, _ = s.render(cam, w, h, spp, ngpus=P)
-            assert np.array_equal(rgba, er), (P, spp, thr, frame)
-            assert _same_hits(hits, eh), (P, spp, thr, frame)
