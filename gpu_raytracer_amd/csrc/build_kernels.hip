@@ -333,6 +333,9 @@ struct FuseArgs {
     uint32_t* err = nullptr;   // set on a barrier timeout
 };
 static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
+#ifndef RT_K1_REVERSE
+#define RT_K1_REVERSE 1
+#endif
 #ifndef RT_K1TB_HALVES
 #define RT_K1TB_HALVES 1  // 10M: K1 157 -> 126 us (66 instead of 106 VGPRs); 1M (fused) unchanged
 #endif
@@ -351,7 +354,11 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
     __shared__ uint32_t s_sw[W];
     for (uint32_t j = threadIdx.x; j < kMsbBuckets; j += kSortThreads) s_start[j] = 0u;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint32_t tile = blockIdx.x, tbase = tile * (uint32_t)kSortTile;
+    // the unfused kernel walks the tiles from the soup's end: K0 has just
+    // streamed the soup front to back, so its last ~256 MB are what the
+    // Infinity Cache still holds (the 10M soup is 360 MB)
+    const uint32_t tile = (FUSED || !RT_K1_REVERSE) ? blockIdx.x : gridDim.x - 1 - blockIdx.x;
+    const uint32_t tbase = tile * (uint32_t)kSortTile;
     const uint32_t wbase = tbase + w * 64u * kTrisPerThread;
     // HALVES (the unfused kernel): the lane's 8 triangles in two batches of 4,
     // so it holds 36 instead of 72 triangle registers -- more resident blocks
