@@ -65,7 +65,8 @@ class rt_camera(C.Structure):
 
 
 class rt_build_times(C.Structure):
-    _fields_ = [(k, C.c_double) for k in ("bounds", "morton", "sort", "topology", "refit", "wide", "total")]
+    _fields_ = ([(k, C.c_double) for k in ("bounds", "morton", "sort", "topology", "refit", "wide", "total")] +
+                [("sort_kind", C.c_uint32), ("fused_k01", C.c_uint32)])
 
 
 def build_library(verbose: bool = False) -> str:

@@ -450,6 +450,8 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
             r->bufs.sort_mode_of = r->msb_probe;
             r->msb_probe = 0;
         }
+        r->times.sort_kind = rt::build_sort_kind(r->bufs, s->n, cfg);
+        r->times.fused_k01 = r->fused ? 1u : 0u;
         r->built = true;
         worst = std::max(worst, (double)tot);
     }

@@ -47,6 +47,8 @@ class BuildTimes:
     refit: float
     wide: float
     total: float
+    sort_kind: int = 2   # 0 LSB, 1 MSB, 2 tile-bucketed gather (the sort later builds use)
+    fused_k01: int = 0   # the last build ran K0 + K1 as one launch
 
 
 class Scene:
@@ -144,7 +146,7 @@ class Scene:
     def build_times(self) -> BuildTimes:
         t = rt_build_times()
         call("rt_bvh_build_times", self._h, C.byref(t))
-        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total)
+        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total, t.sort_kind, t.fused_k01)
 
     @property
     def wide_arity(self) -> int:

@@ -72,9 +72,14 @@ typedef enum {
 } rt_status;
 
 /* per-stage device times of the last build, milliseconds (hipEvents);
- * wide = K7w, the 4-ary trace records derived from the binary tree */
+ * wide = K7w, the 4-ary trace records derived from the binary tree.
+ * sort_kind: the sort this scene's builds use after the last one (its
+ * verdict applied): 0 the 4-pass LSB radix sort, 1 MSB scatter + bucket
+ * sort, 2 the tile-bucketed gather sort; fused_k01: the last build ran
+ * K0 + K1 as one launch (build.fuse_k01). */
 typedef struct {
     double bounds, morton, sort, topology, refit, wide, total;
+    uint32_t sort_kind, fused_k01;
 } rt_build_times;
 
 /* ---- scene ingest (SURVEY.md §8(b) rt_scene_load_obj / rt_scene_from_soup) ---- */

@@ -230,6 +230,22 @@ def test_build_sort_paths_agree_clustered(R, oracle):
     _compare_sorts(R, big)
 
 
+@pytest.mark.parametrize("n", [1_000_000, 1_900_000, 2_000_000, 2_097_152, 2_097_153, 3_000_017, 10_000_000])
+def test_uniform_soup_keeps_gather_sort(R, n):
+    """a uniform soup's sort must not depend on n -- no LSB
+    cliff where the mean bucket (n/1024) nears a fixed cap.  The gather
+    sort's bucket capacity grows with n (mean + 16 sigma + 64, gather_shape),
+    so every size up to 12M keeps it after its probe build; the 1M soup's
+    K0 + K1 run as one launch."""
+    with R.Scene.generate_soup(n, 7) as s:
+        for _ in range(2):
+            s.build()
+            t = s.build_times()
+            assert t.sort_kind == 2, (n, t)
+        if n == 1_000_000:
+            assert t.fused_k01 == 1, t
+
+
 @pytest.mark.parametrize("sort", [1, 2])
 @pytest.mark.parametrize("n", [1_000_000, 3_000_000])  # LDS bucket sort / the _big kernels (n > kMsbMaxN)
 def test_clustered_scene_switches_sort(R, oracle, n, sort):
@@ -250,6 +266,7 @@ def test_clustered_scene_switches_sort(R, oracle, n, sort):
         with R.Scene.from_soup(t) as s:
             for _ in range(3):
                 ms.append(s.build())
+                assert s.build_times().sort_kind == 0  # the verdict: LSB from the first build on
                 got = s.read_bvh()
                 assert np.array_equal(got["keys"], exp["keys"])
                 assert np.array_equal(got["vals"], exp["vals"])
