@@ -5,7 +5,8 @@
 # Each step runs under its own time limit; the first failing step ends the
 # call (no GPU step runs after a failure, a fault or a time limit).
 # Steps (arguments separated by ':'):
-#   tests:<tag>[:<pytest selector>]  GPU tests -> gpurun_out/t_<tag>.log
+#   tests:<tag>[:<pytest selector>]  GPU tests -> gpurun_out/t_<tag>.log ("@" stands for "::",
+#                                    "~" separates node ids)
 #   bench:<tag>[:<bench.py args, ',' for ' '>]  -> gpurun_out/bench_<tag>.json/.err
 #   profile:<tag>:<config>:<steps>   kernel trace + FETCH/WRITE/SQ PMC passes of the
 #                                    timed bench steps -> gpurun_out/prof_<tag>/
@@ -18,8 +19,10 @@ set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 
-run_tests() {  # tag selector
+run_tests() {  # tag selector ("@" for "::" and "~" for " ": the step itself is split at ':')
     local tag=$1 sel=${2:-tests}
+    sel=${sel//@/::}
+    sel=${sel//\~/ }
     echo "[gpu_run] tests $tag: $sel"
     timeout -k 10 900 python -u -m pytest $sel -m gpu -x -v --timeout 180 --timeout-method thread \
         > gpurun_out/t_$tag.log 2>&1 || { tail -40 gpurun_out/t_$tag.log; return 1; }
