@@ -339,45 +339,48 @@ static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
 #ifndef RT_K1TB_HALVES
 #define RT_K1TB_HALVES 1  // 10M: K1 157 -> 126 us (66 instead of 106 VGPRs); 1M (fused) unchanged
 #endif
-template <bool FUSED>
-__global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
+// NT threads per 4096-key tile (NT x kSortTile / NT triangles; the block shape
+// is RT_K1F_NT / RT_K1U_NT below)
+template <bool FUSED, int NT = kSortThreads>
+__global__ __launch_bounds__(NT) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
                                                             BuildParams* __restrict__ params,
                                                             float* __restrict__ partials, uint32_t nb,
                                                             uint32_t* __restrict__ words_tb,
                                                             uint32_t* __restrict__ ghist /* [1024] */,
                                                             uint32_t* __restrict__ tb /* [tile][1024] */,
                                                             FuseArgs fu = FuseArgs{}) {
-    constexpr int W = kSortThreads / 64;
+    constexpr int W = NT / 64;
+    constexpr uint32_t TPT = kSortTile / NT;  // triangles per thread
+    static_assert(TPT * NT == kSortTile && TPT <= 32 && (TPT % 2) == 0, "tile shape");
     __shared__ uint32_t s_word[kSortTile];  // the bucketed tile
     __shared__ __attribute__((aligned(16))) uint32_t s_start[kMsbBuckets];
     __shared__ float red[W][6];
     __shared__ uint32_t s_sw[W];
-    for (uint32_t j = threadIdx.x; j < kMsbBuckets; j += kSortThreads) s_start[j] = 0u;
+    for (uint32_t j = threadIdx.x; j < kMsbBuckets; j += NT) s_start[j] = 0u;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // the unfused kernel walks the tiles from the soup's end: K0 has just
     // streamed the soup front to back, so its last ~256 MB are what the
     // Infinity Cache still holds (the 10M soup is 360 MB)
     const uint32_t tile = (FUSED || !RT_K1_REVERSE) ? blockIdx.x : gridDim.x - 1 - blockIdx.x;
     const uint32_t tbase = tile * (uint32_t)kSortTile;
-    const uint32_t wbase = tbase + w * 64u * kTrisPerThread;
+    const uint32_t wbase = tbase + w * 64u * TPT;
     // HALVES (the unfused kernel): the lane's 8 triangles in two batches of 4,
     // so it holds 36 instead of 72 triangle registers -- more resident blocks
     // per CU to overlap one block's LDS phases with the others' loads
     constexpr bool HALVES = !FUSED && RT_K1TB_HALVES;
-    constexpr uint32_t QL = HALVES ? kTrisPerThread / 2 : kTrisPerThread;
+    constexpr uint32_t QL = HALVES ? TPT / 2 : TPT;
     float t[QL][9];
-    uint32_t okm = HALVES ? load_tri_lanes_part<QL>(tris, n, wbase, 0u, t)
-                          : load_tri_lanes(tris, n, wbase, reinterpret_cast<float(&)[kTrisPerThread][9]>(t));
+    uint32_t okm = load_tri_lanes_part<QL>(tris, n, wbase, 0u, t);
     BuildParams p;
     if constexpr (FUSED) {
         // K0: the zero words, then this tile's partial centroid box, published
-        for (uint32_t j = tile * kSortThreads + threadIdx.x; j < fu.nzero; j += gridDim.x * kSortThreads)
+        for (uint32_t j = tile * NT + threadIdx.x; j < fu.nzero; j += gridDim.x * NT)
             __hip_atomic_store(fu.zero + j, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         float lo[3], hi[3];
 #pragma unroll
         for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
 #pragma unroll
-        for (uint32_t q = 0; q < kTrisPerThread; ++q) {
+        for (uint32_t q = 0; q < TPT; ++q) {
             if ((okm >> q) & 1u) {
                 float bmin[3], bmax[3];
                 tri_bounds(t[q], bmin, bmax);
@@ -408,7 +411,7 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
         // (exact min/max: the same box in every block and as K0 + K1 give)
 #pragma unroll
         for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
-        for (uint32_t b = threadIdx.x; b < gridDim.x; b += kSortThreads) {
+        for (uint32_t b = threadIdx.x; b < gridDim.x; b += NT) {
 #pragma unroll
             for (int c = 0; c < 3; ++c) {
                 lo[c] = fminf(lo[c], __hip_atomic_load(partials + b * 6 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -436,12 +439,12 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
 #pragma unroll
         for (int c = 0; c < 7; ++c) p.pad[c] = 0u;
     } else {
-        p = bounds_final<kSortThreads>(partials, nb, red);  // ends with a barrier
+        p = bounds_final<NT>(partials, nb, red);  // ends with a barrier
     }
     if (tile == 0 && threadIdx.x == 0) *params = p;
-    uint32_t k8[kTrisPerThread];
+    uint32_t k8[TPT];
 #pragma unroll
-    for (uint32_t h = 0; h < kTrisPerThread / QL; ++h) {
+    for (uint32_t h = 0; h < TPT / QL; ++h) {
         if (h > 0) okm |= load_tri_lanes_part<QL>(tris, n, wbase, h * QL, t);
 #pragma unroll
         for (uint32_t qi = 0; qi < QL; ++qi) {
@@ -456,11 +459,11 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
         }
     }
     __syncthreads();
-    constexpr int PER = kMsbBuckets / kSortThreads;  // buckets per thread in scan1024's layout
+    constexpr int PER = kMsbBuckets / NT;  // buckets per thread in scan1024's layout
     uint32_t cnt[PER];
 #pragma unroll
     for (int j = 0; j < PER; ++j) cnt[j] = s_start[threadIdx.x * PER + j];
-    scan1024<kSortThreads>(s_start, s_sw);  // exclusive starts; ends with a barrier
+    scan1024<NT>(s_start, s_sw);  // exclusive starts; ends with a barrier
 #pragma unroll
     for (int j = 0; j < PER; ++j) {
         const uint32_t d = threadIdx.x * PER + j;
@@ -469,17 +472,17 @@ __global__ __launch_bounds__(kSortThreads) void k_morton_tb(const float* __restr
     }
     __syncthreads();  // every start read: the starts become the bucket cursors
 #pragma unroll
-    for (uint32_t q = 0; q < kTrisPerThread; ++q)
+    for (uint32_t q = 0; q < TPT; ++q)
         if ((okm >> q) & 1u) {
             const uint32_t pos = atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);
-            s_word[pos] = (k8[q] << 12) | (w * 64u * kTrisPerThread + q * 64u + lane);  // key bits 0..19, index
+            s_word[pos] = (k8[q] << 12) | (w * 64u * TPT + q * 64u + lane);  // key bits 0..19, index
         }
     __syncthreads();
     const uint32_t trem = n - tbase;
     const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
 #pragma unroll
-    for (uint32_t m = 0; m < kTrisPerThread; ++m) {
-        const uint32_t q = threadIdx.x + m * kSortThreads;
+    for (uint32_t m = 0; m < TPT; ++m) {
+        const uint32_t q = threadIdx.x + m * NT;
         if (q < tcount) words_tb[tbase + q] = s_word[q];
     }
 }
@@ -1634,6 +1637,14 @@ uint32_t build_sort_kind(const BuildBufs& b, uint32_t n, const TraceConfig& cfg)
     return cfg.sort_msb;
 }
 
+// block shapes of K1-TB (a 4096-key tile on 512 threads x 8 triangles, or
+// 1024 x 4 / 256 x 16): fused (FUSED = one block per CU at 1M) and unfused
+#ifndef RT_K1F_NT
+#define RT_K1F_NT 512
+#endif
+#ifndef RT_K1U_NT
+#define RT_K1U_NT 512
+#endif
 std::mutex& fused_gate(int device) {
     static std::mutex m[kMaxDevices];
     return m[device >= 0 && device < kMaxDevices ? device : 0];
@@ -1652,8 +1663,9 @@ bool fused_k01_fits(uint32_t n) {
     std::call_once(once[dev], [dev] {
         int per_cu = 0, cus = 0;
         cap[dev] = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(k_morton_tb<true>),
-                                                         kSortThreads, 0) != hipSuccess)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu,
+                                                         reinterpret_cast<const void*>(k_morton_tb<true, RT_K1F_NT>),
+                                                         RT_K1F_NT, 0) != hipSuccess)
             return;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return;
         cap[dev] = per_cu > 1 ? (uint32_t)(per_cu - 1) * (uint32_t)cus : 0u;
@@ -1686,12 +1698,12 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const bool probe = kind != 0 && !(b.sort_mode != 0 && b.sort_mode_of == kind);
     if (kind == 2 && fused) {
         const FuseArgs fu{b.zero, kZEnd, b.zero + kZBar, b.zero + kZFuseErr};
-        RT_KLAUNCH(k_morton_tb<true>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params, b.partials,
+        RT_KLAUNCH((k_morton_tb<true, RT_K1F_NT>), dim3(sort_tiles(n)), dim3(RT_K1F_NT), 0, s, b.tris, n, b.params, b.partials,
                    sort_tiles(n), b.keys[1], probe ? b.zero + kZHist : nullptr, b.counts, fu);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (fused_out) *fused_out = true;
     } else if (kind == 2) {
-        if (n) RT_KLAUNCH(k_morton_tb<false>, dim3(sort_tiles(n)), dim3(kSortThreads), 0, s, b.tris, n, b.params,
+        if (n) RT_KLAUNCH((k_morton_tb<false, RT_K1U_NT>), dim3(sort_tiles(n)), dim3(RT_K1U_NT), 0, s, b.tris, n, b.params,
                           b.partials, bounds_grid(n), b.keys[1], probe ? b.zero + kZHist : nullptr, b.counts,
                           FuseArgs{});
         if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -2,7 +2,9 @@
 usage: python tools/build_times.py [n] [reps] [key=v,key=v,...]
   keys are rt_config_set knobs, plus lib=<path> (a librtamd variant, e.g.
   from tools/build_exp.sh; default: the in-tree library, or $RT_LIB).
-  $RT_CFG adds knobs the same way."""
+  $RT_CFG adds knobs the same way.  BT_TRACE=1: a 1080p frame of the soup
+  (hits + RGBA written, as bench.py's step) is traced before every timed
+  build, so each build starts with the trace's data in the caches."""
 import os
 import sys
 
@@ -27,20 +29,35 @@ R.config_set("timing.event_fence", int(os.environ.get("RT_EVENT_FENCE", "0")))
 for k, v in knobs:
     R.config_set(k, v)
 s = R.Scene.generate_soup(n, 1)
+between = lambda: None  # noqa: E731
+if os.environ.get("BT_TRACE") == "1":
+    import torch
+    from gpu_raytracer_amd import scenes as S
+    v = S.VIEWS[S.CONFIGS[3].scene]
+    cam = R.camera_look_at(v.eye, v.at, v.up, v.vfov, 1920, 1080)
+    img = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
+    hits = torch.zeros(1920 * 1080 * 4, dtype=torch.float32, device="cuda")
+    s.build()
+
+    def between():
+        s.render_device(cam, 1920, 1080, 1, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
 rows, tot = [], []
 R.config_set("build.stage_events", 1)
 for i in range(reps + 3):
+    between()
     s.build()
     t = s.build_times()
     if i >= 3:
         rows.append([t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total])
 R.config_set("build.stage_events", 0)
 for i in range(reps + 3):
+    between()
     ms = s.build()
     if i >= 3:
         tot.append(ms)
 m = np.median(np.array(rows), 0) * 1e3
 lib = os.path.basename(os.environ.get("RT_LIB", "librtamd.so")) + (" fence" if os.environ.get("RT_EVENT_FENCE") == "1" else "")
 lib += " " + ",".join(f"{k}={v}" for k, v in knobs) if knobs else ""
+lib += " after-trace" if os.environ.get("BT_TRACE") == "1" else ""
 print(f"{lib:<24s} n={n} us: bounds {m[0]:6.1f} morton {m[1]:6.1f} sort {m[2]:6.1f} topo {m[3]:6.1f} "
       f"refit {m[4]:6.1f} wide {m[5]:5.1f} total(stage events) {m[6]:6.1f}  total {np.median(tot) * 1e3:6.1f}")
