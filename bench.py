@@ -622,6 +622,8 @@ def main():
                                       + ((", RCCL gather to rank 0" if args.dist_backend == "nccl" else ", gloo gather (rehearsal)") if world > 1 else "")},
             "build_mprims_per_s": round(n_tris / (build_ms * 1e-3) / 1e6, 2),
             "build_ms": round(build_ms, 4),
+            "build_ms_steps": {"median": round(float(np.median(per[:, 0])), 4), "min": round(float(per[:, 0].min()), 4),
+                               "max": round(float(per[:, 0].max()), 4)},
             "trace_ms": round(trace_ms, 4),
             "gather_ms": round(gather_ms, 4),
             "value_cold": round(rays / ((cold_ms + gather_ms) * 1e-3) / 1e6, 2),
