@@ -660,10 +660,17 @@ def main():
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM,
                                "traffic": pmc.get("build_hbm_bytes") if pmc else None,
+                               "hbm_frac_measured": (round(pmc["build_hbm_bytes"] / (build_ms * 1e-3) / 1e9
+                                                           / HBM_PEAK_GBS, 4)
+                                                     if pmc and pmc.get("build_hbm_bytes") else None),
                                "kernel_sum_ms": pmc.get("build_kernel_sum_ms") if pmc else None,
                                "note": "SURVEY.md §8(d) 404 B/prim over the event-timed build (launch gaps "
                                        "included); traffic = PMC HBM bytes of one build's kernels, kernel_sum_ms = "
-                                       "their rocprof durations (profiles/pmc_summary.json)"},
+                                       "their rocprof durations (profiles/pmc_summary.json); hbm_frac_measured = "
+                                       "traffic over the event-timed build vs 8 TB/s.  bound: HBM is the build's "
+                                       "largest measured fraction (its kernels' VALU issue is ~0.2), though "
+                                       "k_topo_refit itself is bound by its two block rounds and the random "
+                                       "triangle gather's latency (DESIGN.md)"},
             "cpu_baseline": None,
         }
         # the static frame: same CRC for every N (bit-exact tiles)

@@ -1683,7 +1683,8 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
         return (ev && (stages || i == 0 || i == 6)) ? hipEventRecord(ev->e[i], s) : hipSuccess;
     };
     const uint32_t kind = build_sort_kind(b, n, cfg);
-    const bool fused = kind == 2 && allow_fused && cfg.fuse_k01 && fused_k01_fits(n);
+    // fuse_k01 == 2 (tests): fused even when the grid cannot be co-resident
+    const bool fused = kind == 2 && allow_fused && cfg.fuse_k01 && (cfg.fuse_k01 == 2 || fused_k01_fits(n));
     if ((e = rec(0)) != hipSuccess) return e;
     if (!fused) {
         RT_KLAUNCH(k_bounds, dim3(bounds_grid(n)), dim3(256), 0, s, b.tris, n, b.partials, b.zero, kZEnd);

@@ -561,7 +561,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.px_sort" && value >= 0 && value <= 2) c.px_sort = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
-    else if (k == "build.fuse_k01" && (value == 0 || value == 1)) c.fuse_k01 = (uint32_t)value;
+    else if (k == "build.fuse_k01" && value >= 0 && value <= 2) c.fuse_k01 = (uint32_t)value;
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
     else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;

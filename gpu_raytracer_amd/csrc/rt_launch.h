@@ -171,7 +171,8 @@ struct TraceConfig {
     uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t wide_arity = 4;    // build.wide_arity: 4 = K7w 64-B records, 8 = K7w8 96-B records (greedy cut)
     uint32_t fuse_k01 = 1;      // build.fuse_k01: 1 = K0 + K1 as one launch with a grid barrier when the grid
-                                // is co-resident and no other fused build runs on the device (gather sort)
+                                // is co-resident and no other fused build runs on the device (gather sort);
+                                // 2 = even when it cannot be co-resident (tests of the barrier's timeout)
     uint32_t sort_msb = 2;      // build.sort, for 2 <= n <= kMsbBigMaxN: 2 = tile-bucketed gather sort (default),
                                 // 1 = MSB scatter + bucket sort, 0 = 4-pass LSB always
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather

@@ -871,6 +871,13 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     if (m == 0) return;  // block-uniform
     if (m > CAP) {       // block-uniform: beyond one LDS sort
         if (tid == 0) atomicOr(flags + 1, 1u);
+        // the host discards this build (and rebuilds with the LSB sort), but
+        // the stages after it still gather through this bucket's range:
+        // in-range indices there, never stale or uninitialised words
+        for (uint32_t j = tid; j < m; j += NT) {
+            kout[s + j] = 0u;
+            vout[s + j] = s + j;
+        }
         return;
     }
     // 2. run index of every bucket position: each non-empty run marks its

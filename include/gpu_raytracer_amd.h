@@ -354,8 +354,10 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * build finds a bucket beyond one block's LDS sort keeps the LSB sort.
  * "build.fuse_k01" 1 (default) / 0: with the gather sort, K0 (bounds) and K1
  * (Morton) as one launch whose blocks meet at a grid barrier, when every sort
- * tile's block fits the device at once (n up to ~2M) and no other such build
- * runs on the device; else two launches.
+ * tile's block fits the device at once (n up to ~1M) and no other such build
+ * runs on the device; else two launches.  2 (test only): fused even when the
+ * grid cannot be co-resident -- the barrier's bounded waits give up, and the
+ * build fails with RT_EDEVICE instead of hanging.
  * "debug.poison" 0/1: every device buffer the library allocates from then on
  * is filled with 0xFF bytes before first use, so reading a byte no kernel
  * wrote gives the same (wrong) value every run instead of allocator luck.

@@ -259,7 +259,7 @@ CONFIG_KEYS = {
     "trace.px_sort": ([0, 1, 2], [3], 1),
     "trace.blocks": ([0, 4096], [-1], 0),
     "build.sort": ([0, 1, 2], [3, -1], 2),
-    "build.fuse_k01": ([0, 1], [2, -1], 1),
+    "build.fuse_k01": ([0, 1, 2], [3, -1], 1),
     "build.wide_collapse": ([0, 1], [2, -1], 1),
     "build.wide_arity": ([4, 8], [2, 6, 16, -1], 4),
     "build.stage_events": ([0, 1], [2], 0),

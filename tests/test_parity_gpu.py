@@ -230,6 +230,46 @@ def test_build_sort_paths_agree_clustered(R, oracle):
     _compare_sorts(R, big)
 
 
+def test_fused_k01_not_coresident_fails_loudly(R):
+    """The fused K0 + K1's grid barrier must never hang: build.fuse_k01 = 2
+    forces the fused launch on a grid that cannot be co-resident (3M: 733
+    sort tiles against ~256 resident blocks), the first round's blocks give
+    up after their bounded wait (~100 ms), and the build fails with
+    RT_EDEVICE.  The barrier counter is left consistent: the same scene's
+    next builds (two-launch, fused off by the co-residency gate) equal a
+    fresh scene's, and so does a fused 1M build afterwards."""
+    rng = np.random.default_rng(31)
+    big = rng.random((3_000_000, 9), dtype=np.float32)
+    small = rng.random((1_000_000, 9), dtype=np.float32)
+    with R.Scene.from_soup(big) as ref:
+        ref.build()
+        exp = ref.read_bvh()
+    with R.Scene.from_soup(small) as ref:
+        ref.build()
+        exp_small = ref.read_bvh()
+        assert ref.build_times().fused_k01 == 1
+    R.config_set("build.fuse_k01", 2)
+    try:
+        with R.Scene.from_soup(big) as s:
+            with pytest.raises(R.RtError) as e:
+                s.build()
+            assert e.value.status == -4  # RT_EDEVICE
+            R.config_set("build.fuse_k01", 1)
+            for _ in range(2):
+                s.build()
+                assert s.build_times().fused_k01 == 0
+                got = s.read_bvh()
+                assert np.array_equal(got["vals"], exp["vals"])
+                assert np.array_equal(got["nodes"].view(np.uint32), exp["nodes"].view(np.uint32))
+        with R.Scene.from_soup(small) as s:
+            s.build()
+            assert s.build_times().fused_k01 == 1
+            got = s.read_bvh()
+            assert np.array_equal(got["nodes"].view(np.uint32), exp_small["nodes"].view(np.uint32))
+    finally:
+        R.config_set("build.fuse_k01", 1)
+
+
 @pytest.mark.parametrize("n", [1_000_000, 1_900_000, 2_000_000, 2_097_152, 2_097_153, 3_000_017, 10_000_000])
 def test_uniform_soup_keeps_gather_sort(R, n):
     """a uniform soup's sort must not depend on n -- no LSB
