@@ -697,7 +697,33 @@ struct CoopQ {
     uint32_t* ctr = nullptr;       // [kCoopShards] this frame's reservation counters
     uint32_t* ctr_next = nullptr;  // [kCoopShards] the next frame's, zeroed by k_trace_coop
     uint32_t cap = 0;              // entries per shard
+    // trace.coop_async (full frames): the entries are published for a
+    // k_trace_coop running beside k_trace -- the queue is fine-grained
+    // memory (no stale copy in another XCD's L2) and each entry is stamped
+    // last with `epoch`; that consumer claims entries through `take` and the
+    // queue pass after k_trace starts each shard where it stopped
+    uint32_t* take = nullptr;      // [kCoopShards] claims of this frame
+    uint32_t* take_next = nullptr; // [kCoopShards] the next frame's, zeroed with ctr_next
+    uint32_t* gate = nullptr;      // k_trace's last block writes `epoch` here when it starts
+    uint32_t* err = nullptr;       // a consumer's bounded wait gave up (never expected)
+    uint32_t epoch = 0;            // 0: synchronous queue (plain stores, no claims)
 };
+
+// coherent 16-B load (two 64-bit agent-scope relaxed atomic loads)
+__device__ __forceinline__ uint2 ld_coh2(const void* p) {
+    const uint64_t a = __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<void*>(p)), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return make_uint2((uint32_t)a, (uint32_t)(a >> 32));
+}
+__device__ __forceinline__ uint4 ld_coh(const uint4* p) {
+    const uint2 a = ld_coh2(p), b = ld_coh2(reinterpret_cast<const char*>(p) + 8);
+    return make_uint4(a.x, a.y, b.x, b.y);
+}
+template <bool COH>
+__device__ __forceinline__ uint4 ent_ld(const uint4* p) {
+    if constexpr (COH) return ld_coh(p);
+    return *p;
+}
 
 // Called by the lanes that reach the step cap in this step (divergent): one
 // atomic per wave reserves their entries.  Returns 3 (deferred) with the
@@ -709,11 +735,16 @@ template <int NT>
 __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint32_t x, uint32_t y, uint32_t s,
                                            uint32_t pi, float r, float g, float b, const WRay& R,
                                            const uint32_t* sref, const uint16_t* stn) {
+    // The queue lives in fine-grained device memory (dev_alloc_fine), so
+    // these plain stores do not stay dirty in this XCD's L2: a consumer
+    // running beside k_trace (trace.coop_async, another XCD) reads them with
+    // coherent loads.  The stamp, word 11, goes last, after a wait for the
+    // rest.  (Write-through atomic or sc1 buffer stores here instead cost the
+    // full-frame kernel 13-17 VGPRs: 72 -> 85-89, 7 -> 5 waves per SIMD.)
     uint4* e = cq.q + (uint64_t)qslot * kCoopEntry;
     const uint32_t nst = R.sp + (R.cur != RT_SENT ? 1u : 0u);
     e[0] = make_uint4(x, y, s, pi);
     e[1] = make_uint4(__float_as_uint(r), __float_as_uint(g), __float_as_uint(b), R.hp);
-    e[2] = make_uint4(__float_as_uint(R.tb), __float_as_uint(R.hu), __float_as_uint(R.hv), nst);
     for (uint32_t j = 0; j < nst; j += 2) {
         uint32_t rf[2], tn[2];
 #pragma unroll
@@ -724,6 +755,11 @@ __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint
         }
         e[3 + j / 2] = make_uint4(rf[0], tn[0], rf[1], tn[1]);
     }
+    reinterpret_cast<uint2*>(e + 2)[0] = make_uint2(__float_as_uint(R.tb), __float_as_uint(R.hu));
+    reinterpret_cast<uint32_t*>(e + 2)[2] = __float_as_uint(R.hv);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // s_waitcnt: the entry is performed
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(e + 2) + 3, nst | (cq.epoch << 8), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t& qslot) {
@@ -881,6 +917,12 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             tile_order_block<256, kFoldPerThread>(fold.cost, fold.nb, fold.out, s_ref, s_ref + 256, fold.ema);
             return;
         }
+    }
+    if constexpr (CQ && !SHADOW) {
+        // trace.coop_async: the last block has started, so every block is
+        // dispatched -- k_coop_gate lets the concurrent queue pass go
+        if (cq.gate && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
+            __hip_atomic_store(cq.gate, cq.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // tile slot from the block id: consecutive tiles go to different XCDs
     // under the round-robin dispatch, which balances the image's cheap and
@@ -1111,7 +1153,7 @@ __device__ __forceinline__ uint32_t gread_u(uint32_t x, uint32_t src) {
 // axis.  hp = prim.
 // resume (nullable): a queue entry -- start from its best hit and pending
 // entries (pass 1's state) instead of the root.
-template <bool COUNT, int G, int W = 4>
+template <bool COUNT, int G, int W = 4, bool COH = false>
 __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                            const float4* __restrict__ tri_s, uint32_t n, const float* o,
                                            const float* d, CoopLds<G, W>& L, const uint4* __restrict__ resume,
@@ -1130,12 +1172,12 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
     uint32_t hp0 = RT_SENT;  // the best hit's prim when resumed
     uint32_t sp = 1;
     if (resume) {
-        const uint4 h1 = resume[1], h2 = resume[2];
+        const uint4 h1 = ent_ld<COH>(resume + 1), h2 = ent_ld<COH>(resume + 2);
         hp0 = h1.w;
         tb = __uint_as_float(h2.x); hu = __uint_as_float(h2.y); hv = __uint_as_float(h2.z);
-        sp = h2.w;
+        sp = h2.w & 0xFFu;  // the stamp's epoch above
         for (uint32_t i = gl; i < sp; i += G) {
-            const uint4 pr = resume[3 + i / 2];
+            const uint4 pr = ent_ld<COH>(resume + 3 + i / 2);
             L.ref[i] = (i & 1) ? pr.z : pr.x;
             L.tn[i] = __uint_as_float((i & 1) ? pr.w : pr.y);
         }
@@ -1279,7 +1321,59 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // launch (8-11 us, all of it latency) leaves the next frame's critical path
 // -- and leaves the queue to the other blocks.
 constexpr uint32_t kOrderInCoop = 256 * 32;  // up to 8192 tiles: a 1080p full frame has 8160
-template <bool COUNT, bool PACKED, int G, int WA = 4>
+// One queued ray (entry `ent`) finished by group grp: its remaining samples,
+// its hit records and its pixel.  COH: the entry was published by a k_trace
+// still running (trace.coop_async) -- read it with coherent loads.
+template <bool COUNT, int G, int WA, bool COH>
+__device__ __forceinline__ void coop_entry(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
+                                           const float4* __restrict__ tri_s, uint32_t n, const Cam& cam, uint32_t W,
+                                           uint32_t spp, const uint4* ent, CoopLds<G, WA>& L,
+                                           float4* __restrict__ hits, uint32_t* __restrict__ rgba, uint32_t gl,
+                                           uint32_t& cn, uint32_t& ct) {
+    const uint4 a = ent_ld<COH>(ent), b = ent_ld<COH>(ent + 1);
+    const uint32_t x = a.x, y = a.y, pi = a.w;
+    float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
+    for (uint32_t s = a.z; s < spp; ++s) {
+        const uint32_t sidx = (y * W + x) * spp + s;
+        float jx = 0.5f, jy = 0.5f;
+        if (s > 0) {
+            const uint32_t hh = pcg_hash(sidx);
+            jx = (float)(hh >> 8) * 0x1p-24f;
+            jy = (float)(pcg_hash(hh) >> 8) * 0x1p-24f;
+        }
+        const float px = (float)x + jx, py = (float)y + jy;
+        float d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+        float tb, hu, hv;
+        uint32_t hp;
+        coop_trace<COUNT, G, WA, COH>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, L,
+                                      s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
+        if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
+        if (hp != RT_SENT) {
+            r = r + hu;
+            g = g + hv;
+            bl = bl + ((1.0f - hu) - hv);
+        } else {
+            r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
+        }
+    }
+    if (rgba && gl == 0) {
+        const float sc = 1.0f / (float)spp;
+        rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
+    }
+}
+
+// ASYNC (trace.coop_async, full frames): launched on a second stream behind
+// k_coop_gate, so its blocks take the CU slots k_trace's last blocks free
+// while they still run.  Each group claims published entries shard by shard
+// (a CAS on the shard's claim counter, only below its reservation counter)
+// and waits for a claimed entry's stamp -- its writer reserved it in the same
+// step and is storing it -- then finishes the ray; a group leaves when no
+// shard has an unclaimed reserved entry.  Entries reserved later are left to
+// the synchronous pass after k_trace, which starts every shard at its claim
+// counter.  Either way each entry is finished exactly once, by the same code.
+template <bool COUNT, bool PACKED, int G, int WA = 4, bool ASYNC = false>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
                                                     uint32_t W, uint32_t spp, CoopQ cq, float4* __restrict__ hits,
@@ -1291,75 +1385,94 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
-    if (blockIdx.x == 0 && threadIdx.x < kCoopShards) cq.ctr_next[threadIdx.x] = 0u;
-    static_assert(sizeof(CoopLds<G, WA>) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
-    const bool order_block = ord_out && gridDim.x > 1;  // uniform
-    if (order_block && blockIdx.x == 0) {
-        tile_order_block<256, kOrderInCoop / 256>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
-                                  reinterpret_cast<uint32_t*>(&s_l[0]) + 256, ord_ema);
-        return;
-    }
-    const uint32_t b0 = order_block ? 1u : 0u;  // queue work over blocks [b0, gridDim.x)
     const uint32_t lane = threadIdx.x & 63, grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
-    // the shards' filled lengths and their exclusive prefix, lane k = shard k
-    const uint32_t len = min(cq.ctr[lane], cq.cap);
-    uint32_t incl = len;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if (lane >= (uint32_t)o) incl += y;
-    }
-    // the shard table goes through LDS: inside the divergent loop below the
-    // lanes of finished groups are inactive, and a lane read (readlane or a
-    // shuffle) of a value the compiler computes there would see stale lanes
-    __shared__ uint32_t s_excl[kCoopShards], s_len[kCoopShards];
-    if (threadIdx.x < 64) {
-        s_excl[lane] = incl - len;
-        s_len[lane] = len;
-    }
-    __syncthreads();
-    const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
     uint32_t cn = 0, ct = 0;
-    for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
-        // queued ray e lives in the last non-empty shard whose prefix is <= e
-        uint32_t sh = 0, sbase = 0;
-        for (uint32_t k = 0; k < 64; ++k) {
-            const uint32_t ek = s_excl[k];
-            if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
-        }
-        const uint32_t slot = sh * cq.cap + (e - sbase);
-        const uint4* ent = cq.q + (uint64_t)slot * kCoopEntry;
-        const uint4 a = ent[0], b = ent[1];
-        const uint32_t x = a.x, y = a.y, pi = a.w;
-        float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
-        for (uint32_t s = a.z; s < spp; ++s) {
-            const uint32_t sidx = (y * W + x) * spp + s;
-            float jx = 0.5f, jy = 0.5f;
-            if (s > 0) {
-                const uint32_t hh = pcg_hash(sidx);
-                jx = (float)(hh >> 8) * 0x1p-24f;
-                jy = (float)(pcg_hash(hh) >> 8) * 0x1p-24f;
+    if constexpr (ASYNC) {
+        const uint32_t gbase = lane & ~(uint32_t)(G - 1);
+        const uint32_t gid = blockIdx.x * NG + grp;
+        const uint32_t stamp = cq.epoch & 0xFFFFFFu;
+        for (uint32_t k = 0; k < kCoopShards;) {
+            const uint32_t sh = (gid + k) & (kCoopShards - 1);
+            uint32_t t = RT_SENT;
+            if (gl == 0) {
+                uint32_t c = __hip_atomic_load(cq.take + sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                for (;;) {
+                    const uint32_t f = min(__hip_atomic_load(cq.ctr + sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                                           cq.cap);
+                    if (c >= f) break;
+                    uint32_t ex = c;
+                    if (__hip_atomic_compare_exchange_strong(cq.take + sh, &ex, c + 1, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                        t = c;
+                        break;
+                    }
+                    c = ex;
+                }
             }
-            const float px = (float)x + jx, py = (float)y + jy;
-            float d[3];
+            t = (uint32_t)__shfl((int)t, (int)gbase, 64);
+            if (t == RT_SENT) {
+                ++k;
+                continue;
+            }
+            const uint4* ent = cq.q + ((uint64_t)sh * cq.cap + t) * kCoopEntry;
+            if (gl == 0) {  // the stamp (word 11) is stored last; bounded wait (~50 ms)
+                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+                while ((ld_coh2(reinterpret_cast<const char*>(ent + 2) + 8).y >> 8) != stamp) {
+                    __builtin_amdgcn_s_sleep(1);
+                    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
+                        __hip_atomic_store(cq.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            coop_entry<COUNT, G, WA, true>(nodes, wnodes, tri_s, n, cam, W, spp, ent, s_l[grp], hits, rgba, gl, cn, ct);
+        }
+    } else {
+        if (blockIdx.x == 0 && threadIdx.x < kCoopShards) {
+            cq.ctr_next[threadIdx.x] = 0u;
+            if (cq.take_next) cq.take_next[threadIdx.x] = 0u;
+        }
+        static_assert(sizeof(CoopLds<G, WA>) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
+        const bool order_block = ord_out && gridDim.x > 1;  // uniform
+        if (order_block && blockIdx.x == 0) {
+            tile_order_block<256, kOrderInCoop / 256>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
+                                                      reinterpret_cast<uint32_t*>(&s_l[0]) + 256, ord_ema);
+            return;
+        }
+        const uint32_t b0 = order_block ? 1u : 0u;  // queue work over blocks [b0, gridDim.x)
+        // the shards' unfinished entries -- [take, filled) after an ASYNC pass,
+        // else [0, filled) -- and their exclusive prefix, lane k = shard k
+        const uint32_t fill = min(cq.ctr[lane], cq.cap);
+        const uint32_t beg = cq.take ? min(cq.take[lane], fill) : 0u;
+        const uint32_t len = fill - beg;
+        uint32_t incl = len;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
-            float tb, hu, hv;
-            uint32_t hp;
-            coop_trace<COUNT, G, WA>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp],
-                                 s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
-            if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
-            if (hp != RT_SENT) {
-                r = r + hu;
-                g = g + hv;
-                bl = bl + ((1.0f - hu) - hv);
-            } else {
-                r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
-            }
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if (lane >= (uint32_t)o) incl += y;
         }
-        if (rgba && gl == 0) {
-            const float sc = 1.0f / (float)spp;
-            rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
+        // the shard table goes through LDS: inside the divergent loop below the
+        // lanes of finished groups are inactive, and a lane read (readlane or a
+        // shuffle) of a value the compiler computes there would see stale lanes
+        __shared__ uint32_t s_excl[kCoopShards], s_len[kCoopShards], s_beg[kCoopShards];
+        if (threadIdx.x < 64) {
+            s_excl[lane] = incl - len;
+            s_len[lane] = len;
+            s_beg[lane] = beg;
+        }
+        __syncthreads();
+        const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
+        for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
+            // queued ray e lives in the last non-empty shard whose prefix is <= e
+            uint32_t sh = 0, sbase = 0;
+            for (uint32_t k = 0; k < 64; ++k) {
+                const uint32_t ek = s_excl[k];
+                if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
+            }
+            const uint32_t slot = sh * cq.cap + s_beg[sh] + (e - sbase);
+            coop_entry<COUNT, G, WA, false>(nodes, wnodes, tri_s, n, cam, W, spp, cq.q + (uint64_t)slot * kCoopEntry,
+                                            s_l[grp], hits, rgba, gl, cn, ct);
         }
     }
     if (COUNT) {
@@ -1376,6 +1489,18 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     }
 }
 
+// trace.coop_async: holds its stream until k_trace's last block has started
+// (every block of k_trace is then dispatched, so the k_trace_coop behind it
+// only takes the slots k_trace's finishing blocks free); bounded (~20 ms).
+__global__ __launch_bounds__(64) void k_coop_gate(const uint32_t* __restrict__ gate, uint32_t epoch) {
+    if (threadIdx.x == 0) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(const_cast<uint32_t*>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
+            __builtin_amdgcn_s_sleep(2);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) break;
+        }
+    }
+}
 
 // ---------------------------------------------------------------- path mode
 // Path mode [SPEC, DESIGN.md "Path mode"; SURVEY.md §8(f) row 3]: per
@@ -2035,6 +2160,13 @@ bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key
     return true;
 }
 
+// fine-grained device memory (the heavy-ray queue: written by k_trace,
+// read by a k_trace_coop running at the same time on other XCDs)
+hipError_t dev_alloc_fine(void** p, size_t bytes) {
+    *p = nullptr;
+    return hipExtMallocWithFlags(p, bytes ? bytes : 16, hipDeviceMallocFinegrained);
+}
+
 hipError_t dev_alloc(void** p, size_t bytes) {
     *p = nullptr;
     hipError_t e = hipMalloc(p, bytes ? bytes : 16);
@@ -2093,6 +2225,22 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t g
         }
     }
     RT_KLAUNCH((k_trace<C, P, WI, NT, false, false, 4>), dim3(grid), dim3(NT), 0, s, a...);
+}
+
+// the concurrent queue pass's grid (trace.coop_async): one block per CU
+#ifndef RT_COOP_ASYNC_GRID
+#define RT_COOP_ASYNC_GRID 256
+#endif
+
+void sched_release(TileSched& t) {
+    if (t.s2) {
+        (void)hipStreamSynchronize(t.s2);
+        (void)hipStreamDestroy(t.s2);
+    }
+    if (t.ev_go) (void)hipEventDestroy(t.ev_go);
+    if (t.ev_done) (void)hipEventDestroy(t.ev_done);
+    t.s2 = nullptr;
+    t.ev_go = t.ev_done = nullptr;
 }
 
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tris, uint32_t n,
@@ -2223,16 +2371,35 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         sched->prev_cam_valid = true;
     }
     CoopQ cq;
+    // trace.coop_async: full frames (one rank, no counters) also drain the
+    // queue beside k_trace's last blocks, on the scene's second stream
+    const bool async = coop_cap && cfg.coop_async && nranks == 1 && !packed && !counters && !small;
     if (coop_cap) {
         if (sched->coop_fresh) {
-            hipError_t me = hipMemsetAsync(sched->coop_ctr, 0, 2 * kCoopShards * sizeof(uint32_t), s);
+            hipError_t me = hipMemsetAsync(sched->coop_ctr, 0, kCoopCtlWords * sizeof(uint32_t), s);
             if (me != hipSuccess) return me;
             sched->coop_fresh = false;
         }
         cq.q = sched->coop_q;
         cq.ctr = sched->coop_ctr + sched->coop_par * kCoopShards;
         cq.ctr_next = sched->coop_ctr + (sched->coop_par ^ 1u) * kCoopShards;
+        cq.take = sched->coop_ctr + (2 + sched->coop_par) * kCoopShards;
+        cq.take_next = sched->coop_ctr + (2 + (sched->coop_par ^ 1u)) * kCoopShards;
         cq.cap = sched->coop_qcap / kCoopShards;
+        if (async) {
+            if (!sched->s2) {
+                hipError_t e = hipStreamCreateWithFlags(&sched->s2, hipStreamNonBlocking);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&sched->ev_go, hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&sched->ev_done, hipEventDisableTiming);
+                if (e != hipSuccess) return e;
+            }
+            sched->epoch = sched->epoch % 0xFFFFFFu + 1u;  // 24 bits, never 0
+            cq.epoch = sched->epoch;
+            cq.gate = sched->coop_ctr + 4 * kCoopShards;
+            cq.err = sched->coop_ctr + 4 * kCoopShards + 1;
+            hipError_t e = hipEventRecord(sched->ev_go, s);
+            if (e != hipSuccess) return e;
+        }
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
@@ -2290,6 +2457,33 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
                 resident[dev][gi][ai].store(r, std::memory_order_relaxed);
             }
             cgrid = r;
+        }
+        if (async) {
+            // the concurrent pass: behind the gate on the second stream, one
+            // block per CU at most (it only fills slots k_trace frees); the
+            // synchronous pass below then waits for it and takes the rest
+            hipError_t e = hipStreamWaitEvent(sched->s2, sched->ev_go, 0);
+            if (e != hipSuccess) return e;
+            RT_KLAUNCH(k_coop_gate, dim3(1), dim3(64), 0, sched->s2, cq.gate, cq.epoch);
+            const uint32_t agrid = std::min<uint32_t>(cgrid, RT_COOP_ASYNC_GRID);
+#define RT_COOP_A(G)                                                                                               \
+    if (warity == 8)                                                                                               \
+        RT_KLAUNCH((k_trace_coop<false, false, G, 8, true>), dim3(agrid), dim3(256), 0, sched->s2, nodes, wnodes,   \
+                   tris, n, cam, w, spp, cq, H, R, counters);                                                       \
+    else                                                                                                           \
+        RT_KLAUNCH((k_trace_coop<false, false, G, 4, true>), dim3(agrid), dim3(256), 0, sched->s2, nodes, wnodes,   \
+                   tris, n, cam, w, spp, cq, H, R, counters)
+            if (cfg.coop_lanes == 16) {
+                RT_COOP_A(16);
+            } else if (cfg.coop_lanes == 32) {
+                RT_COOP_A(32);
+            } else {
+                RT_COOP_A(64);
+            }
+#undef RT_COOP_A
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if ((e = hipEventRecord(sched->ev_done, sched->s2)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(s, sched->ev_done, 0)) != hipSuccess) return e;
         }
         // block 0 sorts this frame's cost map into the next frame's tile order
         const bool ord = cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
