@@ -45,7 +45,7 @@ struct SchedState {
     void* d = nullptr;  // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per
                         // tile slot
     size_t cap = 0;
-    void* dq = nullptr;  // the heavy-ray queue: control words, then the entries (fine-grained memory)
+    void* dq = nullptr;  // the heavy-ray queue: control words, then the entries (uncached memory)
     size_t qbytes = 0;
     rt::TileSched sched;
     uint32_t key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the maps
@@ -498,9 +498,9 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
             if (r.dq) (void)hipFree(r.dq);
             r.dq = nullptr;
             r.qbytes = 0;
-            hipError_t e = rt::dev_alloc_fine(&r.dq, qneed);
+            hipError_t e = rt::dev_alloc_uncached(&r.dq, qneed);
             if (e == hipErrorOutOfMemory) return fail(RT_ENOMEM, "device allocation failed");
-            if (e != hipSuccess) return hip_fail(e, "hipExtMallocWithFlags (fine-grained)");
+            if (e != hipSuccess) return hip_fail(e, "hipExtMallocWithFlags (uncached)");
             r.qbytes = qneed;
         }
         uint32_t* b = static_cast<uint32_t*>(r.d);

@@ -698,8 +698,8 @@ struct CoopQ {
     uint32_t* ctr_next = nullptr;  // [kCoopShards] the next frame's, zeroed by k_trace_coop
     uint32_t cap = 0;              // entries per shard
     // trace.coop_async (full frames): the entries are published for a
-    // k_trace_coop running beside k_trace -- the queue is fine-grained
-    // memory (no stale copy in another XCD's L2) and each entry is stamped
+    // k_trace_coop running beside k_trace -- the queue is uncached memory
+    // (no copy in any XCD's L2) and each entry is stamped
     // last with `epoch`; that consumer claims entries through `take` and the
     // queue pass after k_trace starts each shard where it stopped
     uint32_t* take = nullptr;      // [kCoopShards] claims of this frame
@@ -735,11 +735,13 @@ template <int NT>
 __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint32_t x, uint32_t y, uint32_t s,
                                            uint32_t pi, float r, float g, float b, const WRay& R,
                                            const uint32_t* sref, const uint16_t* stn) {
-    // The queue lives in fine-grained device memory (dev_alloc_fine), so
-    // these plain stores do not stay dirty in this XCD's L2: a consumer
-    // running beside k_trace (trace.coop_async, another XCD) reads them with
-    // coherent loads.  The stamp, word 11, goes last, after a wait for the
-    // rest.  (Write-through atomic or sc1 buffer stores here instead cost the
+    // The queue lives in uncached device memory (dev_alloc_uncached), so
+    // these plain stores go past this XCD's L2 to memory: a consumer running
+    // beside k_trace (trace.coop_async, another XCD) reads them there.  The
+    // stamp, word 11, goes last, after an explicit wait for the other
+    // stores' acknowledgements (r04: the workgroup-scope release fence did
+    // not order them -- a consumer saw a stamp over a zero body).
+    // (Write-through atomic or sc1 buffer stores here instead cost the
     // full-frame kernel 13-17 VGPRs: 72 -> 85-89, 7 -> 5 waves per SIMD.)
     uint4* e = cq.q + (uint64_t)qslot * kCoopEntry;
     const uint32_t nst = R.sp + (R.cur != RT_SENT ? 1u : 0u);
@@ -757,7 +759,7 @@ __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint
     }
     reinterpret_cast<uint2*>(e + 2)[0] = make_uint2(__float_as_uint(R.tb), __float_as_uint(R.hu));
     reinterpret_cast<uint32_t*>(e + 2)[2] = __float_as_uint(R.hv);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // s_waitcnt: the entry is performed
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding; stores count in vmcnt)
     __hip_atomic_store(reinterpret_cast<uint32_t*>(e + 2) + 3, nst | (cq.epoch << 8), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1381,7 +1383,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                                                     unsigned long long* __restrict__ counters,
                                                     uint32_t* __restrict__ ord_cost = nullptr, uint32_t ord_nb = 0,
                                                     uint32_t* __restrict__ ord_out = nullptr,
-                                                    uint32_t* __restrict__ ord_ema = nullptr) {
+                                                    uint32_t* __restrict__ ord_ema = nullptr, uint32_t npix = 0) {
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
@@ -1426,6 +1428,13 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                 }
             }
             __builtin_amdgcn_wave_barrier();
+            // defence in depth: an entry read before its stores landed must
+            // never index the outputs out of range (the test suite would
+            // then see the wrong pixel; err records it)
+            if (ent_ld<true>(ent).w >= npix) {
+                if (gl == 0) __hip_atomic_store(cq.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                continue;
+            }
             coop_entry<COUNT, G, WA, true>(nodes, wnodes, tri_s, n, cam, W, spp, ent, s_l[grp], hits, rgba, gl, cn, ct);
         }
     } else {
@@ -2160,11 +2169,11 @@ bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key
     return true;
 }
 
-// fine-grained device memory (the heavy-ray queue: written by k_trace,
-// read by a k_trace_coop running at the same time on other XCDs)
-hipError_t dev_alloc_fine(void** p, size_t bytes) {
+// uncached device memory (the heavy-ray queue: written by k_trace, read by
+// a k_trace_coop running at the same time on other XCDs)
+hipError_t dev_alloc_uncached(void** p, size_t bytes) {
     *p = nullptr;
-    return hipExtMallocWithFlags(p, bytes ? bytes : 16, hipDeviceMallocFinegrained);
+    return hipExtMallocWithFlags(p, bytes ? bytes : 16, hipDeviceMallocUncached);
 }
 
 hipError_t dev_alloc(void** p, size_t bytes) {
@@ -2469,10 +2478,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
 #define RT_COOP_A(G)                                                                                               \
     if (warity == 8)                                                                                               \
         RT_KLAUNCH((k_trace_coop<false, false, G, 8, true>), dim3(agrid), dim3(256), 0, sched->s2, nodes, wnodes,   \
-                   tris, n, cam, w, spp, cq, H, R, counters);                                                       \
+                   tris, n, cam, w, spp, cq, H, R, counters, nullptr, 0u, nullptr, nullptr, w * h);                 \
     else                                                                                                           \
         RT_KLAUNCH((k_trace_coop<false, false, G, 4, true>), dim3(agrid), dim3(256), 0, sched->s2, nodes, wnodes,   \
-                   tris, n, cam, w, spp, cq, H, R, counters)
+                   tris, n, cam, w, spp, cq, H, R, counters, nullptr, 0u, nullptr, nullptr, w * h)
             if (cfg.coop_lanes == 16) {
                 RT_COOP_A(16);
             } else if (cfg.coop_lanes == 32) {
