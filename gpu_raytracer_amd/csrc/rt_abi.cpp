@@ -45,7 +45,7 @@ struct SchedState {
     void* d = nullptr;  // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per
                         // tile slot
     size_t cap = 0;
-    void* dq = nullptr;  // the heavy-ray queue: control words, then the entries (uncached memory)
+    void* dq = nullptr;  // the heavy-ray queue's entries (uncached memory; its control words follow the maps)
     size_t qbytes = 0;
     rt::TileSched sched;
     uint32_t key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the maps
@@ -489,8 +489,13 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
     const rt::TraceConfig cfg = rt::config_snapshot();
     // (64 shards of equal size, 2 x 64 counters)
     const uint32_t qcap = (cfg.coop_cap || cfg.coop_cap_tiles) ? (cfg.coop_max + 63u) & ~63u : 0u;
-    const size_t need = 5ull * nb * 4 + 2ull * nb * 512;
-    const size_t qneed = qcap ? rt::kCoopCtlBytes + (size_t)rt::kCoopEntryBytes * qcap : 0;
+    // the queue's control words (device-scope atomics) after the maps; its
+    // entries in uncached memory (written by k_trace, read by a k_trace_coop
+    // running at the same time on other XCDs, trace.coop_async)
+    const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
+    const size_t coff = (maps + 255) & ~size_t(255);
+    const size_t need = qcap ? coff + rt::kCoopCtlBytes : maps;
+    const size_t qneed = qcap ? (size_t)rt::kCoopEntryBytes * qcap : 0;
     if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
         std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
         RTR(grow(&r.d, &r.cap, need));
@@ -511,9 +516,8 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
         r.sched.cost_ema = b + 4 * nb;
         r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 5 * nb);
         r.sched.px_cur = r.sched.px_prev + (size_t)nb * 256;
-        char* qb = static_cast<char*>(r.dq);
-        r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(qb) : nullptr;
-        r.sched.coop_q = qcap ? reinterpret_cast<uint4*>(qb + rt::kCoopCtlBytes) : nullptr;
+        r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(static_cast<char*>(r.d) + coff) : nullptr;
+        r.sched.coop_q = qcap ? static_cast<uint4*>(r.dq) : nullptr;
         r.sched.coop_qcap = qcap;
         r.sched.coop_par = 0;
         r.sched.coop_fresh = true;
