@@ -45,7 +45,7 @@ struct SchedState {
     void* d = nullptr;  // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per
                         // tile slot
     size_t cap = 0;
-    void* dq = nullptr;  // the heavy-ray queue's entries (uncached memory; its control words follow the maps)
+    void* dq = nullptr;  // the heavy-ray queue's entries (its control words follow the maps)
     size_t qbytes = 0;
     rt::TileSched sched;
     uint32_t key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the maps
@@ -489,9 +489,7 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
     const rt::TraceConfig cfg = rt::config_snapshot();
     // (64 shards of equal size, 2 x 64 counters)
     const uint32_t qcap = (cfg.coop_cap || cfg.coop_cap_tiles) ? (cfg.coop_max + 63u) & ~63u : 0u;
-    // the queue's control words (device-scope atomics) after the maps; its
-    // entries in uncached memory (written by k_trace, read by a k_trace_coop
-    // running at the same time on other XCDs, trace.coop_async)
+    // the queue's control words after the maps; its entries apart
     const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
     const size_t coff = (maps + 255) & ~size_t(255);
     const size_t need = qcap ? coff + rt::kCoopCtlBytes : maps;
@@ -503,9 +501,9 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
             if (r.dq) (void)hipFree(r.dq);
             r.dq = nullptr;
             r.qbytes = 0;
-            hipError_t e = rt::dev_alloc_uncached(&r.dq, qneed);
+            hipError_t e = rt::dev_alloc(&r.dq, qneed);
             if (e == hipErrorOutOfMemory) return fail(RT_ENOMEM, "device allocation failed");
-            if (e != hipSuccess) return hip_fail(e, "hipExtMallocWithFlags (uncached)");
+            if (e != hipSuccess) return hip_fail(e, "hipMalloc");
             r.qbytes = qneed;
         }
         uint32_t* b = static_cast<uint32_t*>(r.d);

@@ -211,7 +211,6 @@ void lds_scribble_if(hipStream_t s);
 // Every device buffer of the library is allocated here: hipMalloc, then
 // with debug.poison a 0xFF fill completed before the buffer is handed out.
 hipError_t dev_alloc(void** p, size_t bytes);
-hipError_t dev_alloc_uncached(void** p, size_t bytes);  // uncached (the heavy-ray queue)
 template <class T>
 inline hipError_t dev_alloc(T** p, size_t bytes) { return dev_alloc(reinterpret_cast<void**>(p), bytes); }
 

@@ -698,8 +698,8 @@ struct CoopQ {
     uint32_t* ctr_next = nullptr;  // [kCoopShards] the next frame's, zeroed by k_trace_coop
     uint32_t cap = 0;              // entries per shard
     // trace.coop_async (full frames): the entries are published for a
-    // k_trace_coop running beside k_trace -- the queue is uncached memory
-    // (no copy in any XCD's L2) and each entry is stamped
+    // k_trace_coop running beside k_trace -- each entry is re-stored with
+    // write-through stores at the end of its wave and then stamped
     // last with `epoch`; that consumer claims entries through `take` and the
     // queue pass after k_trace starts each shard where it stopped
     uint32_t* take = nullptr;      // [kCoopShards] claims of this frame
@@ -735,18 +735,11 @@ template <int NT>
 __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint32_t x, uint32_t y, uint32_t s,
                                            uint32_t pi, float r, float g, float b, const WRay& R,
                                            const uint32_t* sref, const uint16_t* stn) {
-    // The queue lives in uncached device memory (dev_alloc_uncached), so
-    // these plain stores go past this XCD's L2 to memory: a consumer running
-    // beside k_trace (trace.coop_async, another XCD) reads them there.  The
-    // stamp, word 11, goes last, after an explicit wait for the other
-    // stores' acknowledgements (r04: the workgroup-scope release fence did
-    // not order them -- a consumer saw a stamp over a zero body).
-    // (Write-through atomic or sc1 buffer stores here instead cost the
-    // full-frame kernel 13-17 VGPRs: 72 -> 85-89, 7 -> 5 waves per SIMD.)
     uint4* e = cq.q + (uint64_t)qslot * kCoopEntry;
     const uint32_t nst = R.sp + (R.cur != RT_SENT ? 1u : 0u);
     e[0] = make_uint4(x, y, s, pi);
     e[1] = make_uint4(__float_as_uint(r), __float_as_uint(g), __float_as_uint(b), R.hp);
+    e[2] = make_uint4(__float_as_uint(R.tb), __float_as_uint(R.hu), __float_as_uint(R.hv), nst);  // unstamped
     for (uint32_t j = 0; j < nst; j += 2) {
         uint32_t rf[2], tn[2];
 #pragma unroll
@@ -757,10 +750,30 @@ __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint
         }
         e[3 + j / 2] = make_uint4(rf[0], tn[0], rf[1], tn[1]);
     }
-    reinterpret_cast<uint2*>(e + 2)[0] = make_uint2(__float_as_uint(R.tb), __float_as_uint(R.hu));
-    reinterpret_cast<uint32_t*>(e + 2)[2] = __float_as_uint(R.hv);
+}
+
+// trace.coop_async: publish a deferred lane's entry at the end of its wave,
+// where few registers are live.  coop_store's plain stores may still sit
+// dirty in this XCD's L2, invisible to a consumer on another XCD; the entry
+// is read back (this wave's own stores: fresh) and stored again with
+// agent-scope atomic stores, which write through, then -- after a wait for
+// them -- stamped with the epoch.  (The same atomic stores at the deferral
+// itself cost the full-frame kernel 13 VGPRs, 7 -> 5 waves per SIMD.)
+__device__ __forceinline__ void coop_publish(const CoopQ& cq, uint32_t qslot) {
+    uint4* e = cq.q + (uint64_t)qslot * kCoopEntry;
+    const uint4 h2 = e[2];
+    const uint32_t nw = 3 + ((h2.w & 0xFFu) + 1) / 2;  // uint4 in use
+    for (uint32_t k = 0; k < nw; ++k) {
+        const uint4 v = e[k];
+        uint64_t* q = reinterpret_cast<uint64_t*>(e + k);
+        __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k != 2)
+            __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding; stores count in vmcnt)
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(e + 2) + 3, nst | (cq.epoch << 8), __ATOMIC_RELAXED,
+    uint64_t* q2 = reinterpret_cast<uint64_t*>(e + 2) + 1;
+    __hip_atomic_store(q2, (uint64_t)h2.z | ((uint64_t)((h2.w & 0xFFu) | (cq.epoch << 8)) << 32), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -1071,6 +1084,9 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             atomicAdd(&counters[0], a);
             atomicAdd(&counters[1], bsum);
         }
+    }
+    if constexpr (CQ && !SHADOW) {
+        if (cq.epoch && dsamp != RT_SENT) coop_publish(cq, qslot);
     }
     if (PX && px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
     if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
@@ -2167,13 +2183,6 @@ bool config_apply(bool (*f)(TraceConfig&, const char*, int64_t), const char* key
     g_trace_config = c;
     g_lds_scribble.store(c.lds_scribble, std::memory_order_relaxed);
     return true;
-}
-
-// uncached device memory (the heavy-ray queue: written by k_trace, read by
-// a k_trace_coop running at the same time on other XCDs)
-hipError_t dev_alloc_uncached(void** p, size_t bytes) {
-    *p = nullptr;
-    return hipExtMallocWithFlags(p, bytes ? bytes : 16, hipDeviceMallocUncached);
 }
 
 hipError_t dev_alloc(void** p, size_t bytes) {
