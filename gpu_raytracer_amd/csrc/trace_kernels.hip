@@ -1385,12 +1385,12 @@ __device__ __forceinline__ void coop_entry(const void* __restrict__ nodes, const
 // ASYNC (trace.coop_async, full frames): launched on a second stream behind
 // k_coop_gate, so its blocks take the CU slots k_trace's last blocks free
 // while they still run.  Each group claims published entries shard by shard
-// (a CAS on the shard's claim counter, only below its reservation counter)
-// and waits for a claimed entry's stamp -- its writer reserved it in the same
-// step and is storing it -- then finishes the ray; a group leaves when no
-// shard has an unclaimed reserved entry.  Entries reserved later are left to
-// the synchronous pass after k_trace, which starts every shard at its claim
-// counter.  Either way each entry is finished exactly once, by the same code.
+// (a CAS on the shard's claim counter, only for the next entry and only when
+// it carries this frame's stamp -- coop_publish writes it at the end of the
+// deferring wave) and finishes the ray; a group leaves when no shard's next
+// entry is published.  The rest is left to the synchronous pass after
+// k_trace, which starts every shard at its claim counter.  Either way each
+// entry is finished exactly once, by the same code.
 template <bool COUNT, bool PACKED, int G, int WA = 4, bool ASYNC = false>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
@@ -1413,11 +1413,16 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
             const uint32_t sh = (gid + k) & (kCoopShards - 1);
             uint32_t t = RT_SENT;
             if (gl == 0) {
+                // claim the shard's next entry if it is published; never wait
+                // for one (a waiting group would poll memory beside k_trace):
+                // what is not published yet is left to the pass after k_trace
                 uint32_t c = __hip_atomic_load(cq.take + sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 for (;;) {
                     const uint32_t f = min(__hip_atomic_load(cq.ctr + sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                                            cq.cap);
                     if (c >= f) break;
+                    const uint4* ec = cq.q + ((uint64_t)sh * cq.cap + c) * kCoopEntry;
+                    if ((ld_coh2(reinterpret_cast<const char*>(ec + 2) + 8).y >> 8) != stamp) break;
                     uint32_t ex = c;
                     if (__hip_atomic_compare_exchange_strong(cq.take + sh, &ex, c + 1, __ATOMIC_RELAXED,
                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
@@ -1433,16 +1438,6 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                 continue;
             }
             const uint4* ent = cq.q + ((uint64_t)sh * cq.cap + t) * kCoopEntry;
-            if (gl == 0) {  // the stamp (word 11) is stored last; bounded wait (~50 ms)
-                const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-                while ((ld_coh2(reinterpret_cast<const char*>(ent + 2) + 8).y >> 8) != stamp) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if (__builtin_amdgcn_s_memrealtime() - t0 > 5000000ull) {
-                        __hip_atomic_store(cq.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        break;
-                    }
-                }
-            }
             __builtin_amdgcn_wave_barrier();
             // defence in depth: an entry read before its stores landed must
             // never index the outputs out of range (the test suite would
