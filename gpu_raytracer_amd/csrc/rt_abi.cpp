@@ -43,10 +43,8 @@ constexpr uint32_t kRefitLeaves = (uint32_t)rt::kRefitT;  // leaves per refit bl
 // shape they belong to.
 struct SchedState {
     void* d = nullptr;  // [order][order next][cost A][cost B][cost mean] u32, [px A][px B] u16 x 256 per
-                        // tile slot
+                        // tile slot, then the heavy-ray queue
     size_t cap = 0;
-    void* dq = nullptr;  // the heavy-ray queue's entries (its control words follow the maps)
-    size_t qbytes = 0;
     rt::TileSched sched;
     uint32_t key[5] = {0, 0, 0, 0, 0};  // w, h, spp, rank, nranks of the maps
 };
@@ -281,11 +279,9 @@ void replica_free(Replica& r) {
     (void)hipSetDevice(r.device);
     if (r.last_stream) (void)hipEventSynchronize(r.last);  // device work on a caller stream
     (void)hipStreamSynchronize(r.stream);
-    rt::sched_release(r.ord.sched);
-    rt::sched_release(r.ord_diag.sched);
     rt::free_build(r.bufs);
     rt::free_path(r.path);
-    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.ord.d, r.ord_diag.d, r.ord.dq, r.ord_diag.dq, r.d_slab, r.d_slab_hits, r.d_recv,
+    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.ord.d, r.ord_diag.d, r.d_slab, r.d_slab_hits, r.d_recv,
                     r.d_recv_hits, (void*)r.dk[0], (void*)r.dk[1], (void*)r.dv[0], (void*)r.dv[1], (void*)r.dcross,
                     (void*)r.dcross_all, (void*)r.dboxes})
         if (p) (void)hipFree(p);
@@ -489,23 +485,12 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
     const rt::TraceConfig cfg = rt::config_snapshot();
     // (64 shards of equal size, 2 x 64 counters)
     const uint32_t qcap = (cfg.coop_cap || cfg.coop_cap_tiles) ? (cfg.coop_max + 63u) & ~63u : 0u;
-    // the queue's control words after the maps; its entries apart
     const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
-    const size_t coff = (maps + 255) & ~size_t(255);
-    const size_t need = qcap ? coff + rt::kCoopCtlBytes : maps;
-    const size_t qneed = qcap ? (size_t)rt::kCoopEntryBytes * qcap : 0;
+    const size_t qoff = (maps + 255) & ~size_t(255);
+    const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
     if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
         std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
         RTR(grow(&r.d, &r.cap, need));
-        if (qneed > r.qbytes) {
-            if (r.dq) (void)hipFree(r.dq);
-            r.dq = nullptr;
-            r.qbytes = 0;
-            hipError_t e = rt::dev_alloc(&r.dq, qneed);
-            if (e == hipErrorOutOfMemory) return fail(RT_ENOMEM, "device allocation failed");
-            if (e != hipSuccess) return hip_fail(e, "hipMalloc");
-            r.qbytes = qneed;
-        }
         uint32_t* b = static_cast<uint32_t*>(r.d);
         r.sched.order = b;
         r.sched.order_next = b + nb;
@@ -514,8 +499,9 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
         r.sched.cost_ema = b + 4 * nb;
         r.sched.px_prev = reinterpret_cast<uint16_t*>(b + 5 * nb);
         r.sched.px_cur = r.sched.px_prev + (size_t)nb * 256;
-        r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(static_cast<char*>(r.d) + coff) : nullptr;
-        r.sched.coop_q = qcap ? static_cast<uint4*>(r.dq) : nullptr;
+        char* qb = static_cast<char*>(r.d) + qoff;
+        r.sched.coop_ctr = qcap ? reinterpret_cast<uint32_t*>(qb) : nullptr;
+        r.sched.coop_q = qcap ? reinterpret_cast<uint4*>(qb + 512) : nullptr;
         r.sched.coop_qcap = qcap;
         r.sched.coop_par = 0;
         r.sched.coop_fresh = true;
@@ -576,7 +562,6 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
     else if (k == "build.fuse_k01" && value >= 0 && value <= 2) c.fuse_k01 = (uint32_t)value;
-    else if (k == "trace.coop_async" && (value == 0 || value == 1)) c.coop_async = (uint32_t)value;
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
     else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;

@@ -187,8 +187,6 @@ struct TraceConfig {
                                   // profiles/coop_sweep_r02b.log, profiles/coop_sweep_hi_r02.log)
     uint32_t coop_lanes = 32;     // lanes per queued ray in k_trace_coop: 16, 32 or 64
     uint32_t coop_max = 65536;    // heavy-ray queue entries per frame shape (rays beyond it trace on alone)
-    uint32_t coop_async = 0;      // full frames: a second k_trace_coop, on a second stream, drains the queue
-                                  // while k_trace's last blocks still run (DESIGN.md "Cooperative heavy rays")
     const uint32_t* order_override = nullptr;  // diagnostic builds: a caller-given dispatch order
     uint32_t poison = 0;          // debug.poison: fill every new device allocation with 0xFF bytes, so a
                                   // read of a byte nothing wrote is deterministic (and visible)
@@ -215,12 +213,6 @@ template <class T>
 inline hipError_t dev_alloc(T** p, size_t bytes) { return dev_alloc(reinterpret_cast<void**>(p), bytes); }
 
 constexpr uint32_t kCoopEntryBytes = 208;  // heavy-ray queue entry (trace_kernels.hip kCoopEntry x 16 B)
-// the queue's control words ahead of its entries: [2][64] reservation
-// counters, [2][64] claim counters (trace.coop_async), the gate word and an
-// error word
-constexpr uint32_t kCoopCtlWords = 2 * 64 + 2 * 64 + 2;
-constexpr size_t kCoopCtlBytes = 2048;
-static_assert(kCoopCtlWords * 4 <= kCoopCtlBytes, "queue control words");
 // 8-ary records are read through 32-bit buffer offsets: the last record ends
 // at (n-1) x 96 B, which must not pass 2^32 - 1 (n <= 44,739,243; above that
 // the build writes 4-ary records, whose (n-1) x 64 B fit up to n = 2^26)
@@ -238,8 +230,7 @@ struct TileSched {
     uint16_t* px_prev = nullptr;    // [nb][256] previous frame's per-pixel steps (trace.px_sort)
     uint16_t* px_cur = nullptr;     // [nb][256] this frame's
     uint4* coop_q = nullptr;        // [coop_qcap] x kCoopEntryBytes heavy-ray queue (trace.coop_cap)
-    uint32_t* coop_ctr = nullptr;   // [kCoopCtlWords]: [2][64] queue counters, alternating frames, [2][64]
-                                    // claim counters, gate, error (kCoopCtlWords)
+    uint32_t* coop_ctr = nullptr;   // [2] queue counters, alternating frames
     uint32_t coop_qcap = 0;
     uint32_t coop_par = 0;          // which counter this frame uses
     CamF prev_cam{};                // camera of the previous frame of this shape (pixel order only if equal)
@@ -248,13 +239,7 @@ struct TileSched {
     bool have_prev = false;
     bool order_ready = false;       // `order` for this frame already sorted by the previous frame's k_trace_coop
     bool fresh = true;              // maps (re)allocated: clear both before the first launch
-    // trace.coop_async: the second stream and its two events (created on first use, sched_release)
-    hipStream_t s2 = nullptr;
-    hipEvent_t ev_go = nullptr, ev_done = nullptr;
-    uint32_t epoch = 0;             // frame counter stamped into the queue entries (never 0)
 };
-// destroys what launch_trace created for `s` (its second stream, events)
-void sched_release(TileSched& s);
 // The process-wide knobs (rt_config_set).  Every launcher works on one
 // consistent copy taken under the config lock, so a concurrent rt_config_set
 // on another thread never tears a launch's settings.

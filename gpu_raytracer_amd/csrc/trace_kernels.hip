@@ -697,33 +697,7 @@ struct CoopQ {
     uint32_t* ctr = nullptr;       // [kCoopShards] this frame's reservation counters
     uint32_t* ctr_next = nullptr;  // [kCoopShards] the next frame's, zeroed by k_trace_coop
     uint32_t cap = 0;              // entries per shard
-    // trace.coop_async (full frames): the entries are published for a
-    // k_trace_coop running beside k_trace -- each entry is re-stored with
-    // write-through stores at the end of its wave and then stamped
-    // last with `epoch`; that consumer claims entries through `take` and the
-    // queue pass after k_trace starts each shard where it stopped
-    uint32_t* take = nullptr;      // [kCoopShards] claims of this frame
-    uint32_t* take_next = nullptr; // [kCoopShards] the next frame's, zeroed with ctr_next
-    uint32_t* gate = nullptr;      // k_trace's last block writes `epoch` here when it starts
-    uint32_t* err = nullptr;       // a consumer's bounded wait gave up (never expected)
-    uint32_t epoch = 0;            // 0: synchronous queue (plain stores, no claims)
 };
-
-// coherent 16-B load (two 64-bit agent-scope relaxed atomic loads)
-__device__ __forceinline__ uint2 ld_coh2(const void* p) {
-    const uint64_t a = __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<void*>(p)), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    return make_uint2((uint32_t)a, (uint32_t)(a >> 32));
-}
-__device__ __forceinline__ uint4 ld_coh(const uint4* p) {
-    const uint2 a = ld_coh2(p), b = ld_coh2(reinterpret_cast<const char*>(p) + 8);
-    return make_uint4(a.x, a.y, b.x, b.y);
-}
-template <bool COH>
-__device__ __forceinline__ uint4 ent_ld(const uint4* p) {
-    if constexpr (COH) return ld_coh(p);
-    return *p;
-}
 
 // Called by the lanes that reach the step cap in this step (divergent): one
 // atomic per wave reserves their entries.  Returns 3 (deferred) with the
@@ -739,7 +713,7 @@ __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint
     const uint32_t nst = R.sp + (R.cur != RT_SENT ? 1u : 0u);
     e[0] = make_uint4(x, y, s, pi);
     e[1] = make_uint4(__float_as_uint(r), __float_as_uint(g), __float_as_uint(b), R.hp);
-    e[2] = make_uint4(__float_as_uint(R.tb), __float_as_uint(R.hu), __float_as_uint(R.hv), nst);  // unstamped
+    e[2] = make_uint4(__float_as_uint(R.tb), __float_as_uint(R.hu), __float_as_uint(R.hv), nst);
     for (uint32_t j = 0; j < nst; j += 2) {
         uint32_t rf[2], tn[2];
 #pragma unroll
@@ -750,31 +724,6 @@ __device__ __forceinline__ void coop_store(const CoopQ& cq, uint32_t qslot, uint
         }
         e[3 + j / 2] = make_uint4(rf[0], tn[0], rf[1], tn[1]);
     }
-}
-
-// trace.coop_async: publish a deferred lane's entry at the end of its wave,
-// where few registers are live.  coop_store's plain stores may still sit
-// dirty in this XCD's L2, invisible to a consumer on another XCD; the entry
-// is read back (this wave's own stores: fresh) and stored again with
-// agent-scope atomic stores, which write through, then -- after a wait for
-// them -- stamped with the epoch.  (The same atomic stores at the deferral
-// itself cost the full-frame kernel 13 VGPRs, 7 -> 5 waves per SIMD.)
-__device__ __forceinline__ void coop_publish(const CoopQ& cq, uint32_t qslot) {
-    uint4* e = cq.q + (uint64_t)qslot * kCoopEntry;
-    const uint4 h2 = e[2];
-    const uint32_t nw = 3 + ((h2.w & 0xFFu) + 1) / 2;  // uint4 in use
-    for (uint32_t k = 0; k < nw; ++k) {
-        const uint4 v = e[k];
-        uint64_t* q = reinterpret_cast<uint64_t*>(e + k);
-        __hip_atomic_store(q, (uint64_t)v.x | ((uint64_t)v.y << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (k != 2)
-            __hip_atomic_store(q + 1, (uint64_t)v.z | ((uint64_t)v.w << 32), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding; stores count in vmcnt)
-    uint64_t* q2 = reinterpret_cast<uint64_t*>(e + 2) + 1;
-    __hip_atomic_store(q2, (uint64_t)h2.z | ((uint64_t)((h2.w & 0xFFu) | (cq.epoch << 8)) << 32), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ int coop_defer(const CoopQ& cq, uint32_t gw, uint32_t& qslot) {
@@ -933,12 +882,6 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             return;
         }
     }
-    if constexpr (CQ && !SHADOW) {
-        // trace.coop_async: the last block has started, so every block is
-        // dispatched -- k_coop_gate lets the concurrent queue pass go
-        if (cq.gate && blockIdx.x == gridDim.x - 1 && threadIdx.x == 0)
-            __hip_atomic_store(cq.gate, cq.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     // tile slot from the block id: consecutive tiles go to different XCDs
     // under the round-robin dispatch, which balances the image's cheap and
     // costly bands over the 8 XCDs (an XCD-banded remap measured 1.2x
@@ -1085,9 +1028,6 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             atomicAdd(&counters[1], bsum);
         }
     }
-    if constexpr (CQ && !SHADOW) {
-        if (cq.epoch && dsamp != RT_SENT) coop_publish(cq, qslot);
-    }
     if (PX && px_cost) px_cost[(uint64_t)slot * 256 + ly * 16 + lx] = (uint16_t)min(steps, 65535u);
     if (cost_out && l == 0) {  // this wave's duration (10-ns ticks) -> the tile's cost map entry
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
@@ -1171,7 +1111,7 @@ __device__ __forceinline__ uint32_t gread_u(uint32_t x, uint32_t src) {
 // axis.  hp = prim.
 // resume (nullable): a queue entry -- start from its best hit and pending
 // entries (pass 1's state) instead of the root.
-template <bool COUNT, int G, int W = 4, bool COH = false>
+template <bool COUNT, int G, int W = 4>
 __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                            const float4* __restrict__ tri_s, uint32_t n, const float* o,
                                            const float* d, CoopLds<G, W>& L, const uint4* __restrict__ resume,
@@ -1190,12 +1130,12 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
     uint32_t hp0 = RT_SENT;  // the best hit's prim when resumed
     uint32_t sp = 1;
     if (resume) {
-        const uint4 h1 = ent_ld<COH>(resume + 1), h2 = ent_ld<COH>(resume + 2);
+        const uint4 h1 = resume[1], h2 = resume[2];
         hp0 = h1.w;
         tb = __uint_as_float(h2.x); hu = __uint_as_float(h2.y); hv = __uint_as_float(h2.z);
-        sp = h2.w & 0xFFu;  // the stamp's epoch above
+        sp = h2.w;
         for (uint32_t i = gl; i < sp; i += G) {
-            const uint4 pr = ent_ld<COH>(resume + 3 + i / 2);
+            const uint4 pr = resume[3 + i / 2];
             L.ref[i] = (i & 1) ? pr.z : pr.x;
             L.tn[i] = __uint_as_float((i & 1) ? pr.w : pr.y);
         }
@@ -1339,59 +1279,7 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // launch (8-11 us, all of it latency) leaves the next frame's critical path
 // -- and leaves the queue to the other blocks.
 constexpr uint32_t kOrderInCoop = 256 * 32;  // up to 8192 tiles: a 1080p full frame has 8160
-// One queued ray (entry `ent`) finished by group grp: its remaining samples,
-// its hit records and its pixel.  COH: the entry was published by a k_trace
-// still running (trace.coop_async) -- read it with coherent loads.
-template <bool COUNT, int G, int WA, bool COH>
-__device__ __forceinline__ void coop_entry(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
-                                           const float4* __restrict__ tri_s, uint32_t n, const Cam& cam, uint32_t W,
-                                           uint32_t spp, const uint4* ent, CoopLds<G, WA>& L,
-                                           float4* __restrict__ hits, uint32_t* __restrict__ rgba, uint32_t gl,
-                                           uint32_t& cn, uint32_t& ct) {
-    const uint4 a = ent_ld<COH>(ent), b = ent_ld<COH>(ent + 1);
-    const uint32_t x = a.x, y = a.y, pi = a.w;
-    float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
-    for (uint32_t s = a.z; s < spp; ++s) {
-        const uint32_t sidx = (y * W + x) * spp + s;
-        float jx = 0.5f, jy = 0.5f;
-        if (s > 0) {
-            const uint32_t hh = pcg_hash(sidx);
-            jx = (float)(hh >> 8) * 0x1p-24f;
-            jy = (float)(pcg_hash(hh) >> 8) * 0x1p-24f;
-        }
-        const float px = (float)x + jx, py = (float)y + jy;
-        float d[3];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
-        float tb, hu, hv;
-        uint32_t hp;
-        coop_trace<COUNT, G, WA, COH>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, L,
-                                      s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
-        if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
-        if (hp != RT_SENT) {
-            r = r + hu;
-            g = g + hv;
-            bl = bl + ((1.0f - hu) - hv);
-        } else {
-            r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
-        }
-    }
-    if (rgba && gl == 0) {
-        const float sc = 1.0f / (float)spp;
-        rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
-    }
-}
-
-// ASYNC (trace.coop_async, full frames): launched on a second stream behind
-// k_coop_gate, so its blocks take the CU slots k_trace's last blocks free
-// while they still run.  Each group claims published entries shard by shard
-// (a CAS on the shard's claim counter, only for the next entry and only when
-// it carries this frame's stamp -- coop_publish writes it at the end of the
-// deferring wave) and finishes the ray; a group leaves when no shard's next
-// entry is published.  The rest is left to the synchronous pass after
-// k_trace, which starts every shard at its claim counter.  Either way each
-// entry is finished exactly once, by the same code.
-template <bool COUNT, bool PACKED, int G, int WA = 4, bool ASYNC = false>
+template <bool COUNT, bool PACKED, int G, int WA = 4>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
                                                     uint32_t W, uint32_t spp, CoopQ cq, float4* __restrict__ hits,
@@ -1399,100 +1287,79 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                                                     unsigned long long* __restrict__ counters,
                                                     uint32_t* __restrict__ ord_cost = nullptr, uint32_t ord_nb = 0,
                                                     uint32_t* __restrict__ ord_out = nullptr,
-                                                    uint32_t* __restrict__ ord_ema = nullptr, uint32_t npix = 0) {
+                                                    uint32_t* __restrict__ ord_ema = nullptr) {
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
+    if (blockIdx.x == 0 && threadIdx.x < kCoopShards) cq.ctr_next[threadIdx.x] = 0u;
+    static_assert(sizeof(CoopLds<G, WA>) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
+    const bool order_block = ord_out && gridDim.x > 1;  // uniform
+    if (order_block && blockIdx.x == 0) {
+        tile_order_block<256, kOrderInCoop / 256>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
+                                  reinterpret_cast<uint32_t*>(&s_l[0]) + 256, ord_ema);
+        return;
+    }
+    const uint32_t b0 = order_block ? 1u : 0u;  // queue work over blocks [b0, gridDim.x)
     const uint32_t lane = threadIdx.x & 63, grp = threadIdx.x / G, gl = threadIdx.x & (G - 1);
-    uint32_t cn = 0, ct = 0;
-    if constexpr (ASYNC) {
-        const uint32_t gbase = lane & ~(uint32_t)(G - 1);
-        const uint32_t gid = blockIdx.x * NG + grp;
-        const uint32_t stamp = cq.epoch & 0xFFFFFFu;
-        for (uint32_t k = 0; k < kCoopShards;) {
-            const uint32_t sh = (gid + k) & (kCoopShards - 1);
-            uint32_t t = RT_SENT;
-            if (gl == 0) {
-                // claim the shard's next entry if it is published; never wait
-                // for one (a waiting group would poll memory beside k_trace):
-                // what is not published yet is left to the pass after k_trace
-                uint32_t c = __hip_atomic_load(cq.take + sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                for (;;) {
-                    const uint32_t f = min(__hip_atomic_load(cq.ctr + sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                                           cq.cap);
-                    if (c >= f) break;
-                    const uint4* ec = cq.q + ((uint64_t)sh * cq.cap + c) * kCoopEntry;
-                    if ((ld_coh2(reinterpret_cast<const char*>(ec + 2) + 8).y >> 8) != stamp) break;
-                    uint32_t ex = c;
-                    if (__hip_atomic_compare_exchange_strong(cq.take + sh, &ex, c + 1, __ATOMIC_RELAXED,
-                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-                        t = c;
-                        break;
-                    }
-                    c = ex;
-                }
-            }
-            t = (uint32_t)__shfl((int)t, (int)gbase, 64);
-            if (t == RT_SENT) {
-                ++k;
-                continue;
-            }
-            const uint4* ent = cq.q + ((uint64_t)sh * cq.cap + t) * kCoopEntry;
-            __builtin_amdgcn_wave_barrier();
-            // defence in depth: an entry read before its stores landed must
-            // never index the outputs out of range (the test suite would
-            // then see the wrong pixel; err records it)
-            if (ent_ld<true>(ent).w >= npix) {
-                if (gl == 0) __hip_atomic_store(cq.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                continue;
-            }
-            coop_entry<COUNT, G, WA, true>(nodes, wnodes, tri_s, n, cam, W, spp, ent, s_l[grp], hits, rgba, gl, cn, ct);
-        }
-    } else {
-        if (blockIdx.x == 0 && threadIdx.x < kCoopShards) {
-            cq.ctr_next[threadIdx.x] = 0u;
-            if (cq.take_next) cq.take_next[threadIdx.x] = 0u;
-        }
-        static_assert(sizeof(CoopLds<G, WA>) >= (256 + 16) * sizeof(uint32_t), "tile_order_block's LDS");
-        const bool order_block = ord_out && gridDim.x > 1;  // uniform
-        if (order_block && blockIdx.x == 0) {
-            tile_order_block<256, kOrderInCoop / 256>(ord_cost, ord_nb, ord_out, reinterpret_cast<uint32_t*>(&s_l[0]),
-                                                      reinterpret_cast<uint32_t*>(&s_l[0]) + 256, ord_ema);
-            return;
-        }
-        const uint32_t b0 = order_block ? 1u : 0u;  // queue work over blocks [b0, gridDim.x)
-        // the shards' unfinished entries -- [take, filled) after an ASYNC pass,
-        // else [0, filled) -- and their exclusive prefix, lane k = shard k
-        const uint32_t fill = min(cq.ctr[lane], cq.cap);
-        const uint32_t beg = cq.take ? min(cq.take[lane], fill) : 0u;
-        const uint32_t len = fill - beg;
-        uint32_t incl = len;
+    // the shards' filled lengths and their exclusive prefix, lane k = shard k
+    const uint32_t len = min(cq.ctr[lane], cq.cap);
+    uint32_t incl = len;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if (lane >= (uint32_t)o) incl += y;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    // the shard table goes through LDS: inside the divergent loop below the
+    // lanes of finished groups are inactive, and a lane read (readlane or a
+    // shuffle) of a value the compiler computes there would see stale lanes
+    __shared__ uint32_t s_excl[kCoopShards], s_len[kCoopShards];
+    if (threadIdx.x < 64) {
+        s_excl[lane] = incl - len;
+        s_len[lane] = len;
+    }
+    __syncthreads();
+    const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
+    uint32_t cn = 0, ct = 0;
+    for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
+        // queued ray e lives in the last non-empty shard whose prefix is <= e
+        uint32_t sh = 0, sbase = 0;
+        for (uint32_t k = 0; k < 64; ++k) {
+            const uint32_t ek = s_excl[k];
+            if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
         }
-        // the shard table goes through LDS: inside the divergent loop below the
-        // lanes of finished groups are inactive, and a lane read (readlane or a
-        // shuffle) of a value the compiler computes there would see stale lanes
-        __shared__ uint32_t s_excl[kCoopShards], s_len[kCoopShards], s_beg[kCoopShards];
-        if (threadIdx.x < 64) {
-            s_excl[lane] = incl - len;
-            s_len[lane] = len;
-            s_beg[lane] = beg;
-        }
-        __syncthreads();
-        const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
-        for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
-            // queued ray e lives in the last non-empty shard whose prefix is <= e
-            uint32_t sh = 0, sbase = 0;
-            for (uint32_t k = 0; k < 64; ++k) {
-                const uint32_t ek = s_excl[k];
-                if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
+        const uint32_t slot = sh * cq.cap + (e - sbase);
+        const uint4* ent = cq.q + (uint64_t)slot * kCoopEntry;
+        const uint4 a = ent[0], b = ent[1];
+        const uint32_t x = a.x, y = a.y, pi = a.w;
+        float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
+        for (uint32_t s = a.z; s < spp; ++s) {
+            const uint32_t sidx = (y * W + x) * spp + s;
+            float jx = 0.5f, jy = 0.5f;
+            if (s > 0) {
+                const uint32_t hh = pcg_hash(sidx);
+                jx = (float)(hh >> 8) * 0x1p-24f;
+                jy = (float)(pcg_hash(hh) >> 8) * 0x1p-24f;
             }
-            const uint32_t slot = sh * cq.cap + s_beg[sh] + (e - sbase);
-            coop_entry<COUNT, G, WA, false>(nodes, wnodes, tri_s, n, cam, W, spp, cq.q + (uint64_t)slot * kCoopEntry,
-                                            s_l[grp], hits, rgba, gl, cn, ct);
+            const float px = (float)x + jx, py = (float)y + jy;
+            float d[3];
+#pragma unroll
+            for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+            float tb, hu, hv;
+            uint32_t hp;
+            coop_trace<COUNT, G, WA>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp],
+                                 s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
+            if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
+            if (hp != RT_SENT) {
+                r = r + hu;
+                g = g + hv;
+                bl = bl + ((1.0f - hu) - hv);
+            } else {
+                r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
+            }
+        }
+        if (rgba && gl == 0) {
+            const float sc = 1.0f / (float)spp;
+            rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
         }
     }
     if (COUNT) {
@@ -1509,18 +1376,6 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     }
 }
 
-// trace.coop_async: holds its stream until k_trace's last block has started
-// (every block of k_trace is then dispatched, so the k_trace_coop behind it
-// only takes the slots k_trace's finishing blocks free); bounded (~20 ms).
-__global__ __launch_bounds__(64) void k_coop_gate(const uint32_t* __restrict__ gate, uint32_t epoch) {
-    if (threadIdx.x == 0) {
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(const_cast<uint32_t*>(gate), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch) {
-            __builtin_amdgcn_s_sleep(2);
-            if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) break;
-        }
-    }
-}
 
 // ---------------------------------------------------------------- path mode
 // Path mode [SPEC, DESIGN.md "Path mode"; SURVEY.md §8(f) row 3]: per
@@ -2240,22 +2095,6 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t g
     RT_KLAUNCH((k_trace<C, P, WI, NT, false, false, 4>), dim3(grid), dim3(NT), 0, s, a...);
 }
 
-// the concurrent queue pass's grid (trace.coop_async): one block per CU
-#ifndef RT_COOP_ASYNC_GRID
-#define RT_COOP_ASYNC_GRID 256
-#endif
-
-void sched_release(TileSched& t) {
-    if (t.s2) {
-        (void)hipStreamSynchronize(t.s2);
-        (void)hipStreamDestroy(t.s2);
-    }
-    if (t.ev_go) (void)hipEventDestroy(t.ev_go);
-    if (t.ev_done) (void)hipEventDestroy(t.ev_done);
-    t.s2 = nullptr;
-    t.ev_go = t.ev_done = nullptr;
-}
-
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tris, uint32_t n,
                         const CamF& c, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
                         bool packed, void* hits, void* rgba, unsigned long long* counters, bool binary_counts,
@@ -2384,35 +2223,16 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         sched->prev_cam_valid = true;
     }
     CoopQ cq;
-    // trace.coop_async: full frames (one rank, no counters) also drain the
-    // queue beside k_trace's last blocks, on the scene's second stream
-    const bool async = coop_cap && cfg.coop_async && nranks == 1 && !packed && !counters && !small;
     if (coop_cap) {
         if (sched->coop_fresh) {
-            hipError_t me = hipMemsetAsync(sched->coop_ctr, 0, kCoopCtlWords * sizeof(uint32_t), s);
+            hipError_t me = hipMemsetAsync(sched->coop_ctr, 0, 2 * kCoopShards * sizeof(uint32_t), s);
             if (me != hipSuccess) return me;
             sched->coop_fresh = false;
         }
         cq.q = sched->coop_q;
         cq.ctr = sched->coop_ctr + sched->coop_par * kCoopShards;
         cq.ctr_next = sched->coop_ctr + (sched->coop_par ^ 1u) * kCoopShards;
-        cq.take = sched->coop_ctr + (2 + sched->coop_par) * kCoopShards;
-        cq.take_next = sched->coop_ctr + (2 + (sched->coop_par ^ 1u)) * kCoopShards;
         cq.cap = sched->coop_qcap / kCoopShards;
-        if (async) {
-            if (!sched->s2) {
-                hipError_t e = hipStreamCreateWithFlags(&sched->s2, hipStreamNonBlocking);
-                if (e == hipSuccess) e = hipEventCreateWithFlags(&sched->ev_go, hipEventDisableTiming);
-                if (e == hipSuccess) e = hipEventCreateWithFlags(&sched->ev_done, hipEventDisableTiming);
-                if (e != hipSuccess) return e;
-            }
-            sched->epoch = sched->epoch % 0xFFFFFFu + 1u;  // 24 bits, never 0
-            cq.epoch = sched->epoch;
-            cq.gate = sched->coop_ctr + 4 * kCoopShards;
-            cq.err = sched->coop_ctr + 4 * kCoopShards + 1;
-            hipError_t e = hipEventRecord(sched->ev_go, s);
-            if (e != hipSuccess) return e;
-        }
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
@@ -2470,33 +2290,6 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
                 resident[dev][gi][ai].store(r, std::memory_order_relaxed);
             }
             cgrid = r;
-        }
-        if (async) {
-            // the concurrent pass: behind the gate on the second stream, one
-            // block per CU at most (it only fills slots k_trace frees); the
-            // synchronous pass below then waits for it and takes the rest
-            hipError_t e = hipStreamWaitEvent(sched->s2, sched->ev_go, 0);
-            if (e != hipSuccess) return e;
-            RT_KLAUNCH(k_coop_gate, dim3(1), dim3(64), 0, sched->s2, cq.gate, cq.epoch);
-            const uint32_t agrid = std::min<uint32_t>(cgrid, RT_COOP_ASYNC_GRID);
-#define RT_COOP_A(G)                                                                                               \
-    if (warity == 8)                                                                                               \
-        RT_KLAUNCH((k_trace_coop<false, false, G, 8, true>), dim3(agrid), dim3(256), 0, sched->s2, nodes, wnodes,   \
-                   tris, n, cam, w, spp, cq, H, R, counters, nullptr, 0u, nullptr, nullptr, w * h);                 \
-    else                                                                                                           \
-        RT_KLAUNCH((k_trace_coop<false, false, G, 4, true>), dim3(agrid), dim3(256), 0, sched->s2, nodes, wnodes,   \
-                   tris, n, cam, w, spp, cq, H, R, counters, nullptr, 0u, nullptr, nullptr, w * h)
-            if (cfg.coop_lanes == 16) {
-                RT_COOP_A(16);
-            } else if (cfg.coop_lanes == 32) {
-                RT_COOP_A(32);
-            } else {
-                RT_COOP_A(64);
-            }
-#undef RT_COOP_A
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-            if ((e = hipEventRecord(sched->ev_done, sched->s2)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(s, sched->ev_done, 0)) != hipSuccess) return e;
         }
         // block 0 sorts this frame's cost map into the next frame's tile order
         const bool ord = cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;

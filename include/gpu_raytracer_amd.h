@@ -343,11 +343,7 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * at 1 spp on 256-thread tiles (off otherwise) and, for one rank's tiles of a
  * multi-GPU frame, by rank count (88 steps for P = 2, 80 for P >= 3);
  * "trace.coop_max" queue entries per frame shape
- * (default 65536; rays beyond it keep tracing alone).  "trace.coop_async"
- * 0/1: for full frames, a second k_trace_coop on the scene's second stream
- * starts when k_trace's last block does and finishes queued rays while
- * k_trace still runs; the pass after k_trace takes the rest (same results).
- * "build.stage_events"
+ * (default 65536; rays beyond it keep tracing alone).  "build.stage_events"
  * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
  * 0/1: timing events of scenes created afterwards record with the
  * system-scope fence (default 0: no L2 writeback at each record).

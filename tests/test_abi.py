@@ -260,7 +260,6 @@ CONFIG_KEYS = {
     "trace.blocks": ([0, 4096], [-1], 0),
     "build.sort": ([0, 1, 2], [3, -1], 2),
     "build.fuse_k01": ([0, 1, 2], [3, -1], 1),
-    "trace.coop_async": ([0, 1], [2, -1], 0),
     "build.wide_collapse": ([0, 1], [2, -1], 1),
     "build.wide_arity": ([4, 8], [2, 6, 16, -1], 4),
     "build.stage_events": ([0, 1], [2], 0),

@@ -5,11 +5,9 @@ queued and finished by k_trace_coop, a group of 16/32/64 lanes per ray, folding 
 and RGBA) whatever the cap, the queue capacity (a full queue leaves rays to
 their own lane), the samples per pixel (a pixel resumes at its deferred
 sample with the colour sums of the earlier ones), the full-frame and the
-per-rank tiled kernels, successive frames (tile/pixel order on), the
+per-rank tiled kernels, successive frames (tile/pixel order on), and the
 frontier hand-off to the binary traversal (a scene of identical triangles,
-whose boxes all overlap, overflows the frontier), and trace.coop_async (a
-second k_trace_coop on a second stream claims queued rays while k_trace
-still runs; the synchronous pass finishes the rest)."""
+whose boxes all overlap, overflows the frontier)."""
 import numpy as np
 import pytest
 
@@ -53,18 +51,16 @@ def _soup_view():
     return SOUP_VIEW
 
 
-@pytest.mark.parametrize("asyn", [0, 1])
 @pytest.mark.parametrize("lanes", [16, 32, 64])
 @pytest.mark.parametrize("cap", [1, 2, 5, 16, 40])
 @pytest.mark.parametrize("spp", [1, 3])
-def test_coop_full_frame(R, oracle, cfg, cap, spp, lanes, asyn):
+def test_coop_full_frame(R, oracle, cfg, cap, spp, lanes):
     V = _soup_view()
     tris = oracle.soup(40000, 11).reshape(-1, 9)
     w, h = 200, 120
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("trace.coop_cap", cap, -1)
     cfg("trace.coop_lanes", lanes, 32)
-    cfg("trace.coop_async", asyn, 0)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
@@ -92,15 +88,13 @@ def test_coop_changes_work_not_result(R, oracle, cfg):
     assert not np.array_equal(base, coop)
 
 
-@pytest.mark.parametrize("asyn", [0, 1])
 @pytest.mark.parametrize("qmax", [1, 7, 100])
-def test_coop_queue_full(R, oracle, cfg, qmax, asyn):
+def test_coop_queue_full(R, oracle, cfg, qmax):
     V = _soup_view()
     tris = oracle.soup(30000, 13).reshape(-1, 9)
     w, h, spp = 150, 100, 2
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("trace.coop_max", qmax, 65536)
-    cfg("trace.coop_async", asyn, 0)
     cfg("trace.coop_cap", 3, -1)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
@@ -154,18 +148,14 @@ def test_coop_frontier_handoff(R, oracle, cfg, lanes):
     assert _same_hits(hits, eh)
 
 
-@pytest.mark.parametrize("asyn,cap", [(0, 48), (1, 48), (1, 96), (1, 8)])
-def test_coop_headline_1m(R, oracle, cfg, asyn, cap):
+def test_coop_headline_1m(R, oracle, cfg):
     """The soup-1M 1080p frame with the tile default cap applied to the full
-    frame (the rays past 48 wide steps, ~10 % of the frame), the full-frame
-    default (96) and a very low one (8: most rays queued, so the concurrent
-    pass has work from the start), synchronous and concurrent == the oracle."""
+    frame (the rays past 48 wide steps, ~10 % of the frame) == the oracle."""
     V = _soup_view()
     tris = oracle.soup(1_000_000, 1).reshape(-1, 9)
     w, h = 1920, 1080
     eh, er = _frame(oracle, tris, V, w, h, 1)
-    cfg("trace.coop_cap", cap, -1)
-    cfg("trace.coop_async", asyn, 0)
+    cfg("trace.coop_cap", 48, -1)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     with R.Scene.from_soup(tris) as s:
         s.build()
