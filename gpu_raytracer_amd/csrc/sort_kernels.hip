@@ -1134,7 +1134,10 @@ struct GatherShape { int nt, p; };
 static GatherShape gather_shape(uint32_t n) {
     const double mean = (double)n / kMsbBuckets;
     const double need = mean + 16.0 * std::sqrt(mean) + 64.0;
-    if (need <= 256 * 8) return {256, 8};
+#ifndef RT_GATHER_SMALL_NT
+#define RT_GATHER_SMALL_NT 256  // the n <= ~1.9M shape: 256 x 8 keys (512 x 4 measured in r04)
+#endif
+    if (need <= 256 * 8) return {RT_GATHER_SMALL_NT, 2048 / RT_GATHER_SMALL_NT};
     if (need <= 512 * 8) return {512, 8};
     if (need <= 1024 * 12) return {1024, 12};
     return {1024, 16};
@@ -1177,7 +1180,10 @@ hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_
     const GatherShape gs = gather_shape(n);
     if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), dense);
     const Gate g{dense, 0u};
-    if (gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, kout, vout, flags, bstart, s, g);
+    if (gs.nt * gs.p == 2048 && gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, kout, vout, flags, bstart, s, g);
+#if RT_GATHER_SMALL_NT == 512
+    if (gs.nt * gs.p == 2048) return gather_launch<512, 4>(words, tb, nt, kout, vout, flags, bstart, s, g);
+#endif
     if (gs.nt == 512) return gather_launch<512, 8>(words, tb, nt, kout, vout, flags, bstart, s, g);
     if (gs.p == 12) return gather_launch<1024, 12>(words, tb, nt, kout, vout, flags, bstart, s, g);
     return gather_launch<1024, 16>(words, tb, nt, kout, vout, flags, bstart, s, g);
