@@ -108,7 +108,13 @@ __device__ __forceinline__ uint32_t load_tri_lanes_part(const float* __restrict_
 }
 
 // ---------------------------------------------------------------- K0
-__global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, uint32_t n,
+#ifndef RT_K0_WAVES
+#define RT_K0_WAVES 1  // min waves per SIMD K0 is compiled for (1: the compiler's choice, 84 VGPRs / 5)
+#endif
+#ifndef RT_K0_HALVES
+#define RT_K0_HALVES 0
+#endif
+__global__ __launch_bounds__(256, RT_K0_WAVES) void k_bounds(const float* __restrict__ tris, uint32_t n,
                                                 float* __restrict__ partials,
                                                 uint32_t* __restrict__ zero_words, uint32_t nzero) {
     __shared__ float red[4][6];
@@ -118,18 +124,25 @@ __global__ __launch_bounds__(256) void k_bounds(const float* __restrict__ tris, 
 #pragma unroll
     for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
     {
-        float t[kTrisPerThread][9];
-        const uint32_t ok = load_tri_lanes(tris, n, (blockIdx.x * 4u + (threadIdx.x >> 6)) * 64u * kTrisPerThread, t);
+        // RT_K0_HALVES: the lane's 8 triangles in batches of QB (36 instead of
+        // 72 triangle registers at QB = 4), for more resident waves
+        constexpr uint32_t QB = RT_K0_HALVES ? kTrisPerThread / 2 : kTrisPerThread;
+        const uint32_t base = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 64u * kTrisPerThread;
 #pragma unroll
-        for (uint32_t q = 0; q < kTrisPerThread; ++q) {
-            if ((ok >> q) & 1u) {
-                float bmin[3], bmax[3];
-                tri_bounds(t[q], bmin, bmax);
+        for (uint32_t h = 0; h < kTrisPerThread / QB; ++h) {
+            float t[QB][9];
+            const uint32_t ok = load_tri_lanes_part<QB>(tris, n, base, h * QB, t);
 #pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    const float cc = (bmin[c] + bmax[c]) * 0.5f;
-                    lo[c] = fminf(lo[c], cc);
-                    hi[c] = fmaxf(hi[c], cc);
+            for (uint32_t qi = 0; qi < QB; ++qi) {
+                if ((ok >> (h * QB + qi)) & 1u) {
+                    float bmin[3], bmax[3];
+                    tri_bounds(t[qi], bmin, bmax);
+#pragma unroll
+                    for (int c = 0; c < 3; ++c) {
+                        const float cc = (bmin[c] + bmax[c]) * 0.5f;
+                        lo[c] = fminf(lo[c], cc);
+                        hi[c] = fmaxf(hi[c], cc);
+                    }
                 }
             }
         }
@@ -341,8 +354,11 @@ static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
 #endif
 // NT threads per 4096-key tile (NT x kSortTile / NT triangles; the block shape
 // is RT_K1F_NT / RT_K1U_NT below)
+#ifndef RT_K1U_WAVES
+#define RT_K1U_WAVES 1  // min waves per SIMD the unfused K1-TB is compiled for (1: the compiler's choice)
+#endif
 template <bool FUSED, int NT = kSortThreads>
-__global__ __launch_bounds__(NT) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
+__global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
                                                             BuildParams* __restrict__ params,
                                                             float* __restrict__ partials, uint32_t nb,
                                                             uint32_t* __restrict__ words_tb,
