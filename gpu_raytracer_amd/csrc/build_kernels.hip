@@ -112,7 +112,7 @@ __device__ __forceinline__ uint32_t load_tri_lanes_part(const float* __restrict_
 #define RT_K0_WAVES 1  // min waves per SIMD K0 is compiled for (1: the compiler's choice, 84 VGPRs / 5)
 #endif
 #ifndef RT_K0_HALVES
-#define RT_K0_HALVES 0
+#define RT_K0_HALVES 0  // 1: 4 + 4 triangles per lane (47 VGPRs, 8 waves): no faster at 10M (r04)
 #endif
 __global__ __launch_bounds__(256, RT_K0_WAVES) void k_bounds(const float* __restrict__ tris, uint32_t n,
                                                 float* __restrict__ partials,
@@ -355,7 +355,7 @@ static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
 // NT threads per 4096-key tile (NT x kSortTile / NT triangles; the block shape
 // is RT_K1F_NT / RT_K1U_NT below)
 #ifndef RT_K1U_WAVES
-#define RT_K1U_WAVES 1  // min waves per SIMD the unfused K1-TB is compiled for (1: the compiler's choice)
+#define RT_K1U_WAVES 8  // the unfused K1-TB at 8 waves per SIMD (62 VGPRs, no spills): 10M K1 80 -> 76 us (r04)
 #endif
 template <bool FUSED, int NT = kSortThreads>
 __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(const float* __restrict__ tris, uint32_t n,
