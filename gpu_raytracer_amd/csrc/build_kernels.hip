@@ -297,31 +297,42 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
 // count, the others wait for the generation to change.  A wait gives up
 // after ~100 ms (s_memrealtime) and sets *err -- a grid that is not
 // co-resident must not hang the GPU (the host reads *err after the build).
-__device__ __forceinline__ bool grid_sync(uint32_t* bar, uint32_t nblocks, uint32_t* err) {
-    __shared__ uint32_t s_ok;
+// It is split for a last-arriver step: grid_arrive_last counts the block in
+// and tells it (block-uniform) whether it is the last; the last block does
+// its step and then grid_open bumps the generation (and resets the count);
+// the others grid_wait for that.  The arrival's old value stays in LDS for
+// grid_wait.
+__device__ __forceinline__ uint32_t* grid_old_slot() {
+    __shared__ uint32_t s_old;
+    return &s_old;
+}
+__device__ __forceinline__ bool grid_arrive_last(uint32_t* bar, uint32_t nblocks) {
+    uint32_t* s_old = grid_old_slot();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
+    if (threadIdx.x == 0) *s_old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    return (*s_old & 0xFFFFu) == nblocks - 1;
+}
+__device__ __forceinline__ void grid_open(uint32_t* bar, uint32_t nblocks) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 0x10000u - nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void grid_wait(uint32_t* bar, uint32_t* err) {
+    const uint32_t old = *grid_old_slot();
     if (threadIdx.x == 0) {
-        const uint32_t old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t ok = 1;
-        if ((old & 0xFFFFu) == nblocks - 1) {
-            __hip_atomic_fetch_add(bar, 0x10000u - nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-            while ((__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == (old >> 16)) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
-                    ok = 0;
-                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while ((__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 16) == (old >> 16)) {
+            __builtin_amdgcn_s_sleep(1);
+            if (__builtin_amdgcn_s_memrealtime() - t0 > 10000000ull) {
+                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
             }
         }
-        s_ok = ok;
     }
-    __syncthreads();
-    return s_ok != 0;
 }
+
 
 // K1 + the first level of the gather sort (r04, sort_kernels.hip "tile-bucketed
 // gather sort"): the block's 4096 Morton keys are also grouped by bucket
@@ -344,6 +355,7 @@ struct FuseArgs {
     uint32_t nzero = 0;
     uint32_t* bar = nullptr;   // grid barrier counter (never zeroed: self-resetting)
     uint32_t* err = nullptr;   // set on a barrier timeout
+    float* box = nullptr;      // [6] the global centroid box, from the barrier's last block
 };
 static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
 #ifndef RT_K1_REVERSE
@@ -422,32 +434,50 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
             for (int k = 1; k < W; ++k) v = c < 3 ? fminf(v, red[k][c]) : fmaxf(v, red[k][c]);
             __hip_atomic_store(partials + tile * 6 + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        grid_sync(fu.bar, gridDim.x, fu.err);
-        // the second level, as bounds_final: every block reduces all partials
-        // (exact min/max: the same box in every block and as K0 + K1 give)
+        // The second level, as bounds_final (exact min/max: the same box as K0
+        // + K1 give), done ONCE: by the block that arrives last at the grid
+        // barrier -- every partial is published by then -- which stores the
+        // box and only then opens the barrier; the others read its 6 words.
+        // (Every block reducing all partials itself put tiles x 1470 coherent
+        // loads on the same few lines.)
+        if (grid_arrive_last(fu.bar, gridDim.x)) {  // block-uniform
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
-        for (uint32_t b = threadIdx.x; b < gridDim.x; b += NT) {
+            for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
+            for (uint32_t b = threadIdx.x; b < gridDim.x; b += NT) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                lo[c] = fminf(lo[c], __hip_atomic_load(partials + b * 6 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                hi[c] = fmaxf(hi[c], __hip_atomic_load(partials + b * 6 + 3 + c, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT));
+                for (int c = 0; c < 3; ++c) {
+                    lo[c] = fminf(lo[c], __hip_atomic_load(partials + b * 6 + c, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+                    hi[c] = fmaxf(hi[c], __hip_atomic_load(partials + b * 6 + 3 + c, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT));
+                }
             }
-        }
 #pragma unroll
-        for (int c = 0; c < 3; ++c) { lo[c] = wave_min(lo[c]); hi[c] = wave_max(hi[c]); }
-        __syncthreads();  // red[] reads of the partial box done
-        if (lane == 0) {
+            for (int c = 0; c < 3; ++c) { lo[c] = wave_min(lo[c]); hi[c] = wave_max(hi[c]); }
+            __syncthreads();  // red[] reads of the partial box done
+            if (lane == 0) {
 #pragma unroll
-            for (int c = 0; c < 3; ++c) { red[w][c] = lo[c]; red[w][3 + c] = hi[c]; }
+                for (int c = 0; c < 3; ++c) { red[w][c] = lo[c]; red[w][3 + c] = hi[c]; }
+            }
+            __syncthreads();
+            if (threadIdx.x < 6) {
+                const int c = threadIdx.x;
+                float v = red[0][c];
+#pragma unroll
+                for (int k = 1; k < W; ++k) v = c < 3 ? fminf(v, red[k][c]) : fmaxf(v, red[k][c]);
+                __hip_atomic_store(fu.box + c, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            grid_open(fu.bar, gridDim.x);
+        } else {
+            grid_wait(fu.bar, fu.err);
         }
+        __syncthreads();  // red[] free again
+        if (threadIdx.x < 6)
+            red[0][threadIdx.x] = __hip_atomic_load(fu.box + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            float a = red[0][c], b = red[0][3 + c];
-#pragma unroll
-            for (int k = 1; k < W; ++k) { a = fminf(a, red[k][c]); b = fmaxf(b, red[k][3 + c]); }
+            const float a = red[0][c], b = red[0][3 + c];
             p.lo[c] = a;
             p.hi[c] = b;
             p.inv[c] = (b > a) ? 1.0f / (b - a) : 0.0f;  // §9.2, correctly rounded
@@ -1714,7 +1744,8 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     // decides its later builds' sort (the host reads kZDense afterwards)
     const bool probe = kind != 0 && !(b.sort_mode != 0 && b.sort_mode_of == kind);
     if (kind == 2 && fused) {
-        const FuseArgs fu{b.zero, kZEnd, b.zero + kZBar, b.zero + kZFuseErr};
+        const FuseArgs fu{b.zero, kZEnd, b.zero + kZBar, b.zero + kZFuseErr,
+                          reinterpret_cast<float*>(b.zero + kZBox)};
         RT_KLAUNCH((k_morton_tb<true, RT_K1F_NT>), dim3(sort_tiles(n)), dim3(RT_K1F_NT), 0, s, b.tris, n, b.params, b.partials,
                    sort_tiles(n), b.keys[1], probe ? b.zero + kZHist : nullptr, b.counts, fu);
         if ((e = hipGetLastError()) != hipSuccess) return e;

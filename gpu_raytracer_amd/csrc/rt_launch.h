@@ -66,7 +66,8 @@ constexpr uint32_t kZEnd = 2084;        // words zeroed by K0 every build
 // (self-resetting) and its timeout flag (cleared by the host when it sees it)
 constexpr uint32_t kZBar = 2084;
 constexpr uint32_t kZFuseErr = 2085;
-constexpr uint32_t kZAlloc = 2088;      // words of the zero region
+constexpr uint32_t kZBox = 2088;        // [6] the fused K0+K1's global centroid box (its last block writes it)
+constexpr uint32_t kZAlloc = 2096;      // words of the zero region
 
 
 hipError_t alloc_build(BuildBufs& b, uint32_t n);
