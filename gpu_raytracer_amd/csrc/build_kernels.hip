@@ -398,6 +398,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
     constexpr bool HALVES = !FUSED && RT_K1TB_HALVES;
     constexpr uint32_t QL = HALVES ? TPT / 2 : TPT;
     float t[QL][9];
+    if (FUSED) RT_STAMP_HI(0);
     uint32_t okm = load_tri_lanes_part<QL>(tris, n, wbase, 0u, t);
     BuildParams p;
     if constexpr (FUSED) {
@@ -440,6 +441,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
         // box and only then opens the barrier; the others read its 6 words.
         // (Every block reducing all partials itself put tiles x 1470 coherent
         // loads on the same few lines.)
+        RT_STAMP_HI(1);  // triangles loaded, partial box published
         if (grid_arrive_last(fu.bar, gridDim.x)) {  // block-uniform
 #pragma unroll
             for (int c = 0; c < 3; ++c) { lo[c] = __builtin_inff(); hi[c] = -__builtin_inff(); }
@@ -472,6 +474,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
             grid_wait(fu.bar, fu.err);
         }
         __syncthreads();  // red[] free again
+        RT_STAMP_HI(2);  // through the barrier
         if (threadIdx.x < 6)
             red[0][threadIdx.x] = __hip_atomic_load(fu.box + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __syncthreads();
@@ -488,6 +491,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
         p = bounds_final<NT>(partials, nb, red);  // ends with a barrier
     }
     if (tile == 0 && threadIdx.x == 0) *params = p;
+    if (FUSED) RT_STAMP_HI(3);  // box read
     uint32_t k8[TPT];
 #pragma unroll
     for (uint32_t h = 0; h < TPT / QL; ++h) {
@@ -505,6 +509,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
         }
     }
     __syncthreads();
+    if (FUSED) RT_STAMP_HI(4);  // keys + LDS histogram
     constexpr int PER = kMsbBuckets / NT;  // buckets per thread in scan1024's layout
     uint32_t cnt[PER];
 #pragma unroll
@@ -517,6 +522,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
         if (ghist && cnt[j]) atomicAdd(&ghist[d], cnt[j]);  // a probe build's verdict needs the totals
     }
     __syncthreads();  // every start read: the starts become the bucket cursors
+    if (FUSED) RT_STAMP_HI(5);  // scan + table
 #pragma unroll
     for (uint32_t q = 0; q < TPT; ++q)
         if ((okm >> q) & 1u) {
@@ -524,6 +530,7 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
             s_word[pos] = (k8[q] << 12) | (w * 64u * TPT + q * 64u + lane);  // key bits 0..19, index
         }
     __syncthreads();
+    if (FUSED) RT_STAMP_HI(6);  // LDS scatter
     const uint32_t trem = n - tbase;
     const uint32_t tcount = trem < (uint32_t)kSortTile ? trem : (uint32_t)kSortTile;
 #pragma unroll
@@ -531,6 +538,12 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
         const uint32_t q = threadIdx.x + m * NT;
         if (q < tcount) words_tb[tbase + q] = s_word[q];
     }
+#ifdef RT_STAMPS
+    if (FUSED) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // the stamp after the stores land
+        RT_STAMP_HI(7);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- K4 (+K5)

@@ -172,7 +172,18 @@ static __device__ unsigned long long g_rt_stamps[1u << 20];
     do {                                                                     \
         if (threadIdx.x == 0) g_rt_stamps[(uint64_t)blockIdx.x * 8 + (s)] = (v); \
     } while (0)
+// a second record set from block 65536 on (a kernel that runs before another
+// stamped kernel of the same translation unit)
+#define RT_STAMP_HI(s)                                                       \
+    do {                                                                     \
+        if (threadIdx.x == 0) {                                              \
+            __builtin_amdgcn_sched_barrier(0);                               \
+            g_rt_stamps[(65536ull + blockIdx.x) * 8 + (s)] = __builtin_amdgcn_s_memrealtime(); \
+            __builtin_amdgcn_sched_barrier(0);                               \
+        }                                                                    \
+    } while (0)
 #else
+#define RT_STAMP_HI(s) do {} while (0)
 #define RT_STAMP(s) do {} while (0)
 #define RT_STAMP_VAL(s, v) do {} while (0)
 #endif

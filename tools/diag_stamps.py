@@ -40,6 +40,12 @@ s = R.Scene.generate_soup(n, 1)
 for _ in range(3):
     s.build()
 M = (n + 511) // 512
+if n <= 1_048_576:  # the fused K0 + K1 (its records from block 65536 on)
+    T = (n + 4095) // 4096
+    allst = stamps(65536 + T)
+    report("k_morton_tb<fused>", allst[65536:65536 + T, :8],
+           ["loads+partial box", "barrier (+ last block's reduction)", "box read", "keys+LDS histogram",
+            "scan+table", "cursor scatter (LDS)", "word stores"], 8)
 report("k_topo_refit", stamps(M)[:, :6], ["key window+sync", "topology+leaf (thread 0)", "scans+flags+sync",
                                           "sparse-table sweep+sync", "node+K7w stores"], 6)
 keys = np.random.default_rng(0).integers(0, 2**30, n, dtype=np.uint64).astype(np.uint32)
