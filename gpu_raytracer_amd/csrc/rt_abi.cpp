@@ -554,7 +554,7 @@ rt_status need_built(rt_scene* s, Replica** out) {
 bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     const std::string k(key);
     if (k == "trace.variant" && value >= 0 && value <= 2) c.variant = (uint32_t)value;
-    else if (k == "trace.stack_cap" && value >= 0 && value <= 18) c.stack_cap = (uint32_t)value;
+    else if (k == "trace.stack_cap" && value >= 0 && value <= rt::kWideStackMax) c.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) c.wg = (uint32_t)value;
     else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) c.wg_tiles = (uint32_t)value;
     else if (k == "trace.tile_order" && (value == 0 || value == 1)) c.tile_order = (uint32_t)value;

@@ -139,7 +139,23 @@ template <> struct WideFmt<8> {
     static constexpr uint32_t words = 6, bytes = 96;
     static constexpr int stack = 18;
 };
-constexpr int kWideStackMax = 18;
+// 4-ary stacks of 64-thread blocks (one rank's tiles of a multi-GPU frame):
+// 20 entries.  A ray whose stack overflows finishes in the binary traversal,
+// uncapped by the heavy-ray queue, and one such ray sets its rank's time: on
+// the bench's orbit a few frames hold overflowing rays, and the rank that owns
+// their tiles took 0.19-0.25 ms against 0.12 for the others.  At 64 threads
+// the deeper stack costs no occupancy (8 KB per block: 20 blocks per CU, the
+// tile kernel's 96 VGPRs allow 5 waves per SIMD anyway); the 256-thread
+// full-frame kernels keep 14 (20 would take 6 blocks per CU to 5).
+// (profiles/ab_stack_depth_r04.log)
+#ifndef RT_WIDE_STACK64
+#define RT_WIDE_STACK64 20
+#endif
+template <int W, int NT> struct StackOf {
+    static constexpr int v = (W == 4 && NT == 64) ? RT_WIDE_STACK64 : WideFmt<W>::stack;
+};
+constexpr int kWideStackMax = (RT_WIDE_STACK64 > 18 && RT_WIDE_STACK64 > kWideStack) ? RT_WIDE_STACK64
+                              : (kWideStack > 18 ? kWideStack : 18);
 constexpr uint32_t kWideRecMaxBytes = 96;  // wnodes is allocated for either arity
 constexpr uint32_t kPoolCounters = 32;  // pool-trace unit counters, 128 B apart (work buffer >= 4 KiB)
 

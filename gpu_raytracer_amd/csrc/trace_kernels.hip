@@ -666,7 +666,7 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
 // it -- is queued for k_trace_coop, which traces it with a whole wave.
 // Entries of kCoopEntry x 16 B: {x, y, deferred sample, output pixel index}
 // {r, g, b sums of the earlier samples, best prim} {tb, hu, hv, nst} and
-// the deferred sample's traversal state -- its nst <= kWideStack + 1 pending
+// the deferred sample's traversal state -- its nst <= the stack depth + 1 pending
 // entries {ref, tn} bottom to top (the lane's stack, then its current entry):
 // k_trace_coop resumes the ray there instead of restarting it at the root.
 // They live in kCoopShards shards of `cap` entries, each with its own reservation counter
@@ -691,7 +691,7 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
 constexpr uint32_t kCoopShards = 64;
 constexpr uint32_t kCoopFrontier = kWideStackMax + 1;        // pending entries a deferred ray can have (either arity)
 constexpr uint32_t kCoopEntry = 3 + (kCoopFrontier + 1) / 2;  // uint4 per queue entry
-static_assert(kCoopEntry * 16 == kCoopEntryBytes, "rt_launch.h sizes the queue");
+static_assert(kCoopEntry * 16 <= kCoopEntryBytes, "rt_launch.h sizes the queue");
 struct CoopQ {
     uint4* q = nullptr;
     uint32_t* ctr = nullptr;       // [kCoopShards] this frame's reservation counters
@@ -870,7 +870,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     // PX: the per-pixel order (below); its ranking borrows s_ref, so the
     // binary instance (no stack) still sizes s_ref for tile_pixel_order
     constexpr bool PX = !SHADOW && !COUNT && NT == 256;
-    constexpr uint32_t kStackWords = (WIDE || SHADOW) ? (WideFmt<WA>::stack + 1) * NT : 1u;
+    constexpr uint32_t kStackWords = (WIDE || SHADOW) ? (StackOf<WA, NT>::v + 1) * NT : 1u;
     constexpr uint32_t kRefWords = (PX && kStackWords < 144u) ? 144u : kStackWords;
     __shared__ uint32_t s_ref[kRefWords];
     __shared__ uint16_t s_tn[kStackWords];
@@ -1400,8 +1400,8 @@ __global__ __launch_bounds__(NT) void k_path(const void* __restrict__ nodes, con
                                               uint32_t H, uint32_t spp, uint32_t tilesX, PathCfg pc,
                                               float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                               unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t s_ref[(WideFmt<WA>::stack + 1) * NT];
-    __shared__ uint16_t s_tn[(WideFmt<WA>::stack + 1) * NT];
+    __shared__ uint32_t s_ref[(StackOf<WA, NT>::v + 1) * NT];
+    __shared__ uint16_t s_tn[(StackOf<WA, NT>::v + 1) * NT];
     constexpr uint32_t WPB = NT / 64;
     const uint32_t gw = blockIdx.x * WPB + (threadIdx.x >> 6);
     const uint32_t t = gw >> 2;
@@ -2060,10 +2060,13 @@ hipError_t dev_alloc(void** p, size_t bytes) {
     return e;
 }
 
-// the wide stack entries a launch uses: trace.stack_cap (tests force
-// overflows with small values), at most the arity's stack; 0 = all of it
-static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity) {
-    const uint32_t full = warity == 8 ? (uint32_t)WideFmt<8>::stack : (uint32_t)WideFmt<4>::stack;
+// the wide stack entries a launch of NT-thread blocks uses: trace.stack_cap
+// (tests force overflows with small values), at most the kernel's stack
+// (StackOf: arity and block size); 0 = all of it
+static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity, uint32_t nt) {
+    const uint32_t full = warity == 8   ? (uint32_t)StackOf<8, 256>::v
+                          : nt == 64    ? (uint32_t)StackOf<4, 64>::v
+                                        : (uint32_t)StackOf<4, 256>::v;
     return cfg.stack_cap ? min(cfg.stack_cap, full) : full;
 }
 
@@ -2111,7 +2114,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     if (warity != 4 && warity != 8) return hipErrorInvalidValue;
     if (warity == 8 && n > kWide8MaxN) return hipErrorInvalidValue;  // the build keeps 8-ary records to n <= kWide8MaxN
-    const uint32_t cap = stack_cap_for(cfg, warity);
+    const uint32_t cap = stack_cap_for(cfg, warity, 256);  // the pool's 256-thread blocks
     if (cfg.variant == 1 && wnodes && warity == 4 && n >= 2 && !binary_counts && work) {
         const uint32_t nunits = nb * 4;
         hipError_t me = hipMemsetAsync(work, 0, kPoolCounters * 128, s);
@@ -2238,7 +2241,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
     k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, spp == 1, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, \
-                             wnodes, cap, tris, n,                                                                       \
+                             wnodes, stack_cap_for(cfg, warity, NT), tris, n,                                            \
                              cam, w, h, spp, rank, nranks, tilesX, H, R, counters, (const float*)nullptr, Light{},      \
                              order, cost_out, px_prev, px_cost, coop_cap, cq, fold)
 #define RT_TRACE(C, P, WI) \
@@ -2343,7 +2346,7 @@ hipError_t launch_trace_shadow(const void* nodes, const uint4* wnodes, uint32_t 
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     if (warity != 4 && warity != 8) return hipErrorInvalidValue;
     const bool wide = wnodes && n >= 2 && cfg.variant != 2;
-    const uint32_t cap = stack_cap_for(cfg, warity);
+    const uint32_t cap = stack_cap_for(cfg, warity, 256);
 #define RT_SHADOW(C, WI, WW)                                                                                       \
     RT_KLAUNCH((k_trace<C, false, WI, 256, true, false, WW>), dim3(nb), dim3(256), 0, s, nodes, wnodes, cap, \
                        tri_s, n, cam, w, h, spp, 0u, 1u, tilesX, H, R, counters, tris, lt)
@@ -2381,8 +2384,8 @@ hipError_t launch_trace_path(const void* nodes, const uint4* wnodes, uint32_t wa
     // K7w records unless the binary traversal is asked for (variant 2)
     const uint4* wn = (cfg.variant != 2) ? wnodes : nullptr;
     if (warity != 4 && warity != 8) return hipErrorInvalidValue;
-    const uint32_t cap = stack_cap_for(cfg, warity);
     const bool small = cfg.path_wg == 64;
+    const uint32_t cap = stack_cap_for(cfg, warity, small ? 64 : 256);
 #define RT_PATH(C, NT)                                                                                                 \
     if (warity == 8)                                                                                                 \
         RT_KLAUNCH((k_path<C, NT, 8>), dim3(nb * (256 / NT)), dim3(NT), 0, s, nodes, wn, cap, tri_s, tris, n, \
@@ -2451,7 +2454,7 @@ hipError_t launch_path_wavefront(const void* nodes, const uint4* wnodes, uint32_
     const uint32_t tilesX = (w + 15) / 16;
     const uint4* wn = (cfg.variant != 2) ? wnodes : nullptr;
     if (warity != 4 && warity != 8) return hipErrorInvalidValue;
-    const uint32_t wcap = stack_cap_for(cfg, warity);
+    const uint32_t wcap = stack_cap_for(cfg, warity, 256);
     const bool w8 = warity == 8;
     const uint32_t batch = pb.cap / per_tile;
     float4* H = reinterpret_cast<float4*>(hits);

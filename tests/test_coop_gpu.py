@@ -163,3 +163,54 @@ def test_coop_headline_1m(R, oracle, cfg):
             hits, rgba, _ = s.render(cam, w, h, 1)
             assert np.array_equal(rgba, er), frame
             assert _same_hits(hits, eh), frame
+
+
+@pytest.mark.parametrize("P", [2, 3])
+@pytest.mark.parametrize("cap", [0, 14, 16, 20])
+def test_tile_stack_depths(R, oracle, cfg, P, cap):
+    """One rank's tiles run 64-thread blocks with 20-entry stacks (14 for the
+    256-thread full frames): every stack depth up to 20, through the
+    overflow hand-off and the queue (whose entries carry up to 21 pending
+    subtrees), == the oracle, on a scene of overlapping clusters."""
+    base = oracle.soup(8, 21).reshape(-1, 9)
+    tris = np.concatenate([np.repeat(base, 40, axis=0), oracle.soup(20000, 22).reshape(-1, 9) * 0.3 + 0.35,
+                           oracle.soup(20000, 23).reshape(-1, 9)])
+    tris = np.ascontiguousarray(tris, np.float32)
+    V = _soup_view()
+    w, h = 112, 80
+    eh, er = _frame(oracle, tris, V, w, h, 1)
+    cfg("render.emulate", 1, 0)
+    cfg("trace.stack_cap", cap, 0)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for frame in range(2):
+            hits, rgba, _ = s.render(cam, w, h, 1, ngpus=P)
+            assert np.array_equal(rgba, er), (P, cap, frame)
+            assert _same_hits(hits, eh), (P, cap, frame)
+
+
+def test_orbit_frame_8_ranks_1m(R, oracle, cfg):
+    """The bench's orbiting camera at step 8 (soup-1M 1080p), where a few
+    rays need more than 14 stack entries: the emulated 8-rank frame (20-entry
+    tile stacks) and the full frame (14 entries, binary hand-off) == the
+    oracle over the whole image."""
+    import bench
+    V = _soup_view()
+    tris = oracle.soup(1_000_000, 1).reshape(-1, 9)
+    w, h = 1920, 1080
+    eye = bench.orbit_view(V, 8)
+
+    class _V:
+        pass
+    view = _V()
+    view.eye, view.at, view.up, view.vfov = eye, V.at, V.up, V.vfov
+    eh, er = _frame(oracle, tris, view, w, h, 1)
+    cfg("render.emulate", 1, 0)
+    cam = R.camera_look_at(eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for P in (8, 1):
+            hits, rgba, _ = s.render(cam, w, h, 1, ngpus=P)
+            assert np.array_equal(rgba, er), P
+            assert _same_hits(hits, eh), P

@@ -44,4 +44,6 @@ for P in (2, 4, 8):
             cam = R.camera_look_at(orbit(f), V.at, V.up, V.vfov, w, h)
             ms.append(s.render_tiles_device(cam, w, h, spp, r, P, slab.data_ptr(), timed=True))
         t.append(float(np.median(ms[2:])))
+        if os.environ.get("RO_VERBOSE"):
+            print(f"  P={P} rank {r}: " + " ".join(f"{x:.4f}" for x in ms), flush=True)
     print(f"P={P}: " + " ".join(f"{x:.4f}" for x in t) + f" | max {max(t):.4f} mean {np.mean(t):.4f}", flush=True)
