@@ -136,11 +136,14 @@ struct CamF { float eye[3], w00[3], du[3], dv[3]; };
 // trace.coop_cap_tiles = -1 (the default): the step cap one rank's tiles use,
 // by rank count.  A rank of a two-way split holds twice the tiles of P = 4
 // and is partly throughput-bound, so it gains from queueing fewer rays:
-// P=2 0.213 -> 0.206 ms at 88 against 80, while P=4/8 are best at 80.
+// P=2 0.213 -> 0.206 ms at 88 against 80, while P=4 is best at 80.  With the
+// rank kernels' 20-entry stacks (r04) P=8 is best lower: 72 steps, orbit max
+// over ranks 0.1172 / 0.1182 ms against 0.1229 / 0.1218 at 80 (64: 0.1187 /
+// 0.1180; profiles/coop_cap_tiles_orbit_r04.log).
 constexpr uint32_t kCoopCapAuto = 0xFFFFFFFFu;
 inline uint32_t coop_cap_for_tiles(uint32_t knob, uint32_t nranks) {
     if (knob != kCoopCapAuto) return knob;
-    return nranks <= 2 ? 88u : 80u;
+    return nranks <= 2 ? 88u : nranks <= 4 ? 80u : 72u;
 }
 // full frames: auto = 96 steps for 1-spp frames on 256-thread tiles, whose
 // k_trace instance (SPPC = 1) has the queue at no register cost (72 VGPRs
