@@ -140,16 +140,17 @@ template <> struct WideFmt<8> {
     static constexpr int stack = 18;
 };
 // 4-ary stacks of 64-thread blocks (one rank's tiles of a multi-GPU frame):
-// 20 entries.  A ray whose stack overflows finishes in the binary traversal,
+// 16 entries.  A ray whose stack overflows finishes in the binary traversal,
 // uncapped by the heavy-ray queue, and one such ray sets its rank's time: on
 // the bench's orbit a few frames hold overflowing rays, and the rank that owns
-// their tiles took 0.19-0.25 ms against 0.12 for the others.  At 64 threads
-// the deeper stack costs no occupancy (8 KB per block: 20 blocks per CU, the
-// tile kernel's 96 VGPRs allow 5 waves per SIMD anyway); the 256-thread
-// full-frame kernels keep 14 (20 would take 6 blocks per CU to 5).
-// (profiles/ab_stack_depth_r04.log)
+// their tiles took 0.19-0.25 ms against 0.12 for the others
+// (profiles/ab_stack_depth_r04.log: 20 entries fixed it).  16 entries fix it
+// as well and leave the 1-spp tile kernel (77 VGPRs) its 6 waves per SIMD:
+// 6.4 KB per block, 24 blocks per CU (profiles/ab_tile_spp1_stack16_r04.log).
+// The 256-thread full-frame kernels keep 14 (16-24 entries cost them a block
+// per CU or more, and overflows are rare in a full frame's throughput).
 #ifndef RT_WIDE_STACK64
-#define RT_WIDE_STACK64 20
+#define RT_WIDE_STACK64 16
 #endif
 template <int W, int NT> struct StackOf {
     static constexpr int v = (W == 4 && NT == 64) ? RT_WIDE_STACK64 : WideFmt<W>::stack;

@@ -2075,6 +2075,14 @@ static uint32_t stack_cap_for(const TraceConfig& cfg, uint32_t warity, uint32_t 
 #ifndef RT_SPP1
 #define RT_SPP1 1  // 0: 1-spp full frames run the generic kernel (A/B)
 #endif
+// One rank's 1-spp tiles run the 1-spp instance too (r04): 77 VGPRs, 6 waves
+// per SIMD with the 16-entry tile stacks (RT_WIDE_STACK64).  No faster at
+// P = 4 / 8, where a rank's waves are resident at once; at P = 2 (1.6
+// rounds of waves) the orbit's max over ranks 0.2247 -> 0.2099 ms
+// (profiles/ab_tile_spp1_stack16_r04.log).  0: the generic kernel (A/B).
+#ifndef RT_SPP1_TILES
+#define RT_SPP1_TILES 1
+#endif
 template <bool C, bool P, bool WI, int NT, typename... A>
 static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t grid, hipStream_t s, A... a) {
     if constexpr (WI) {
@@ -2084,9 +2092,9 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t g
             return;
         }
         if (buf) {
-            // (one rank's tiles keep the generic kernel: its 1-spp instance, 77 VGPRs / 6 waves
-            // instead of 96 / 5, measured no faster per rank, profiles/ab_occupancy_r03.log)
-            if (cq && RT_SPP1 && !C && !P && NT == 256 && spp1)  // full frames with the queue (trace.coop_cap)
+            // (one rank's tiles: the 1-spp instance since r04, RT_SPP1_TILES; r03 measured it
+            // no faster per rank on the static camera, profiles/ab_occupancy_r03.log)
+            if (cq && RT_SPP1 && !C && (RT_SPP1_TILES ? true : !P && NT == 256) && spp1)  // full frames with the queue (trace.coop_cap)
                 RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true, 1>), dim3(grid), dim3(NT), 0, s, a...);
             else if (cq) RT_KLAUNCH((k_trace<C, P, true, NT, false, true, 4, true>), dim3(grid), dim3(NT), 0, s, a...);
             else if (RT_SPP1 && !C && !P && NT == 256 && spp1)  // the headline kernel: 1 spp full frames

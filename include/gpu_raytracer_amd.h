@@ -317,8 +317,8 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * wide (4-ary) traversal over the K7w records (default), 1 = wide traversal
  * with per-lane refill from 8x8-pixel units dealt statically to a resident
  * grid, 2 = one thread per pixel, binary traversal; "trace.blocks" variant-1
- * grid (0 = resident capacity); "trace.stack_cap" (1..20; 0 = all, the
- * default: 14 for 4-ary records on 256-thread blocks, 20 on 64-thread
+ * grid (0 = resident capacity); "trace.stack_cap" (1..18; 0 = all, the
+ * default: 14 for 4-ary records on 256-thread blocks, 16 on 64-thread
  * blocks -- one rank's tiles --, 18 for 8-ary) wide-traversal stack
  * entries -- rays that need more are re-traced by the binary traversal;
  * "build.wide_arity" 4 (default) / 8: K7w 4-ary or K7w8 8-ary trace records

@@ -252,7 +252,7 @@ def test_bvh_cache_rejects_without_device_work(rt, tmp_path):
 # restored afterwards (include/gpu_raytracer_amd.h; INTEGRATION.md "tuning").
 CONFIG_KEYS = {
     "trace.variant": ([0, 1, 2], [3, -1], 0),
-    "trace.stack_cap": ([0, 1, 14, 18, 20], [-1, 21], 0),
+    "trace.stack_cap": ([0, 1, 14, 16, 18], [-1, 19], 0),
     "trace.wg": ([64, 256], [128], 256),
     "trace.wg_tiles": ([64, 256], [32], 64),
     "trace.tile_order": ([0, 1], [2], 1),

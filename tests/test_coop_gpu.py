@@ -166,12 +166,12 @@ def test_coop_headline_1m(R, oracle, cfg):
 
 
 @pytest.mark.parametrize("P", [2, 3])
-@pytest.mark.parametrize("cap", [0, 14, 16, 20])
+@pytest.mark.parametrize("cap", [0, 14, 15, 16])
 def test_tile_stack_depths(R, oracle, cfg, P, cap):
-    """One rank's tiles run 64-thread blocks with 20-entry stacks (14 for the
-    256-thread full frames): every stack depth up to 20, through the
-    overflow hand-off and the queue (whose entries carry up to 21 pending
-    subtrees), == the oracle, on a scene of overlapping clusters."""
+    """One rank's tiles run 64-thread blocks with 16-entry stacks (14 for the
+    256-thread full frames) and the 1-spp kernel: stack depths up to 16,
+    through the overflow hand-off and the queue, == the oracle, on a scene of
+    overlapping clusters."""
     base = oracle.soup(8, 21).reshape(-1, 9)
     tris = np.concatenate([np.repeat(base, 40, axis=0), oracle.soup(20000, 22).reshape(-1, 9) * 0.3 + 0.35,
                            oracle.soup(20000, 23).reshape(-1, 9)])
@@ -192,7 +192,7 @@ def test_tile_stack_depths(R, oracle, cfg, P, cap):
 
 def test_orbit_frame_8_ranks_1m(R, oracle, cfg):
     """The bench's orbiting camera at step 8 (soup-1M 1080p), where a few
-    rays need more than 14 stack entries: the emulated 8-rank frame (20-entry
+    rays need more than 14 stack entries: the emulated 8-rank frame (16-entry
     tile stacks) and the full frame (14 entries, binary hand-off) == the
     oracle over the whole image."""
     import bench
