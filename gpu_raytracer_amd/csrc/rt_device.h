@@ -87,7 +87,10 @@ constexpr uint32_t kMsbMaxN = 512u * kSortTile;
 // and 1024-thread bucket sorts of up to 12288 keys (sort_kernels.hip); a
 // uniform soup's buckets hold n/1024 +- a few sigma keys
 constexpr uint32_t kMsbBigMaxN = 12u * 1000u * 1000u;
-constexpr int kRefitT = 512;                           // leaves per refit block
+#ifndef RT_REFIT_T
+#define RT_REFIT_T 512  // A/B builds only (tools/build_exp.sh)
+#endif
+constexpr int kRefitT = RT_REFIT_T;                     // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity
 
 // ---- K7w wide (4-ary) trace tree, derived from the binary tree after K6.
