@@ -216,7 +216,7 @@ hipError_t dev_alloc(void** p, size_t bytes);
 template <class T>
 inline hipError_t dev_alloc(T** p, size_t bytes) { return dev_alloc(reinterpret_cast<void**>(p), bytes); }
 
-constexpr uint32_t kCoopEntryBytes = 256;  // heavy-ray queue entry stride bound (trace_kernels.hip kCoopEntry x 16 B <= this)
+constexpr uint32_t kCoopEntryBytes = 208;  // heavy-ray queue entry (trace_kernels.hip kCoopEntry x 16 B: 19 pending subtrees)
 // 8-ary records are read through 32-bit buffer offsets: the last record ends
 // at (n-1) x 96 B, which must not pass 2^32 - 1 (n <= 44,739,243; above that
 // the build writes 4-ary records, whose (n-1) x 64 B fit up to n = 2^26)

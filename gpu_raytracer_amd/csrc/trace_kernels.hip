@@ -691,7 +691,7 @@ __device__ __forceinline__ uint32_t tile_pixel_order(const uint16_t* __restrict_
 constexpr uint32_t kCoopShards = 64;
 constexpr uint32_t kCoopFrontier = kWideStackMax + 1;        // pending entries a deferred ray can have (either arity)
 constexpr uint32_t kCoopEntry = 3 + (kCoopFrontier + 1) / 2;  // uint4 per queue entry
-static_assert(kCoopEntry * 16 <= kCoopEntryBytes, "rt_launch.h sizes the queue");
+static_assert(kCoopEntry * 16 == kCoopEntryBytes, "rt_launch.h sizes the queue (deeper stacks: raise kCoopEntryBytes)");
 struct CoopQ {
     uint4* q = nullptr;
     uint32_t* ctr = nullptr;       // [kCoopShards] this frame's reservation counters
