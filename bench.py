@@ -326,7 +326,56 @@ def roofline_of(kernel_bytes, trace_ms, pmc):
             "pmc_trace_kernel_us": pmc.get("trace_kernel_avg_us") if pmc else None}
 
 
-def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None):
+EMU_RANKS = (2, 4, 8)
+
+
+def rank_emulation(R, S, scene, key, torch, dev, frames=6, drop=2, ranks=EMU_RANKS, full_ms=None):
+    """EMULATED multi-GPU scaling on ONE GPU (SURVEY.md
+    §8(e)): the GPU plays each rank r < P in turn and traces only that rank's
+    image tiles (t = r mod P, rt_render_tiles_device -- the exact launch a
+    rank of `bench.py --gpus P` makes), `frames` successive frames of the
+    bench's orbiting camera per rank (the tile / pixel order maps are per
+    frame shape, so each rank warms its own; the first `drop` frames are
+    dropped), median per rank.  No RCCL gather and no concurrency between
+    ranks: this projects the trace's strong scaling only.  Reported: every
+    rank's median, max and mean over ranks, and speedup / efficiency of the
+    max-rank time against the full frame on the same cameras (`full_ms`,
+    measured here the same way unless given)."""
+    cfg = S.CONFIGS[key]
+    view = S.VIEWS[cfg.scene]
+    w, h, spp = cfg.w, cfg.h, cfg.spp
+    cams = [R.camera_look_at(orbit_view(view, i), view.at, view.up, view.vfov, w, h) for i in range(frames)]
+    if full_ms is None:
+        img = torch.zeros(w * h, dtype=torch.int32, device=dev)
+        hits = torch.empty(w * h * spp * 4, dtype=torch.float32, device=dev)
+        full = [scene.render_device(c, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+                for c in cams]
+        del img, hits
+        full_ms = float(np.median(full[drop:]))
+    out = {"emulated": True,
+           "method": f"one GPU plays each rank in turn (rt_render_tiles_device of rank r's tiles, t = r mod P), "
+                     f"{frames} orbit frames per rank, median of the last {frames - drop}; no gather, no overlap",
+           "workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{key - 1}])",
+           "full_frame_ms": round(full_ms, 4), "P": {}}
+    for P in ranks:
+        tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
+        slab = torch.zeros(max(tmax, 1) * 256, dtype=torch.int32, device=dev)
+        slab_hits = torch.empty(max(tmax, 1) * 256 * spp * 4, dtype=torch.float32, device=dev)
+        per = []
+        for r in range(P):
+            ms = [scene.render_tiles_device(c, w, h, spp, r, P, slab.data_ptr(), slab_hits.data_ptr(), timed=True)
+                  for c in cams]
+            per.append(float(np.median(ms[drop:])))
+        del slab, slab_hits
+        mx = max(per)
+        out["P"][str(P)] = {"max_ms": round(mx, 4), "mean_ms": round(float(np.mean(per)), 4),
+                            "per_rank_ms": [round(x, 4) for x in per],
+                            "speedup": round(full_ms / mx, 3), "efficiency": round(full_ms / (P * mx), 3),
+                            "mrays_per_s_projected": round(w * h * spp / (mx * 1e-3) / 1e6, 1)}
+    return out
+
+
+def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None, emulate=False):
     """One N=1 line for another BASELINE config (untimed by the step
     contract): build + full-frame trace, static camera, with its row-major
     (cold) time and the kernel's own byte rate."""
@@ -353,6 +402,8 @@ def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None):
     rays = w * h * spp
     kb = 64.0 * float(wk[0]) + 48.0 * float(wk[1]) + 16.0 * rays + 4.0 * w * h
     tr, bd = float(np.mean(t)), float(np.mean(b))
+    del img, hits
+    emu = rank_emulation(R, S, scene, key, torch, dev) if emulate else None
     scene.close()
     pmc = load_pmc(pmc_json, cfg.name, 1) if pmc_json else None
     return {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{key - 1}])", "n_tris": cfg.n,
@@ -367,6 +418,7 @@ def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None):
             # requested bytes mostly hit L2/MALL (they can exceed the HBM peak),
             # so they are priced against the aggregate L2 bandwidth
             "kernel_l2_frac": round(kb / (tr * 1e-3) / 1e9 / L2_PEAK_GBS, 4),
+            "rank_emulation": emu,
             "scene_variant": "splitmix64 soup (SURVEY.md §9.9)" if cfg.scene == "soup"
             else "procedural substitute (SURVEY.md §9.9; no asset files offline)"}
 
@@ -685,6 +737,9 @@ def main():
             out["secondary"] = secondary_rays(S, scene, cfg, cam_static, w, h, spp, img, hits, args, torch, dev,
                                               static_ms)
             out["path"] = path_tracing(S, scene, cfg, cam_static, w, h, spp, img, args, torch, dev)
+        if world == 1 and not args.no_extra:
+            out["rank_emulation"] = {f"configs[{args.config - 1}]": rank_emulation(R, S, scene, args.config, torch,
+                                                                                   dev)}
         if world == 1 and not args.no_cpu_baseline:
             # every CPU this process may run on at once: the affinity set,
             # capped by the cgroup quota (oversubscribing a quota only adds switches)
@@ -700,7 +755,11 @@ def main():
             if key == args.config:
                 continue
             try:
-                out["other_configs"][f"config{key}"] = other_config(R, S, key, torch, dev, pmc_json=args.pmc_json)
+                oc = other_config(R, S, key, torch, dev, pmc_json=args.pmc_json, emulate=key in (4, 5))
+                emu = oc.pop("rank_emulation")
+                if emu:
+                    out.setdefault("rank_emulation", {})[f"configs[{key - 1}]"] = emu
+                out["other_configs"][f"config{key}"] = oc
             except Exception as exc:  # a side measurement: never lose the headline line over it
                 out["other_configs"][f"config{key}"] = {"error": f"{type(exc).__name__}: {exc}"[:200]}
     if rank == 0:

@@ -66,7 +66,8 @@ class rt_camera(C.Structure):
 
 class rt_build_times(C.Structure):
     _fields_ = ([(k, C.c_double) for k in ("bounds", "morton", "sort", "topology", "refit", "wide", "total")] +
-                [("sort_kind", C.c_uint32), ("fused_k01", C.c_uint32)])
+                [("sort_kind", C.c_uint32), ("fused_k01", C.c_uint32), ("fused_fallback", C.c_uint32),
+                 ("lsb_redo", C.c_uint32)])
 
 
 def build_library(verbose: bool = False) -> str:

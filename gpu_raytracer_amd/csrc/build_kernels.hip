@@ -302,12 +302,27 @@ __global__ __launch_bounds__(kSortThreads) void k_morton(const float* __restrict
 // its step and then grid_open bumps the generation (and resets the count);
 // the others grid_wait for that.  The arrival's old value stays in LDS for
 // grid_wait.
+// Publication order: a workgroup-scope release emits no vmcnt
+// wait outside tgsplit mode, so the write-through stores a wave has handed
+// over could still be in flight when thread 0's arrival (or the opening
+// RMW) reaches L2 -- the last arriver on another XCD would then reduce a
+// stale partial box.  Every wave therefore drains its own vector memory
+// counter (s_waitcnt vmcnt(0): on gfx9 stores count there too, and a
+// write-through store is acknowledged once it is visible device-wide) before
+// the block's s_barrier; thread 0's RMW follows that barrier.  An agent-scope
+// release RMW would also write back the XCD's whole L2 (buffer_wbl2), which
+// is what made the fenced barrier cost ~59 us.  tests/test_isa.py checks the
+// emitted order in librtamd.so.
+__device__ __forceinline__ void drain_vm_stores() {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt/lgkmcnt untouched (max)
+}
 __device__ __forceinline__ uint32_t* grid_old_slot() {
     __shared__ uint32_t s_old;
     return &s_old;
 }
 __device__ __forceinline__ bool grid_arrive_last(uint32_t* bar, uint32_t nblocks) {
     uint32_t* s_old = grid_old_slot();
+    drain_vm_stores();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) *s_old = __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -315,6 +330,7 @@ __device__ __forceinline__ bool grid_arrive_last(uint32_t* bar, uint32_t nblocks
     return (*s_old & 0xFFFFu) == nblocks - 1;
 }
 __device__ __forceinline__ void grid_open(uint32_t* bar, uint32_t nblocks) {
+    drain_vm_stores();  // the published box is acknowledged before the generation moves
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add(bar, 0x10000u - nblocks, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

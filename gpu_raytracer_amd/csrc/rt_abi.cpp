@@ -126,6 +126,8 @@ rt_status hip_fail(hipError_t e, const char* where) {
     return fail(RT_EDEVICE, std::string(where) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")");
 }
 
+rt_status hip_status(hipError_t e, const char* where) { return e == hipSuccess ? RT_OK : hip_fail(e, where); }
+
 #define HIPR(expr)                                          \
     do {                                                    \
         hipError_t _e = (expr);                             \
@@ -410,10 +412,18 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
                                         &r->fused, r->d_flag);
         if (e != hipSuccess) return hip_fail(e, "launch_build");
     }
+    // Every replica is synchronized and checked before anything returns
+    // (an early return left later replicas' flags unread while
+    // their fused grids could still run after the gates were released).
+    rt_status first_err = RT_OK;
     double worst = 0.0;
     for (Replica* r : targets) {
         HIPR(hipSetDevice(r->device));
         HIPR(hipStreamSynchronize(r->stream));
+    }
+    // stage times of the build just synchronized; the total is what this
+    // call spent on the replica: a discarded build's time is added to its redo
+    auto read_times = [&](Replica* r, double spent_before) -> rt_status {
         float t[6] = {0, 0, 0, 0, 0, 0};
         if (stages)
             for (int i = 0; i < 6; ++i) HIPR(hipEventElapsedTime(&t[i], r->ev.e[i], r->ev.e[i + 1]));
@@ -425,25 +435,67 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         r->times.wide = t[5];
         float tot = 0;
         HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
-        r->times.total = tot;
+        r->times.total = spent_before + tot;
+        return RT_OK;
+    };
+    for (Replica* r : targets) {
+        HIPR(hipSetDevice(r->device));
+        if (rt_status st = read_times(r, 0.0); st != RT_OK) {
+            if (first_err == RT_OK) first_err = st;
+            continue;
+        }
         const uint32_t* hf = r->h_flag;  // [0] dense, [1] clustered bins, [2] bucket overflow, [5] barrier timeout
-        if (r->fused && hf[rt::kZFuseErr - rt::kZDense]) {  // a block of the fused grid gave up at the barrier
-            HIPR(hipMemset(r->bufs.zero + rt::kZFuseErr, 0, 4));
-            return fail(RT_EDEVICE, "fused bounds+Morton: grid barrier timed out (grid not co-resident)");
+        r->times.fused_fallback = 0u;
+        r->times.lsb_redo = 0u;
+        if (r->fused && hf[rt::kZFuseErr - rt::kZDense]) {
+            // A block of the fused grid gave up at the barrier: the grid was
+            // not co-resident (another tenant held CUs).  Its later kernels
+            // ran in bounds on a wrong box, so the build is discarded and
+            // redone here with the two-launch K0 + K1 (VERDICT r04 item 3;
+            // times.fused_fallback reports it).  The word lies past kZEnd
+            // (no build zeroes it), so it is cleared first.
+            if (rt_status st = hip_status(hipMemsetAsync(r->bufs.zero + rt::kZFuseErr, 0, 4, r->stream),
+                                          "clear barrier flag");
+                st != RT_OK) {
+                if (first_err == RT_OK) first_err = st;
+                continue;
+            }
+            const double spent = r->times.total;
+            for (int i = 0; i < 8; ++i) r->h_flag[i] = 0;
+            hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, &r->msb_probe, false,
+                                            &r->fused, r->d_flag);
+            if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+            if (e != hipSuccess) {
+                if (first_err == RT_OK) first_err = hip_fail(e, "launch_build (unfused redo)");
+                continue;
+            }
+            if (rt_status st = read_times(r, spent); st != RT_OK) {
+                if (first_err == RT_OK) first_err = st;
+                continue;
+            }
+            r->times.fused_fallback = 1u;
         }
         const uint32_t kind = rt::build_sort_kind(r->bufs, s->n, cfg);
-        if (kind == 2 && hf[rt::kZGatherFlags + 1 - rt::kZDense]) {
+        if (kind == 2 && (hf[rt::kZGatherFlags + 1 - rt::kZDense] || cfg.force_lsb_redo)) {
             // a bucket outgrew its block's LDS (the verdict should have sent
             // this scene to the LSB sort): that bucket is unsorted -- keep
             // the LSB sort for this scene and build again with it
+            // (debug.force_lsb_redo takes this branch for the tests)
             r->bufs.sort_mode = 2;
             r->bufs.sort_mode_of = kind;
             r->msb_probe = 0;
+            const double spent = r->times.total;
             hipError_t e = rt::launch_build(r->bufs, s->n, r->stream, &r->ev, stages, cfg, nullptr, false, &r->fused);
-            if (e != hipSuccess) return hip_fail(e, "launch_build (LSB)");
-            HIPR(hipStreamSynchronize(r->stream));
-            HIPR(hipEventElapsedTime(&tot, r->ev.e[0], r->ev.e[6]));
-            r->times.total = tot;
+            if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+            if (e != hipSuccess) {
+                if (first_err == RT_OK) first_err = hip_fail(e, "launch_build (LSB)");
+                continue;
+            }
+            if (rt_status st = read_times(r, spent); st != RT_OK) {
+                if (first_err == RT_OK) first_err = st;
+                continue;
+            }
+            r->times.lsb_redo = 1u;
         } else if (r->msb_probe) {  // the scene's first build with this sort ran both sorts gated on its verdict
             const bool lsb = hf[0] != 0 || (r->msb_probe == 2 && hf[rt::kZGatherFlags - rt::kZDense] != 0);
             r->bufs.sort_mode = lsb ? 2u : 1u;
@@ -453,8 +505,9 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         r->times.sort_kind = rt::build_sort_kind(r->bufs, s->n, cfg);
         r->times.fused_k01 = r->fused ? 1u : 0u;
         r->built = true;
-        worst = std::max(worst, (double)tot);
+        worst = std::max(worst, r->times.total);
     }
+    if (first_err != RT_OK) return first_err;
     if (ms_out) *ms_out = worst;
     return RT_OK;
 }
@@ -581,6 +634,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
     else if (k == "debug.poison" && (value == 0 || value == 1)) c.poison = (uint32_t)value;
     else if (k == "debug.lds_scribble" && (value == 0 || value == 1)) c.lds_scribble = (uint32_t)value;
+    else if (k == "debug.force_lsb_redo" && (value == 0 || value == 1)) c.force_lsb_redo = (uint32_t)value;
     else return false;
     return true;
 }
@@ -590,7 +644,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
-const char* rt_version(void) { return "gpu_raytracer_amd 0.2 (gfx950)"; }
+const char* rt_version(void) { return "gpu_raytracer_amd 0.3 (gfx950)"; }
 
 rt_status rt_config_set(const char* key, int64_t value) {
     if (!key) return fail(RT_EINVAL, "null key");

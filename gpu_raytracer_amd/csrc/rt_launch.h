@@ -197,6 +197,8 @@ struct TraceConfig {
     uint32_t lds_scribble = 0;    // debug.lds_scribble: before every kernel launch, fill the LDS of the
                                   // CUs with a fresh pseudo-random pattern, so a kernel that reads LDS
                                   // it did not write gives a different (wrong) result every launch
+    uint32_t force_lsb_redo = 0;  // debug.force_lsb_redo: treat every gather-sort build as if a bucket
+                                  // had overflowed (tests the host's discard-and-redo branch)
 };
 // Both debug knobs also start on from the environment (RT_DEBUG_POISON=1,
 // RT_DEBUG_LDS_SCRIBBLE=1), so a whole test suite can run under them.

@@ -49,6 +49,8 @@ class BuildTimes:
     total: float
     sort_kind: int = 2   # 0 LSB, 1 MSB, 2 tile-bucketed gather (the sort later builds use)
     fused_k01: int = 0   # the last build ran K0 + K1 as one launch
+    fused_fallback: int = 0  # its fused barrier gave up and the build was redone with two launches
+    lsb_redo: int = 0    # a gather bucket overflowed and the build was redone with the LSB sort
 
 
 class Scene:
@@ -146,7 +148,8 @@ class Scene:
     def build_times(self) -> BuildTimes:
         t = rt_build_times()
         call("rt_bvh_build_times", self._h, C.byref(t))
-        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total, t.sort_kind, t.fused_k01)
+        return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total, t.sort_kind, t.fused_k01,
+                          t.fused_fallback, t.lsb_redo)
 
     @property
     def wide_arity(self) -> int:

@@ -76,10 +76,15 @@ typedef enum {
  * sort_kind: the sort this scene's builds use after the last one (its
  * verdict applied): 0 the 4-pass LSB radix sort, 1 MSB scatter + bucket
  * sort, 2 the tile-bucketed gather sort; fused_k01: the last build ran
- * K0 + K1 as one launch (build.fuse_k01). */
+ * K0 + K1 as one launch (build.fuse_k01).  fused_fallback: the fused
+ * launch's grid barrier gave up (its grid was not co-resident) and the build
+ * was redone with two launches; lsb_redo: a gather-sort bucket overflowed and
+ * the build was redone with the LSB sort.  After a redo the stage fields are
+ * the redo's and `total` is both builds together.  (Layout of rt_version 0.3:
+ * 0.2 had neither redo field.) */
 typedef struct {
     double bounds, morton, sort, topology, refit, wide, total;
-    uint32_t sort_kind, fused_k01;
+    uint32_t sort_kind, fused_k01, fused_fallback, lsb_redo;
 } rt_build_times;
 
 /* ---- scene ingest (SURVEY.md §8(b) rt_scene_load_obj / rt_scene_from_soup) ---- */
