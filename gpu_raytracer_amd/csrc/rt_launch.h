@@ -161,6 +161,8 @@ struct TraceConfig {
     uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
     uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
     uint32_t wg_tiles = 64;     // same, for one rank's tiles of a multi-GPU frame (nranks > 1)
+    uint32_t spp_lanes = 1;     // samples in lanes (k_trace_sl) for 2..16 (power of two) spp: 1 = one rank's
+                                // tiles (default), 2 = full frames too, 0 = off (a lane loops over its samples)
     uint32_t stack_cap = 0;     // wide stack entries used (tests force the overflow path); 0 = the arity's
                                 // whole stack (14 entries for 4-ary records, 18 for 8-ary)
     uint32_t path_wave = 1;     // path mode: 0 megakernel, 1 wavefront (default: faster on soup-1M and Sponza)

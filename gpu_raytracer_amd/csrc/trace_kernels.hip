@@ -1042,6 +1042,123 @@ __global__ __launch_bounds__(1024) void k_tile_order(uint32_t* __restrict__ cost
     tile_order_block<1024, kOrderPerThread>(cost, nb, order, s_hist, s_sum, ema);
 }
 
+// ------------------------------------------------------- samples in lanes
+// trace.spp_lanes (r05, DESIGN.md (e) "Samples in lanes for one rank's
+// tiles"): a multi-spp frame whose S = spp samples per pixel (a power of two,
+// 2..16) are traced by S adjacent lanes at once -- one ray per lane, and a
+// wave (a unit) holds the S samples of 64/S pixels of a compact block of its
+// tile (8x4 pixels at 2 spp, 4x4 at 4, 4x2 at 8, 2x2 at 16).  A tile is 4S units.  The loop kernel (k_trace, a lane runs its
+// pixel's samples one after the other) makes the costliest pixel's S
+// dependent traversals one lane's chain: a rank of an 8-GPU 10M 4Kx4 frame
+// ran 1.2-1.3 ms against a 0.6-ms share (r05: max-rank efficiency 0.45 with
+// the queue off, 0.30 with it).  Here the longest chain is one ray, capped by
+// the heavy-ray queue like a 1-spp frame's.  The colour is the same ordered
+// sum as the loop's, r = ((0 + c_0) + c_1) + ..., taken over the pixel's
+// lanes with shuffles, then q8(r * (1/spp)): bit-identical images and hits.
+// A sample that the queue takes is finished by k_trace_coop (one ray:
+// kCoopOne) and its pixel's colour by k_coop_resolve from the hits of all
+// its samples; the rest of the wave never waits for it.
+constexpr uint32_t kCoopOne = 0x80000000u;  // queue entry's sample word: this sample only (samples in lanes)
+
+template <int S>
+struct SlShape {
+    // (32 / 64 samples would spill in the colour sum's shuffles: the loop kernel keeps them)
+    static_assert(S >= 2 && S <= 16 && (S & (S - 1)) == 0, "2..16 samples, a power of two");
+    static constexpr uint32_t PW = 64 / S;                                          // pixels per unit
+    static constexpr uint32_t TW = S == 2 ? 8 : S <= 8 ? 4 : 2;                    // block width
+    static constexpr uint32_t TH = PW / TW, TPR = 16 / TW, UPT = 256 / PW;          // rows, blocks per row, units per tile
+};
+
+template <bool PACKED, int NT, int S>
+__global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __restrict__ nodes,
+                                                                 const uint4* __restrict__ wnodes, uint32_t wcap,
+                                                                 const float4* __restrict__ tri_s, uint32_t n,
+                                                                 Cam cam, uint32_t W, uint32_t H, uint32_t rank,
+                                                                 uint32_t nranks, uint32_t tilesX,
+                                                                 float4* __restrict__ hits, uint32_t* __restrict__ rgba,
+                                                                 const uint32_t* __restrict__ order,
+                                                                 uint32_t* __restrict__ cost_out, uint32_t coop_cap,
+                                                                 CoopQ cq) {
+    using SH = SlShape<S>;
+    constexpr uint32_t kStackWords = (StackOf<4, NT>::v + 1) * NT;
+    __shared__ uint32_t s_ref[kStackWords];
+    __shared__ uint16_t s_tn[kStackWords];
+    const uint32_t gw = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);  // global unit (wave) id
+    const uint32_t ti = gw / SH::UPT, q = gw % SH::UPT;
+    const uint32_t slot = order ? order[ti] : ti;
+    const uint32_t t = rank + slot * nranks;
+    const uint32_t tx = t % tilesX, ty = t / tilesX;
+    const uint32_t l = threadIdx.x & 63, p = l / S, smp = l % S;
+    const uint32_t lx = (q % SH::TPR) * SH::TW + p % SH::TW, ly = (q / SH::TPR) * SH::TH + p / SH::TW;
+    const uint32_t x = tx * 16 + lx, y = ty * 16 + ly;
+    const bool valid = x < W && y < H;
+    const uint32_t pi = PACKED ? slot * 256 + ly * 16 + lx : y * W + x;
+    const unsigned long long wt0 = cost_out ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
+    bool deferred = false;
+    if (valid) {
+        const uint32_t sidx = (y * W + x) * S + smp;
+        float jx = 0.5f, jy = 0.5f;
+        if (smp > 0) {
+            const uint32_t h = pcg_hash(sidx);
+            jx = (float)(h >> 8) * 0x1p-24f;
+            jy = (float)(pcg_hash(h) >> 8) * 0x1p-24f;
+        }
+        const float px = (float)x + jx, py = (float)y + jy;
+        float d[3];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) d[c] = (cam.w00[c] + px * cam.du[c]) + py * cam.dv[c];
+        WRay R;
+        wray_init(cam.eye, d, R, scene_box(nodes));
+        int st = R.fin ? 0 : 2;
+        uint32_t cn = 0, ct = 0, qslot = 0;
+        const WideMem M = wide_mem<4>(wnodes, tri_s, n);
+        while (st == 0) {
+            st = wide_step<false, NT, false, PACKED, true, 4>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
+                                                            s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct, false, &M);
+            if (coop_cap != 0 && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
+        }
+        if (st == 3) {  // heavy: k_trace_coop finishes this sample, k_coop_resolve its pixel
+            coop_store<NT>(cq, qslot, x, y, smp | kCoopOne, pi, 0.0f, 0.0f, 0.0f, R, s_ref + threadIdx.x,
+                           s_tn + threadIdx.x);
+            deferred = true;
+        } else {
+            if (st == 2) {
+                if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
+                trace_ray_from<false>(reinterpret_cast<const char*>(nodes), tri_s, n, cam.eye, d,
+                                      R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1), R.tb, R.hu, R.hv, R.hp, cn,
+                                      ct);
+            }
+            if (hits) hits[(uint64_t)pi * S + smp] = make_float4(R.tb, R.hu, R.hv, __uint_as_float(R.hp));
+            if (R.hp != RT_SENT) {
+                cr = R.hu;
+                cg = R.hv;
+                cb = (1.0f - R.hu) - R.hv;
+            }
+        }
+    }
+    // the pixel's colour: the loop's ordered sum over its S lanes (every lane
+    // of the wave takes part in the shuffles)
+    const uint64_t dm = __ballot(deferred);
+    const uint32_t base = p * S;
+    float r = 0.0f, g = 0.0f, b = 0.0f;
+#pragma unroll
+    for (int k = 0; k < S; ++k) {
+        r = r + __uint_as_float((uint32_t)__shfl((int)__float_as_uint(cr), (int)(base + k), 64));
+        g = g + __uint_as_float((uint32_t)__shfl((int)__float_as_uint(cg), (int)(base + k), 64));
+        b = b + __uint_as_float((uint32_t)__shfl((int)__float_as_uint(cb), (int)(base + k), 64));
+    }
+    const uint64_t pm = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << base;
+    if (valid && smp == 0 && !(dm & pm) && rgba) {
+        const float sc = 1.0f / (float)S;
+        rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+    }
+    if (cost_out && l == 0) {  // this unit's duration -> its tile's cost map entry (the tile order's key)
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
+        atomicMax(&cost_out[slot], (uint32_t)min(dt, 0xFFFFFFFFull));
+    }
+}
+
 // ------------------------------------------------------ cooperative heavy rays
 // DESIGN.md "Cooperative heavy rays".  A group of G lanes (16, 32 or 64:
 // trace.coop_lanes) traces one queued ray: a frame's (or one rank's
@@ -1331,8 +1448,12 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
         const uint4* ent = cq.q + (uint64_t)slot * kCoopEntry;
         const uint4 a = ent[0], b = ent[1];
         const uint32_t x = a.x, y = a.y, pi = a.w;
+        // kCoopOne (samples in lanes): this sample only; its pixel's colour is
+        // k_coop_resolve's.  Else the pixel from this sample on.
+        const bool one = (a.z & kCoopOne) != 0u;
+        const uint32_t s0 = a.z & ~kCoopOne, s1 = one ? s0 + 1 : spp;
         float r = __uint_as_float(b.x), g = __uint_as_float(b.y), bl = __uint_as_float(b.z);
-        for (uint32_t s = a.z; s < spp; ++s) {
+        for (uint32_t s = s0; s < s1; ++s) {
             const uint32_t sidx = (y * W + x) * spp + s;
             float jx = 0.5f, jy = 0.5f;
             if (s > 0) {
@@ -1347,7 +1468,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
             float tb, hu, hv;
             uint32_t hp;
             coop_trace<COUNT, G, WA>(reinterpret_cast<const char*>(nodes), wnodes, tri_s, n, cam.eye, d, s_l[grp],
-                                 s == a.z ? ent : nullptr, tb, hu, hv, hp, cn, ct);
+                                 s == s0 ? ent : nullptr, tb, hu, hv, hp, cn, ct);
             if (hits && gl == 0) hits[(uint64_t)pi * spp + s] = make_float4(tb, hu, hv, __uint_as_float(hp));
             if (hp != RT_SENT) {
                 r = r + hu;
@@ -1357,7 +1478,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                 r = r + 0.0f; g = g + 0.0f; bl = bl + 0.0f;
             }
         }
-        if (rgba && gl == 0) {
+        if (rgba && gl == 0 && !one) {
             const float sc = 1.0f / (float)spp;
             rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(bl * sc) << 16) | (255u << 24);
         }
@@ -1376,6 +1497,52 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     }
 }
 
+// Samples in lanes: the colour of every pixel with a queued sample, from the
+// hits of all its samples (k_trace_sl wrote the others, k_trace_coop the
+// queued ones), as the loop's ordered sum.  One thread per queue entry; a
+// pixel with several queued samples is written once per entry, with the same
+// value.  After k_trace_coop on the same stream, so every hit is in place.
+__global__ __launch_bounds__(256) void k_coop_resolve(CoopQ cq, uint32_t spp, const float4* __restrict__ hits,
+                                                      uint32_t* __restrict__ rgba) {
+    __shared__ uint32_t s_excl[kCoopShards], s_len[kCoopShards];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t len = min(cq.ctr[lane], cq.cap);
+    uint32_t incl = len;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= (uint32_t)o) incl += y;
+    }
+    if (threadIdx.x < 64) {
+        s_excl[lane] = incl - len;
+        s_len[lane] = len;
+    }
+    __syncthreads();
+    const uint32_t cnt = s_excl[63] + s_len[63];
+    for (uint32_t e = blockIdx.x * 256 + threadIdx.x; e < cnt; e += gridDim.x * 256) {
+        uint32_t sh = 0, sbase = 0;
+        for (uint32_t k = 0; k < 64; ++k) {
+            const uint32_t ek = s_excl[k];
+            if (s_len[k] > 0 && ek <= e) { sh = k; sbase = ek; }
+        }
+        const uint4 a = cq.q[(uint64_t)(sh * cq.cap + (e - sbase)) * kCoopEntry];
+        if (!(a.z & kCoopOne)) continue;
+        const uint32_t pi = a.w;
+        float r = 0.0f, g = 0.0f, b = 0.0f;
+        for (uint32_t s = 0; s < spp; ++s) {
+            const float4 h = hits[(uint64_t)pi * spp + s];
+            if (__float_as_uint(h.w) != RT_SENT) {
+                r = r + h.y;
+                g = g + h.z;
+                b = b + ((1.0f - h.y) - h.z);
+            } else {
+                r = r + 0.0f; g = g + 0.0f; b = b + 0.0f;
+            }
+        }
+        const float sc = 1.0f / (float)spp;
+        rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+    }
+}
 
 // ---------------------------------------------------------------- path mode
 // Path mode [SPEC, DESIGN.md "Path mode"; SURVEY.md §8(f) row 3]: per
@@ -2171,12 +2338,21 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // next frame's order is sorted by an extra block of this launch
     // (OrderFold) instead of a k_tile_order launch ahead of it
     // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
-    const uint32_t coop_cap =
+    const uint32_t coop_cap0 =
         wide && sched && sched->coop_q && n <= kBufMaxN
             ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : coop_cap_for_frame(cfg.coop_cap, spp, small))
             : 0u;
+    // samples in lanes (k_trace_sl): multi-spp tiles by default (trace.spp_lanes = 1), full frames too at 2
+    const bool sl = spp >= 2 && spp <= 16 && (spp & (spp - 1)) == 0 && wide && warity == 4 && !counters &&
+                    n <= kBufMaxN && cfg.buf_loads &&
+                    (cfg.spp_lanes == 2 || (cfg.spp_lanes == 1 && (packed || nranks > 1)));
+    // its queue needs the hits of every sample (k_coop_resolve), so no queue without a hits buffer
+    const uint32_t sl_cap = !sl || !hits || !sched || !sched->coop_q ? 0u
+                            : (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks)
+                                          : coop_cap_for_frame(cfg.coop_cap, 1, false));
+    const uint32_t coop_cap = sl ? sl_cap : coop_cap0;
     const bool can_fold = RT_ORDER_FOLD && sched && nranks == 1 && !packed && !small && wide && !counters &&
-                          !cfg.order_override && coop_cap == 0 && nb <= 256 * kFoldPerThread;
+                          !cfg.order_override && coop_cap == 0 && nb <= 256 * kFoldPerThread && !sl;
     OrderFold fold;
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
@@ -2223,7 +2399,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // different cost together and cost 3 % (0.372 vs 0.383 ms,
     // profiles/ab_moving_r02.log), so after a camera change the frame keeps
     // the quadrant layout and only records its costs for the next one.
-    if (cost_out && !small && sched->px_cur &&
+    if (cost_out && !small && !sl && sched->px_cur &&
         (cfg.px_sort == 2 || (cfg.px_sort == 1 && nranks == 1))) {
         const bool same_cam = sched->prev_cam_valid && std::memcmp(&sched->prev_cam, &c, sizeof(CamF)) == 0;
         if (sched->have_prev && same_cam) px_prev = sched->px_prev;
@@ -2260,7 +2436,28 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     } else {                       \
         RT_TRACE(C, P, false);     \
     }
-    if (counters) {
+    if (sl) {
+        const uint32_t nt = small ? 64u : 256u;
+        const uint32_t grid = (uint32_t)((uint64_t)nb * 4 * spp / (nt / 64));
+        const uint32_t wc = stack_cap_for(cfg, 4, nt);
+#define RT_SL(P, NT, S_)                                                                                           \
+    RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
+               nranks, tilesX, H, R, order, cost_out, coop_cap, cq)
+#define RT_SL_S(P, NT)                  \
+    switch (spp) {                      \
+        case 2: RT_SL(P, NT, 2); break;   \
+        case 4: RT_SL(P, NT, 4); break;   \
+        case 8: RT_SL(P, NT, 8); break;   \
+        default: RT_SL(P, NT, 16); break; \
+    }
+        if (packed) {
+            if (small) { RT_SL_S(true, 64); } else { RT_SL_S(true, 256); }
+        } else {
+            if (small) { RT_SL_S(false, 64); } else { RT_SL_S(false, 256); }
+        }
+#undef RT_SL_S
+#undef RT_SL
+    } else if (counters) {
         if (packed) { RT_TRACE_W(true, true); } else { RT_TRACE_W(true, false); }
     } else {
         if (packed) { RT_TRACE_W(false, true); } else { RT_TRACE_W(false, false); }
@@ -2329,6 +2526,11 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         }
 #undef RT_COOP
 #undef RT_COOP_G
+        if (sl) {  // the colours of the pixels with a queued sample
+            hipError_t le2 = hipGetLastError();
+            if (le2 != hipSuccess) return le2;
+            RT_KLAUNCH(k_coop_resolve, dim3(64), dim3(256), 0, s, cq, spp, H, R);
+        }
         sched->coop_par ^= 1u;
         if (ord) sched->order_ready = true;
     }

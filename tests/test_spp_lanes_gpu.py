@@ -1,0 +1,177 @@
+"""Samples in lanes (trace.spp_lanes, k_trace_sl; DESIGN.md (e) "Samples in
+lanes for one rank's tiles"): at 2/4/8/16 spp a pixel's samples are traced
+by adjacent lanes, one ray each, and its colour is the loop's ordered sum
+over them (shuffles); a sample the heavy-ray queue takes is finished by
+k_trace_coop alone (kCoopOne) and its pixel's colour by k_coop_resolve from
+the hits.  Every frame must equal the CPU oracle bit for bit -- hits and
+RGBA -- across the queue caps (many queued samples, several per pixel), a
+full or tiny queue, no hits buffer (queue off), forced stack overflows
+(binary hand-off), odd frame sizes, successive frames (tile order), the
+per-rank tiles (default) and full frames (spp_lanes = 2)."""
+import numpy as np
+import pytest
+
+from conftest import bits
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def R(rt):
+    if rt.device_count() < 1:
+        pytest.fail("no GPU visible to librtamd")
+    return rt
+
+
+@pytest.fixture()
+def cfg(R):
+    keys = []
+
+    def set_(k, v, default):
+        keys.append((k, default))
+        R.config_set(k, v)
+    yield set_
+    for k, d in reversed(keys):
+        R.config_set(k, d)
+
+
+def _view():
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    return SOUP_VIEW
+
+
+def _frame(oracle, tris, w, h, spp):
+    V = _view()
+    exp = oracle.build(tris)
+    cam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    eh, _ = oracle.trace(exp["nodes"], tris, cam, w, h, spp)
+    return eh, oracle.shade(eh, w, h, spp)
+
+
+def _cam(R, w, h):
+    V = _view()
+    return R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+
+
+def _same_hits(a, b):
+    return all(np.array_equal(bits(a[k]), bits(b[k])) for k in ("t", "u", "v", "prim"))
+
+
+@pytest.fixture(scope="module")
+def scene30k(oracle):
+    return oracle.soup(30000, 21).reshape(-1, 9)
+
+
+@pytest.mark.parametrize("spp", [2, 4, 8, 16])
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("cap", [0, 1, 6])
+def test_spp_lanes_tiles(R, oracle, cfg, scene30k, spp, P, cap):
+    """Emulated P-rank frames through k_trace_sl: queue off (cap 0), every
+    sample queued after 1 step (most pixels resolved from hits), and a cap
+    that queues a fraction; two successive frames (tile order on)."""
+    w, h = 70, 45
+    eh, er = _frame(oracle, scene30k, w, h, spp)
+    cfg("render.emulate", 1, 0)
+    cfg("trace.coop_cap_tiles", cap, -1)
+    with R.Scene.from_soup(scene30k) as s:
+        s.build()
+        for frame in range(2):
+            hits, rgba, _ = s.render(_cam(R, w, h), w, h, spp, ngpus=P)
+            assert np.array_equal(rgba, er), (spp, P, cap, frame)
+            assert _same_hits(hits, eh), (spp, P, cap, frame)
+
+
+@pytest.mark.parametrize("qmax", [1, 9, 200])
+def test_spp_lanes_queue_capacity(R, oracle, cfg, scene30k, qmax):
+    """A queue that fills: the samples that find their shard full trace on
+    in their own lane, the others are resolved."""
+    w, h, spp, P = 90, 50, 4, 3
+    eh, er = _frame(oracle, scene30k, w, h, spp)
+    cfg("render.emulate", 1, 0)
+    cfg("trace.coop_cap_tiles", 2, -1)
+    cfg("trace.coop_max", qmax, 65536)
+    with R.Scene.from_soup(scene30k) as s:
+        s.build()
+        hits, rgba, _ = s.render(_cam(R, w, h), w, h, spp, ngpus=P)
+        assert np.array_equal(rgba, er), qmax
+        assert _same_hits(hits, eh), qmax
+
+
+def test_spp_lanes_rgba_only(R, oracle, cfg, scene30k):
+    """No hits buffer: the queue needs the hits to resolve, so it is off and
+    every sample finishes in its lane -- the image still equals the oracle."""
+    w, h, spp = 64, 40, 4
+    _, er = _frame(oracle, scene30k, w, h, spp)
+    cfg("render.emulate", 1, 0)
+    cfg("trace.coop_cap_tiles", 1, -1)
+    with R.Scene.from_soup(scene30k) as s:
+        s.build()
+        for P in (2, 8):
+            hits, rgba, _ = s.render(_cam(R, w, h), w, h, spp, hits=False, ngpus=P)
+            assert hits is None
+            assert np.array_equal(rgba, er), P
+
+
+@pytest.mark.parametrize("stack", [1, 3])
+def test_spp_lanes_stack_overflow(R, oracle, cfg, scene30k, stack):
+    """Stack caps 1/3 send most rays through the binary hand-off, with and
+    without the queue in front of it."""
+    w, h, spp = 60, 44, 8
+    eh, er = _frame(oracle, scene30k, w, h, spp)
+    cfg("render.emulate", 1, 0)
+    cfg("trace.stack_cap", stack, 0)
+    with R.Scene.from_soup(scene30k) as s:
+        s.build()
+        for cap in (0, 4):
+            R.config_set("trace.coop_cap_tiles", cap)
+            hits, rgba, _ = s.render(_cam(R, w, h), w, h, spp, ngpus=3)
+            assert np.array_equal(rgba, er), (stack, cap)
+            assert _same_hits(hits, eh), (stack, cap)
+        R.config_set("trace.coop_cap_tiles", -1)
+
+
+@pytest.mark.parametrize("spp", [2, 4, 16])
+@pytest.mark.parametrize("cap", [0, 3])
+@pytest.mark.parametrize("wg", [64, 256])
+def test_spp_lanes_full_frames(R, oracle, cfg, scene30k, spp, cap, wg):
+    """trace.spp_lanes = 2: full frames too (256- and 64-thread blocks), with
+    and without the queue; odd frame size; three frames."""
+    w, h = 77, 41
+    eh, er = _frame(oracle, scene30k, w, h, spp)
+    cfg("trace.spp_lanes", 2, 1)
+    cfg("trace.coop_cap", cap, -1)
+    cfg("trace.wg", wg, 256)
+    with R.Scene.from_soup(scene30k) as s:
+        s.build()
+        for frame in range(3):
+            hits, rgba, _ = s.render(_cam(R, w, h), w, h, spp)
+            assert np.array_equal(rgba, er), (spp, cap, wg, frame)
+            assert _same_hits(hits, eh), (spp, cap, wg, frame)
+
+
+def test_spp_lanes_equals_loop_kernel(R, cfg):
+    """The same frame of a 300K soup through k_trace_sl and through the loop
+    kernel (spp_lanes = 0), per rank at P = 8 and in full: identical slabs,
+    hits and images (no oracle: a device-only comparison at a larger size)."""
+    import torch
+    w, h, spp, P = 480, 270, 4, 8
+    cam = _cam(R, w, h)
+    with R.Scene.generate_soup(300_000, 3) as s:
+        s.build()
+        outs = {}
+        for mode in (0, 1):
+            R.config_set("trace.spp_lanes", mode)
+            got = []
+            for r in range(P):
+                nb = R.tiles_for_rank(w, h, r, P)
+                slab = torch.zeros(nb * 256, dtype=torch.int32, device="cuda")
+                sh = torch.zeros(nb * 256 * spp * 4, dtype=torch.float32, device="cuda")
+                for _ in range(2):
+                    s.render_tiles_device(cam, w, h, spp, r, P, slab.data_ptr(), sh.data_ptr())
+                torch.cuda.synchronize()
+                got.append((slab.cpu().numpy().copy(), sh.cpu().numpy().view(np.uint32).copy()))
+            outs[mode] = got
+        R.config_set("trace.spp_lanes", 1)
+        for r in range(P):
+            assert np.array_equal(outs[0][r][0], outs[1][r][0]), r
+            assert np.array_equal(outs[0][r][1], outs[1][r][1]), r
