@@ -153,6 +153,13 @@ inline uint32_t coop_cap_for_frame(uint32_t knob, uint32_t spp, bool small) {
     if (knob != kCoopCapAuto) return knob;
     return spp == 1 && !small ? 96u : 0u;
 }
+// samples in lanes (k_trace_sl, one ray per lane): auto = no queue.  r05,
+// bench orbit (tools/rank_emul.py, profiles/ab_sl_coop_cap_r05.log): the
+// queue's group pass costs more than the single-ray tail it removes -- soup-10M
+// 4Kx4 full frame 3.98 ms off / 4.09 at 160 / 4.16 at 96, P=8 max rank 0.607 /
+// 0.632 at 128 / 0.77 at 72 / 0.81 at 48; Sponza substitute 16 spp full 1.97 /
+// 1.97 / 1.94, P=8 0.256 / 0.262 / 0.277 ms.
+inline uint32_t coop_cap_for_sl(uint32_t knob) { return knob == kCoopCapAuto ? 0u : knob; }
 
 // Trace kernel selection / tuning (rt_config_set); every setting gives
 // bit-identical hits and images.
@@ -161,8 +168,10 @@ struct TraceConfig {
     uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
     uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
     uint32_t wg_tiles = 64;     // same, for one rank's tiles of a multi-GPU frame (nranks > 1)
-    uint32_t spp_lanes = 1;     // samples in lanes (k_trace_sl) for 2..16 (power of two) spp: 1 = one rank's
-                                // tiles (default), 2 = full frames too, 0 = off (a lane loops over its samples)
+    uint32_t nt_hits = 1;       // nontemporal hit-record stores: 1 = frames of >= 2 spp (default), 2 = always,
+                                // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged)
+    uint32_t spp_lanes = 2;     // samples in lanes (k_trace_sl) for 2..16 (power of two) spp: 2 = full frames and
+                                // one rank's tiles (default), 1 = tiles only, 0 = off (a lane loops over its samples)
     uint32_t stack_cap = 0;     // wide stack entries used (tests force the overflow path); 0 = the arity's
                                 // whole stack (14 entries for 4-ary records, 18 for 8-ary)
     uint32_t path_wave = 1;     // path mode: 0 megakernel, 1 wavefront (default: faster on soup-1M and Sponza)

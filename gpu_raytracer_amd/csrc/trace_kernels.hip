@@ -550,6 +550,21 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// A hit record store.  nt (trace.nt_hits): nontemporal -- a multi-spp
+// frame's hit records (530 MB at 4Kx4 or 1080p x 16) stream to HBM while the
+// trace, which uses a few % of HBM bandwidth, runs, instead of staying dirty
+// in L2 / the MALL until the next build's soup read evicts them (DESIGN.md
+// "(d)", the 10M K0 read floor).
+typedef float rt_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_hit(float4* p, float4 v, uint32_t nt) {
+    if (nt) {
+        const rt_f4 x = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(x, reinterpret_cast<rt_f4*>(p));
+    } else {
+        *p = v;
+    }
+}
+
 __device__ __forceinline__ uint32_t q8(float x) { return (uint32_t)fminf(fmaxf(x * 255.0f + 0.5f, 0.0f), 255.0f); }
 
 // Shading frame of a hit (shadow and path modes): P = o + t d,
@@ -866,7 +881,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                const uint16_t* __restrict__ px_prev = nullptr,
                                                uint16_t* __restrict__ px_cost = nullptr,
                                                uint32_t coop_cap = 0, CoopQ cq = CoopQ{},
-                                               OrderFold fold = OrderFold{}) {
+                                               OrderFold fold = OrderFold{}, uint32_t nt_hits = 0) {
     // PX: the per-pixel order (below); its ranking borrows s_ref, so the
     // binary instance (no stack) still sizes s_ref for tile_pixel_order
     constexpr bool PX = !SHADOW && !COUNT && NT == 256;
@@ -966,7 +981,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             }
             if (hits) {
                 const uint64_t hi = PACKED ? ((uint64_t)slot * 256 + ly * 16 + lx) * spp + s : (uint64_t)sidx;
-                hits[hi] = make_float4(tb, hu, hv, __uint_as_float(hp));
+                store_hit(hits + hi, make_float4(tb, hu, hv, __uint_as_float(hp)), nt_hits);
             }
             if (SHADOW) {
                 float f = 0.0f;
@@ -1078,7 +1093,7 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
                                                                  float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                                  const uint32_t* __restrict__ order,
                                                                  uint32_t* __restrict__ cost_out, uint32_t coop_cap,
-                                                                 CoopQ cq) {
+                                                                 CoopQ cq, uint32_t nt_hits) {
     using SH = SlShape<S>;
     constexpr uint32_t kStackWords = (StackOf<4, NT>::v + 1) * NT;
     __shared__ uint32_t s_ref[kStackWords];
@@ -1129,7 +1144,7 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
                                       R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1), R.tb, R.hu, R.hv, R.hp, cn,
                                       ct);
             }
-            if (hits) hits[(uint64_t)pi * S + smp] = make_float4(R.tb, R.hu, R.hv, __uint_as_float(R.hp));
+            if (hits) store_hit(hits + (uint64_t)pi * S + smp, make_float4(R.tb, R.hu, R.hv, __uint_as_float(R.hp)), nt_hits);
             if (R.hp != RT_SENT) {
                 cr = R.hu;
                 cg = R.hv;
@@ -1213,8 +1228,8 @@ struct CoopLds {
 template <int G>
 __device__ __forceinline__ uint64_t gballot(bool p, uint32_t gbase) {
     const uint64_t b = __ballot(p);
-    if (G == 64) return b;
-    return (b >> gbase) & ((1ull << G) - 1ull);
+    if constexpr (G == 64) return b;
+    else return (b >> gbase) & ((1ull << G) - 1ull);
 }
 
 __device__ __forceinline__ float gread_f(float x, uint32_t src) {
@@ -2342,14 +2357,14 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         wide && sched && sched->coop_q && n <= kBufMaxN
             ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : coop_cap_for_frame(cfg.coop_cap, spp, small))
             : 0u;
-    // samples in lanes (k_trace_sl): multi-spp tiles by default (trace.spp_lanes = 1), full frames too at 2
+    // samples in lanes (k_trace_sl): multi-spp tiles and full frames (trace.spp_lanes = 2, the default;
+    // 1 = tiles only)
     const bool sl = spp >= 2 && spp <= 16 && (spp & (spp - 1)) == 0 && wide && warity == 4 && !counters &&
                     n <= kBufMaxN && cfg.buf_loads &&
                     (cfg.spp_lanes == 2 || (cfg.spp_lanes == 1 && (packed || nranks > 1)));
     // its queue needs the hits of every sample (k_coop_resolve), so no queue without a hits buffer
     const uint32_t sl_cap = !sl || !hits || !sched || !sched->coop_q ? 0u
-                            : (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks)
-                                          : coop_cap_for_frame(cfg.coop_cap, 1, false));
+                            : coop_cap_for_sl(nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap);
     const uint32_t coop_cap = sl ? sl_cap : coop_cap0;
     const bool can_fold = RT_ORDER_FOLD && sched && nranks == 1 && !packed && !small && wide && !counters &&
                           !cfg.order_override && coop_cap == 0 && nb <= 256 * kFoldPerThread && !sl;
@@ -2423,11 +2438,13 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
+    // nontemporal hit records: trace.nt_hits 1 = frames of >= 2 spp, 2 = always, 0 = never
+    const uint32_t nt_hits = (cfg.nt_hits == 2 || (cfg.nt_hits == 1 && spp >= 2)) ? 1u : 0u;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
     k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, spp == 1, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, \
                              wnodes, stack_cap_for(cfg, warity, NT), tris, n,                                            \
                              cam, w, h, spp, rank, nranks, tilesX, H, R, counters, (const float*)nullptr, Light{},      \
-                             order, cost_out, px_prev, px_cost, coop_cap, cq, fold)
+                             order, cost_out, px_prev, px_cost, coop_cap, cq, fold, nt_hits)
 #define RT_TRACE(C, P, WI) \
     if (small) RT_TRACE_NT(C, P, WI, 64); else RT_TRACE_NT(C, P, WI, 256)
 #define RT_TRACE_W(C, P)           \
@@ -2442,7 +2459,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         const uint32_t wc = stack_cap_for(cfg, 4, nt);
 #define RT_SL(P, NT, S_)                                                                                           \
     RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
-               nranks, tilesX, H, R, order, cost_out, coop_cap, cq)
+               nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits)
 #define RT_SL_S(P, NT)                  \
     switch (spp) {                      \
         case 2: RT_SL(P, NT, 2); break;   \

@@ -7,7 +7,7 @@ the hits.  Every frame must equal the CPU oracle bit for bit -- hits and
 RGBA -- across the queue caps (many queued samples, several per pixel), a
 full or tiny queue, no hits buffer (queue off), forced stack overflows
 (binary hand-off), odd frame sizes, successive frames (tile order), the
-per-rank tiles (default) and full frames (spp_lanes = 2)."""
+per-rank tiles and full frames (spp_lanes = 2, the default; 1 = tiles only)."""
 import numpy as np
 import pytest
 
@@ -138,7 +138,7 @@ def test_spp_lanes_full_frames(R, oracle, cfg, scene30k, spp, cap, wg):
     and without the queue; odd frame size; three frames."""
     w, h = 77, 41
     eh, er = _frame(oracle, scene30k, w, h, spp)
-    cfg("trace.spp_lanes", 2, 1)
+    cfg("trace.spp_lanes", 2, 2)
     cfg("trace.coop_cap", cap, -1)
     cfg("trace.wg", wg, 256)
     with R.Scene.from_soup(scene30k) as s:
@@ -171,7 +171,18 @@ def test_spp_lanes_equals_loop_kernel(R, cfg):
                 torch.cuda.synchronize()
                 got.append((slab.cpu().numpy().copy(), sh.cpu().numpy().view(np.uint32).copy()))
             outs[mode] = got
-        R.config_set("trace.spp_lanes", 1)
+        full = {}
+        for mode in (0, 2):
+            R.config_set("trace.spp_lanes", mode)
+            img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+            hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
+            for _ in range(2):
+                s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr())
+            torch.cuda.synchronize()
+            full[mode] = (img.cpu().numpy().copy(), hb.cpu().numpy().view(np.uint32).copy())
+        R.config_set("trace.spp_lanes", 2)
         for r in range(P):
             assert np.array_equal(outs[0][r][0], outs[1][r][0]), r
             assert np.array_equal(outs[0][r][1], outs[1][r][1]), r
+        assert np.array_equal(full[0][0], full[2][0])
+        assert np.array_equal(full[0][1], full[2][1])

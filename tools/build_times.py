@@ -30,17 +30,21 @@ for k, v in knobs:
     R.config_set(k, v)
 s = R.Scene.generate_soup(n, 1)
 between = lambda: None  # noqa: E731
-if os.environ.get("BT_TRACE") == "1":
+if os.environ.get("BT_TRACE", "0") != "0":
+    # BT_TRACE=1: the 1080p1 frame; BT_TRACE=c<k>: the frame of scenes.CONFIGS[k] (c5: 3840x2160x4)
     import torch
     from gpu_raytracer_amd import scenes as S
+    bt = os.environ["BT_TRACE"]
+    ck = int(bt[1:]) if bt.startswith("c") else 3
+    fw, fh, fs = S.CONFIGS[ck].w, S.CONFIGS[ck].h, S.CONFIGS[ck].spp
     v = S.VIEWS[S.CONFIGS[3].scene]
-    cam = R.camera_look_at(v.eye, v.at, v.up, v.vfov, 1920, 1080)
-    img = torch.zeros(1920 * 1080, dtype=torch.int32, device="cuda")
-    hits = torch.zeros(1920 * 1080 * 4, dtype=torch.float32, device="cuda")
+    cam = R.camera_look_at(v.eye, v.at, v.up, v.vfov, fw, fh)
+    img = torch.zeros(fw * fh, dtype=torch.int32, device="cuda")
+    hits = torch.zeros(fw * fh * fs * 4, dtype=torch.float32, device="cuda")
     s.build()
 
     def between():
-        s.render_device(cam, 1920, 1080, 1, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+        s.render_device(cam, fw, fh, fs, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
 rows, tot = [], []
 R.config_set("build.stage_events", 1)
 for i in range(reps + 3):
@@ -58,6 +62,7 @@ for i in range(reps + 3):
 m = np.median(np.array(rows), 0) * 1e3
 lib = os.path.basename(os.environ.get("RT_LIB", "librtamd.so")) + (" fence" if os.environ.get("RT_EVENT_FENCE") == "1" else "")
 lib += " " + ",".join(f"{k}={v}" for k, v in knobs) if knobs else ""
-lib += " after-trace" if os.environ.get("BT_TRACE") == "1" else ""
+lib += (" after-trace" + ("" if os.environ["BT_TRACE"] == "1" else " " + os.environ["BT_TRACE"])
+        if os.environ.get("BT_TRACE", "0") != "0" else "")
 print(f"{lib:<24s} n={n} us: bounds {m[0]:6.1f} morton {m[1]:6.1f} sort {m[2]:6.1f} topo {m[3]:6.1f} "
       f"refit {m[4]:6.1f} wide {m[5]:5.1f} total(stage events) {m[6]:6.1f}  total {np.median(tot) * 1e3:6.1f}")

@@ -13,6 +13,7 @@
 #   pmclds:<tag>:<config>:<steps>    the LDS counter pass (SQ_INSTS_LDS, bank conflicts, ...)
 #                                    -> gpurun_out/prof_<tag>/lds/
 #   py:<tag>:<script>[:<args, "~" for " ">]  a tools/ script -> gpurun_out/<tag>.log
+#   pyenv:<tag>:<VAR=v~VAR2=v>:<script>[:<args>]  the same with environment variables
 #   kstats:<tag>:<script>:<args>[:<counters>]  the script under rocprofv3 (kernel trace + stats,
 #                                    or one --pmc pass) -> gpurun_out/ks_<tag>/
 set -o pipefail
@@ -92,6 +93,13 @@ run_py() {  # tag script args
     tail -5 gpurun_out/$tag.log
 }
 
+run_pyenv() {  # tag env-assignments ("~" between) script args: a tools/ script with environment variables
+    local tag=$1 envs=${2//\~/ } script=$3 args=${4//\~/ }
+    echo "[gpu_run] pyenv $tag: $envs $script $args"
+    env $envs timeout -k 10 900 python -u $script $args > gpurun_out/$tag.log 2>&1 || { tail -40 gpurun_out/$tag.log; return 1; }
+    tail -5 gpurun_out/$tag.log
+}
+
 for step in "$@"; do
     IFS=':' read -r kind a b c d <<< "$step"
     case $kind in
@@ -100,6 +108,7 @@ for step in "$@"; do
         profile) run_profile "$a" "$b" "$c" || exit 1 ;;
         pmclds) run_pmclds "$a" "$b" "$c" || exit 1 ;;
         py) run_py "$a" "$b" "$c" || exit 1 ;;
+        pyenv) run_pyenv "$a" "$b" "$c" "$d" || exit 1 ;;
         kstats) run_kstats "$a" "$b" "$c" "$d" || exit 1 ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
