@@ -1330,9 +1330,52 @@ __global__ __launch_bounds__(256) void k_sparse_far(float* __restrict__ table, u
     }
 }
 
-// LDS segment tree over the M per-block totals (M <= kLdsTreeMaxBlocks) or a
-// global sparse table (levels built by k_sparse_near / k_sparse_far) for larger M.
-template <bool LDS_TREE>
+// Group tables (r05, the default crossing path up to kLdsTreeMaxBlocks
+// groups): the m per-block totals (table level 0, written by k_topo_refit)
+// in groups of kGroupBlocks = 64 blocks, one wave per group:
+//   levels 1..5  U totals [b, b + 2^k) inside the group (range queries of
+//                fewer than 64 blocks: two entries of one level),
+//   level  6     U totals [group start, b]  (in-group prefix),
+//   level  7     U totals [b, group end]    (in-group suffix),
+//   level  8     the group totals ([ng] entries),
+// at table + k * m * 6.  A middle-block range [bl, br) that crosses groups is
+// then gsuf[bl] U (groups strictly between, an LDS segment tree over <= 2048
+// group totals in each k_refit_cross block) U gpre[br - 1].  This replaces the
+// global sparse table (k_sparse_near + k_sparse_far, whose top levels loop
+// over up to 2^(L-9) entries each: 21 us at 10M with 512-leaf blocks, ~4x
+// that with 256) and the per-block LDS tree over up to 2048 block totals
+// (98 KB of LDS in each of the crossing kernel's blocks) with one wave per 64
+// blocks.  min/max are exact, so every box is the same union.
+constexpr uint32_t kGroupBlocks = 64;
+__global__ __launch_bounds__(64) void k_group_tables(float* __restrict__ table, uint32_t m) {
+    const uint32_t g = blockIdx.x, l = threadIdx.x, b = g * kGroupBlocks + l;
+    const bool ok = b < m;
+    const Aabb t = ok ? load_aabb(table, b) : aabb_empty();
+    Aabb pre = t, suf = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { shfl_up_aabb(pre, o); shfl_down_aabb(suf, o); }
+    if (ok) {
+        store_aabb(table + 6ull * m * 6, b, pre);
+        store_aabb(table + 7ull * m * 6, b, suf);
+    }
+    if (l == 0) store_aabb(table + 8ull * m * 6, g, suf);  // lane 0's suffix = the whole group
+    Aabb v = t;
+#pragma unroll
+    for (int k = 1; k <= 5; ++k) {
+        const int h = 1 << (k - 1);
+        Aabb u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { u.lo[c] = __shfl_down(v.lo[c], h, 64); u.hi[c] = __shfl_down(v.hi[c], h, 64); }
+        if ((int)l + h < 64) aabb_union(v, u);  // entries past the group end are never queried
+        if (ok) store_aabb(table + (uint64_t)k * m * 6, b, v);
+    }
+}
+
+// K6 for the crossing nodes: box = suffix(l) U middle block totals U
+// prefix(r).  MODE 1: the group tables above (ng <= kLdsTreeMaxBlocks);
+// MODE 0: the global sparse table (levels built by k_sparse_near /
+// k_sparse_far) for larger m.
+template <int MODE>
 __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ topo,
                                                      const float* __restrict__ prebuf, const float* __restrict__ sufbuf,
                                                      const float* __restrict__ table /* totals, or sparse levels */,
@@ -1359,13 +1402,15 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
     // off the critical path)
     const uint32_t q0 = blockIdx.x * 256 + threadIdx.x;
     uint32_t i0 = q0 < count ? node_of(q0) : 0u;
+    const uint32_t ng = (m + kGroupBlocks - 1) / kGroupBlocks;
     uint32_t P = 1;
-    while (P < m) P <<= 1;
-    if (LDS_TREE) {
-        for (uint32_t j = threadIdx.x; j < P; j += 256) tree[P + j] = j < m ? load_aabb(table, j) : aabb_empty();
+    while (P < ng) P <<= 1;
+    const float* gtot = table + 8ull * m * 6;
+    if (MODE == 1) {
+        for (uint32_t j = threadIdx.x; j < P; j += 256) tree[P + j] = j < ng ? load_aabb(gtot, j) : aabb_empty();
     }
     uint4 tp0 = q0 < count ? topo[i0] : make_uint4(0u, 0u, 0u, 0u);
-    if (LDS_TREE) {
+    if (MODE == 1) {
         __syncthreads();
         for (uint32_t len = P >> 1; len >= 1; len >>= 1) {
             for (uint32_t j = threadIdx.x; j < len; j += 256) {
@@ -1385,13 +1430,24 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
         aabb_union(box, load_aabb(prebuf, r));
         const uint32_t bl = l / T + 1, br = r / T;  // middle blocks [bl, br)
         if (bl < br) {
-            if (LDS_TREE) {
-                uint32_t a = bl + P, b = br + P;
-                while (a < b) {
-                    if (a & 1) aabb_union(box, tree[a++]);
-                    if (b & 1) aabb_union(box, tree[--b]);
-                    a >>= 1;
-                    b >>= 1;
+            if (MODE == 1) {
+                const uint32_t gl = bl / kGroupBlocks, gr = (br - 1) / kGroupBlocks;
+                if (gl == gr) {  // inside one group: two entries of one in-group level
+                    const uint32_t len = br - bl;
+                    const uint32_t s = 31 - __clz((int)len);
+                    const float* lvl = table + (uint64_t)s * m * 6;
+                    aabb_union(box, load_aabb(lvl, bl));
+                    aabb_union(box, load_aabb(lvl, br - (1u << s)));
+                } else {
+                    aabb_union(box, load_aabb(table + 7ull * m * 6, bl));      // in-group suffix
+                    aabb_union(box, load_aabb(table + 6ull * m * 6, br - 1));  // in-group prefix
+                    uint32_t a = gl + 1 + P, b = gr + P;                       // groups strictly between
+                    while (a < b) {
+                        if (a & 1) aabb_union(box, tree[a++]);
+                        if (b & 1) aabb_union(box, tree[--b]);
+                        a >>= 1;
+                        b >>= 1;
+                    }
                 }
             } else {
                 const uint32_t len = br - bl;
@@ -1403,6 +1459,108 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
         }
         store_node(nodes, i, box, tp.x, tp.y);
     }
+}
+
+// The greedy cut of wide_entries (collapse = 1) for a record built from
+// global memory (k_wide_cross), with each entry's box and topology cached
+// from ONE load of its record -- an internal entry's 32-B node record holds
+// both (topo_of_node), a leaf entry's triangle record gives its box -- so the
+// chain is X's topology word, its children's records, then one round of
+// records per replacement: 4 dependent rounds instead of 7 (the generic form
+// loads a picked entry's topology again after choosing it, and every final
+// entry's box once more for the record).  Same entries, same boxes, so the
+// same record bytes (tests: build parity compares every K7w record's
+// containment and the BVH digests).
+struct WEnt {
+    Aabb box;
+    uint32_t left, mx;  // topology (internal entries): left child, range end
+};
+__device__ __forceinline__ WEnt went_load(const void* nodes, const float4* tri_s, uint32_t i, uint32_t L0) {
+    WEnt e;
+    if (i < L0) {
+        const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)i * 32);
+        const float4 A = p[0], B = p[1];
+        e.box.lo[0] = A.x; e.box.lo[1] = A.y; e.box.lo[2] = A.z;
+        e.box.hi[0] = A.w; e.box.hi[1] = B.x; e.box.hi[2] = B.y;
+        const uint32_t esc = __float_as_uint(B.w);
+        e.left = __float_as_uint(B.z);
+        e.mx = esc == RT_SENT ? L0 : esc >= L0 ? esc - L0 - 1 : esc - 1;
+    } else {
+        e.box = leaf_box(tri_s, i - L0);
+        e.left = 0u;
+        e.mx = 0u;
+    }
+    return e;
+}
+
+template <int W>
+__device__ __forceinline__ void wide_record_g(uint32_t X, const uint4& tx, const Aabb& bx, uint32_t L0,
+                                              const void* __restrict__ nodes, const float4* __restrict__ tri_s,
+                                              uint4* __restrict__ wnodes) {
+    // per entry: node index, box (6 floats), left child, range end, surface --
+    // scalar arrays with static indices only (selects of whole structs went
+    // through scratch)
+    uint32_t node[W], el[W], em[W];
+    float bb[6][W], ar[W];
+    auto put = [&](int i, uint32_t nd, const WEnt& e) {
+        node[i] = nd;
+        el[i] = e.left;
+        em[i] = e.mx;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { bb[c][i] = e.box.lo[c]; bb[3 + c][i] = e.box.hi[c]; }
+        ar[i] = nd < L0 ? half_area(e.box) : 0.0f;
+    };
+    uint32_t l, r;
+    kids_of(tx, L0, l, r);
+    put(0, l, went_load(nodes, tri_s, l, L0));
+    put(1, r, went_load(nodes, tri_s, r, L0));
+#pragma unroll
+    for (int i = 2; i < W; ++i) {
+        node[i] = RT_SENT; el[i] = 0u; em[i] = 0u; ar[i] = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { bb[c][i] = bx.lo[c]; bb[3 + c][i] = bx.hi[c]; }
+    }
+#pragma unroll
+    for (int step = 0; step < W - 2; ++step) {
+        int best = -1;
+        float ba = 0.0f;
+#pragma unroll
+        for (int i = 0; i < step + 2; ++i) {
+            if (node[i] < L0) {
+                if (best < 0 || ar[i] > ba) { best = i; ba = ar[i]; }
+            }
+        }
+        if (best < 0) continue;  // no internal entry left (nor in the later steps)
+        uint32_t pl = el[0], pm = em[0];
+#pragma unroll
+        for (int i = 1; i < step + 2; ++i) {
+            pl = best == i ? el[i] : pl;
+            pm = best == i ? em[i] : pm;
+        }
+        uint32_t c0, c1;
+        kids_of(make_uint4(pl, 0u, 0u, pm), L0, c0, c1);
+        const WEnt e0 = went_load(nodes, tri_s, c0, L0), e1 = went_load(nodes, tri_s, c1, L0);
+        // shift the entries after `best` one slot right, then put the two children at best, best + 1
+#pragma unroll
+        for (int i = W - 1; i >= 1; --i) {
+            if (i > best + 1) {
+                node[i] = node[i - 1]; el[i] = el[i - 1]; em[i] = em[i - 1]; ar[i] = ar[i - 1];
+#pragma unroll
+                for (int c = 0; c < 6; ++c) bb[c][i] = bb[c][i - 1];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            if (i == best) put(i, c0, e0);
+            if (i == best + 1) put(i, c1, e1);
+        }
+    }
+    store_wide<W>(wnodes, X, bx, node, [&](int i) {
+        Aabb b;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { b.lo[c] = bb[c][i]; b.hi[c] = bb[3 + c][i]; }
+        return b;
+    }, L0);
 }
 
 // K7w records of the crossing internal nodes, once K6t has written their
@@ -1425,6 +1583,10 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         const uint32_t X = cross[sh * cross_cap + (q - pre[sh])];
         if (X >= L0) continue;
         const uint4 tx = topo[X];
+        if (collapse == 1 || W != 4) {  // the greedy cut, one record load per entry
+            wide_record_g<W>(X, tx, load_aabb_node(nodes, X), L0, nodes, tri_s, wnodes);
+            continue;
+        }
         uint32_t node[W];
         // internal boxes from `nodes`, leaf boxes from the triangle records;
         // a descendant's children from its node record (k_topo_refit writes
@@ -1436,8 +1598,8 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
     }
 }
 
-template __global__ void k_refit_cross<true>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
-template __global__ void k_refit_cross<false>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
+template __global__ void k_refit_cross<1>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
+template __global__ void k_refit_cross<0>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
 
 // ================================================================ launchers
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
@@ -1459,7 +1621,7 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     b.cap_n = n;
     b.ntiles = sort_tiles((uint32_t)N);
     b.m_blocks = cdiv(N, kRefitT);
-    b.levels = sparse_levels(b.m_blocks);
+    b.levels = std::max<uint32_t>(sparse_levels(b.m_blocks), 9u);  // group tables: levels 0..8
     b.nzero = kZEnd;
     hipError_t e;
 #define RT_ALLOC(ptr, bytes) \
@@ -1551,7 +1713,7 @@ static hipError_t ensure_cross_attr() {
     if (e != hipSuccess) return e;
     if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
     std::call_once(once[dev], [dev] {
-        err[dev] = hipFuncSetAttribute((const void*)k_refit_cross<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        err[dev] = hipFuncSetAttribute((const void*)k_refit_cross<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        2 * kLdsTreeMaxBlocks * (int)sizeof(Aabb));
     });
     return err[dev];
@@ -1581,19 +1743,21 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
                                 hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     if (m <= 1) return hipGetLastError();
-    if (m <= (uint32_t)kLdsTreeMaxBlocks) {
+    const uint32_t ng = cdiv(m, kGroupBlocks);
+    if (ng <= (uint32_t)kLdsTreeMaxBlocks) {
         uint32_t P = 1;
-        while (P < m) P <<= 1;
+        while (P < ng) P <<= 1;
         const size_t lds = 2ull * P * sizeof(Aabb);
         const hipError_t e = ensure_cross_attr();
         if (e != hipSuccess) return e;
-        RT_KLAUNCH(k_refit_cross<true>, dim3(RT_CROSS_GRID), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
-                           b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
+        RT_KLAUNCH(k_group_tables, dim3(ng), dim3(kGroupBlocks), 0, s, b.table, m);
+        RT_KLAUNCH(k_refit_cross<1>, dim3(cross_grid(m, RT_CROSS_GRID)), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf,
+                   b.table, m, b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
         const uint32_t L = sparse_levels(m);
         RT_KLAUNCH(k_sparse_near, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table, m, L);
         if (L > kSparseNear + 1) RT_KLAUNCH(k_sparse_far, dim3(cdiv(m, 256)), dim3(256), 0, s, b.table, m, L);
-        RT_KLAUNCH(k_refit_cross<false>, dim3(cross_grid(m, 256)), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
+        RT_KLAUNCH(k_refit_cross<0>, dim3(cross_grid(m, 256)), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
     if (arity == 8)

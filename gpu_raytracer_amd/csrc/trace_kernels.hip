@@ -1008,7 +1008,8 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
         if (dsamp == RT_SENT && rgba) {
             const float sc = 1.0f / (float)spp;
             const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
-            rgba[pi] = px;
+            if (nt_hits > 1) __builtin_nontemporal_store(px, rgba + pi);
+            else rgba[pi] = px;
         }
     }
 #ifdef RT_STAMPS
@@ -1166,7 +1167,9 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
     const uint64_t pm = (S == 64 ? ~0ull : ((1ull << S) - 1ull)) << base;
     if (valid && smp == 0 && !(dm & pm) && rgba) {
         const float sc = 1.0f / (float)S;
-        rgba[pi] = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+        const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
+        if (nt_hits > 1) __builtin_nontemporal_store(px, rgba + pi);
+        else rgba[pi] = px;
     }
     if (cost_out && l == 0) {  // this unit's duration -> its tile's cost map entry (the tile order's key)
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
@@ -2438,8 +2441,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
-    // nontemporal hit records: trace.nt_hits 1 = frames of >= 2 spp, 2 = always, 0 = never
-    const uint32_t nt_hits = (cfg.nt_hits == 2 || (cfg.nt_hits == 1 && spp >= 2)) ? 1u : 0u;
+    // nontemporal hit records: trace.nt_hits 1 = frames of >= 2 spp, 2 = always, 0 = never; 3 = multi-spp
+    // hits and RGBA (A/B: the kernels' nt_hits > 1 also streams the RGBA stores)
+    const uint32_t nt_hits = (cfg.nt_hits == 2 || ((cfg.nt_hits == 1 || cfg.nt_hits == 3) && spp >= 2))
+                                 ? (cfg.nt_hits == 3 ? 2u : 1u) : 0u;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
     k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, spp == 1, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, \
                              wnodes, stack_cap_for(cfg, warity, NT), tris, n,                                            \

@@ -43,8 +43,10 @@ if os.environ.get("BT_TRACE", "0") != "0":
     hits = torch.zeros(fw * fh * fs * 4, dtype=torch.float32, device="cuda")
     s.build()
 
+    nohits = os.environ.get("BT_HITS") == "0"  # the frame writes RGBA only
+
     def between():
-        s.render_device(cam, fw, fh, fs, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+        s.render_device(cam, fw, fh, fs, d_rgba=img.data_ptr(), d_hits=0 if nohits else hits.data_ptr(), timed=True)
 rows, tot = [], []
 R.config_set("build.stage_events", 1)
 for i in range(reps + 3):
