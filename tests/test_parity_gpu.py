@@ -610,3 +610,51 @@ def test_tile_order_moving_camera(R, oracle):
             hits, rgba, _ = s.render(cam, w, h, 1)
             assert np.array_equal(rgba, oracle.shade(eh, w, h, 1)), i
             assert np.array_equal(bits(hits["t"]), bits(eh["t"])), i
+
+
+def test_crossing_ranges_at_group_boundaries(R, oracle):
+    """The crossing stage's group tables (k_group_tables: 64 refit blocks per
+    group) on crafted sorted keys whose subtrees cover exactly one whole group
+    of middle blocks, or sit inside one, for 512- and 256-leaf refit blocks:
+    rt_stage_refit's every node record == boxes unioned in numpy over each
+    node's leaf range (a sparse table), with the oracle's topology and escape
+    links.  (A middle range of exactly 64 blocks once took a non-existent
+    in-group level.)"""
+    n = 140_000
+    segs = [0, 32_356, 65_587, 98_057, 114_692, 131_072 + 77, n]  # segment j: keys j << 24 | offset
+    keys = np.zeros(n, np.uint32)
+    for j in range(len(segs) - 1):
+        keys[segs[j]:segs[j + 1]] = (j << 24) | np.arange(segs[j + 1] - segs[j], dtype=np.uint32)
+    vals = np.arange(n, dtype=np.uint32)
+    tris = soup(oracle, n, 5)
+    nodes = R.stage_refit(keys, vals, tris)
+    left, right, rlo, rhi, parent = oracle.karras(keys)
+    esc = oracle.escape(n, left, right, parent)
+    t = tris.reshape(n, 3, 3)
+    blo, bhi = t.min(axis=1), t.max(axis=1)
+    # sparse tables of the leaf boxes, then every internal node's range union
+    tabs_lo, tabs_hi = [blo], [bhi]
+    k = 1
+    while (1 << k) <= n:
+        h = 1 << (k - 1)
+        a, b = tabs_lo[-1], tabs_hi[-1]
+        tabs_lo.append(np.minimum(a[:-h], a[h:]))
+        tabs_hi.append(np.maximum(b[:-h], b[h:]))
+        k += 1
+    ln = (rhi - rlo + 1).astype(np.int64)
+    lv = np.floor(np.log2(ln)).astype(np.int64)
+    exp_lo = np.zeros((n - 1, 3), np.float32)
+    exp_hi = np.zeros((n - 1, 3), np.float32)
+    for s in np.unique(lv):
+        sel = np.nonzero(lv == s)[0]
+        a0, a1 = rlo[sel].astype(np.int64), (rhi[sel].astype(np.int64) - (1 << s) + 1)
+        exp_lo[sel] = np.minimum(tabs_lo[s][a0], tabs_lo[s][a1])
+        exp_hi[sel] = np.maximum(tabs_hi[s][a0], tabs_hi[s][a1])
+    g = nodes[: n - 1]
+    assert np.array_equal(g["a"], left)
+    assert np.array_equal(g["esc"], esc[: n - 1])
+    assert np.array_equal(bits(g["lo"]), bits(exp_lo))
+    assert np.array_equal(bits(g["hi"]), bits(exp_hi))
+    lf = nodes[n - 1:]
+    assert np.array_equal(lf["a"], vals) and np.array_equal(lf["esc"], esc[n - 1:])
+    assert np.array_equal(bits(lf["lo"]), bits(blo)) and np.array_equal(bits(lf["hi"]), bits(bhi))
