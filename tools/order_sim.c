@@ -136,3 +136,95 @@ void osim_trace(const orc_node* nodes, uint32_t n, const float* tris, const orc_
             stackmax[i] = (uint8_t)(ms > 255 ? 255 : ms);
         }
 }
+
+/* VERDICT r04 item 6 (certified nearest-first, the stop rule): per ray, the
+ * subtrees the nearest-first pass culls ONLY because their entry tn exceeds
+ * the best self-consistent t found so far (tn <= tf: the float slab test
+ * passes, so §9.7 -- whose tb can be larger there -- may enter them).  A
+ * sound certificate must show that no triangle inside such a subtree has a
+ * Moller-Trumbore t below the answer, i.e. bound MT's forward error for every
+ * triangle in it; that error grows like 1/|d.n| (the ray nearly in the
+ * triangle's plane), so the bound needs the subtree's normal cone, and a cone
+ * over more than a few random triangles spans the sphere.  Reported per ray:
+ * the number of such subtrees and the largest one's leaf count (range length
+ * from rlo/rhi; a leaf counts 1).  nf_hz_count[i], nf_hz_max[i]. */
+static uint32_t nf_hazards(const orc_node* nodes, uint32_t n, const float* tris, const float* o, const float* d,
+                           const float* invd, const uint32_t* rlo, const uint32_t* rhi, uint32_t* hz_count,
+                           uint32_t* hz_max) {
+    uint32_t stk[256];
+    float stn[256];
+    uint32_t sp = 0, cnt = 0, L0 = n - 1, hc = 0, hm = 0;
+    float bt = INFINITY;
+    float rtn, rtf;
+    slab(&nodes[0], o, invd, &rtn, &rtf);
+    uint32_t cur = (rtn <= rtf) ? 0u : SENT;
+    float ctn = rtn;
+#define HZ(node_)                                                                          \
+    do {                                                                                   \
+        const uint32_t s_ = (node_) >= L0 ? 1u : rhi[(node_)] - rlo[(node_)] + 1u;       \
+        ++hc;                                                                              \
+        if (s_ > hm) hm = s_;                                                              \
+    } while (0)
+    for (;;) {
+        if (cur == SENT) {
+            if (!sp) break;
+            --sp;
+            cur = stk[sp];
+            ctn = stn[sp];
+        }
+        if (ctn > bt) { HZ(cur); cur = SENT; continue; }  /* popped after bt shrank below its entry */
+        const orc_node* nd = &nodes[cur];
+        ++cnt;
+        if (cur >= L0) {
+            float tn, tf, t, u, v;
+            slab(nd, o, invd, &tn, &tf);
+            if (tn <= tf && orc_intersect_tri(o, d, tris + (size_t)nd->a * 9, INFINITY, &t, &u, &v) && tn <= t &&
+                t < bt)
+                bt = t;
+            cur = SENT;
+            continue;
+        }
+        const uint32_t l = nd->a, r = nodes[l].esc;
+        float ln, lf, rn, rf;
+        slab(&nodes[l], o, invd, &ln, &lf);
+        slab(&nodes[r], o, invd, &rn, &rf);
+        const int lg = ln <= lf, rg = rn <= rf;  /* geometric hits (tb-independent) */
+        const int lh = lg && ln <= bt, rh = rg && rn <= bt;
+        if (lg && !lh) HZ(l);
+        if (rg && !rh) HZ(r);
+        if (lh && rh) {
+            const int lfirst = ln <= rn;
+            stk[sp] = lfirst ? r : l;
+            stn[sp] = lfirst ? rn : ln;
+            ++sp;
+            cur = lfirst ? l : r;
+            ctn = lfirst ? ln : rn;
+        } else if (lh) { cur = l; ctn = ln; }
+        else if (rh) { cur = r; ctn = rn; }
+        else cur = SENT;
+    }
+#undef HZ
+    *hz_count = hc;
+    *hz_max = hm;
+    return cnt;
+}
+
+void osim_hazards(const orc_node* nodes, uint32_t n, const float* tris, const orc_camera* c, uint32_t w,
+                  uint32_t y0, uint32_t y1, const uint32_t* rlo, const uint32_t* rhi, uint16_t* pre_steps,
+                  uint32_t* hz_count, uint32_t* hz_max) {
+    for (uint32_t y = y0; y < y1; ++y)
+        for (uint32_t x = 0; x < w; ++x) {
+            const float px = (float)x + 0.5f, py = (float)y + 0.5f;
+            float d[3], invd[3];
+            for (int a = 0; a < 3; ++a) {
+                d[a] = (c->w00[a] + px * c->du[a]) + py * c->dv[a];
+                invd[a] = 1.0f / d[a];
+            }
+            uint32_t p1;
+            float t1;
+            const uint64_t i = (uint64_t)y * w + x;
+            const uint32_t a = pre(nodes, n, tris, c->eye, d, invd, &p1, &t1);
+            pre_steps[i] = (uint16_t)(a > 65535 ? 65535 : a);
+            nf_hazards(nodes, n, tris, c->eye, d, invd, rlo, rhi, &hz_count[i], &hz_max[i]);
+        }
+}
