@@ -1123,62 +1123,6 @@ __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoO
     node[3 % W] = a1 != RT_SENT ? b1 : RT_SENT;
 }
 
-// Group tables (r05, the default crossing path up to kLdsTreeMaxBlocks
-// groups): the m per-block totals (table level 0, written by k_topo_refit)
-// in groups of kGroupBlocks = 64 blocks, one wave per group:
-//   levels 1..5  U totals [b, b + 2^k) inside the group (range queries of
-//                fewer than 64 blocks: two entries of one level),
-//   level  6     U totals [group start, b]  (in-group prefix),
-//   level  7     U totals [b, group end]    (in-group suffix),
-//   level  8     the group totals ([ng] entries),
-// at table + k * m * 6.  A middle-block range [bl, br) that crosses groups is
-// then gsuf[bl] U (groups strictly between, an LDS segment tree over <= 2048
-// group totals in each k_refit_cross block) U gpre[br - 1].  This replaces the
-// global sparse table (k_sparse_near + k_sparse_far, whose top levels loop
-// over up to 2^(L-9) entries each: 21 us at 10M with 512-leaf blocks, ~4x
-// that with 256) and the per-block LDS tree over up to 2048 block totals
-// (98 KB of LDS in each of the crossing kernel's blocks) with one wave per 64
-// blocks.  min/max are exact, so every box is the same union.
-// The single-GPU build folds them into k_topo_refit (a group's last block
-// to finish computes them: arrival counters, the fused K0 + K1's publication
-// order -- write-through totals, vmcnt(0), then the arrival), which saves the
-// launch (~5 us at 1M); the distributed build's merge launches k_group_tables.
-constexpr uint32_t kGroupBlocks = 64;
-// One wave (lane l = block 64g + l) computes group g's tables; `t` is the
-// lane's block total (empty past m).
-__device__ __forceinline__ void group_tables_wave(float* __restrict__ table, uint32_t m, uint32_t g, const Aabb& t) {
-    const uint32_t l = threadIdx.x & 63, b = g * kGroupBlocks + l;
-    const bool ok = b < m;
-    // one scan at a time, loops not unrolled: k_topo_refit folds this in, and
-    // its register budget (64 VGPRs for 8 waves per SIMD) is set elsewhere
-    Aabb v = t;
-#pragma unroll 1
-    for (int o = 1; o < 64; o <<= 1) shfl_up_aabb(v, o);
-    if (ok) store_aabb(table + 6ull * m * 6, b, v);
-    v = t;
-#pragma unroll 1
-    for (int o = 1; o < 64; o <<= 1) shfl_down_aabb(v, o);
-    if (ok) store_aabb(table + 7ull * m * 6, b, v);
-    if (l == 0) store_aabb(table + 8ull * m * 6, g, v);  // lane 0's suffix = the whole group
-    v = t;
-#pragma unroll 1
-    for (int k = 1; k <= 5; ++k) {
-        const int h = 1 << (k - 1);
-        Aabb u;
-#pragma unroll
-        for (int c = 0; c < 3; ++c) { u.lo[c] = __shfl_down(v.lo[c], h, 64); u.hi[c] = __shfl_down(v.hi[c], h, 64); }
-        if ((int)l + h < 64) aabb_union(v, u);  // entries past the group end are never queried
-        if (ok) store_aabb(table + (uint64_t)k * m * 6, b, v);
-    }
-}
-// The group tables as their own launch: the distributed build's merge, whose
-// totals arrive by all-gather (the single-GPU build folds them into
-// k_topo_refit: its last block of each group computes them).
-__global__ __launch_bounds__(64) void k_group_tables(float* __restrict__ table, uint32_t m) {
-    const uint32_t b = blockIdx.x * kGroupBlocks + threadIdx.x;
-    group_tables_wave(table, m, blockIdx.x, b < m ? load_aabb(table, b) : aabb_empty());
-}
-
 // K4 + K6 local + K7w local, fused.  One block = kRefitT consecutive sorted
 // leaves [B0, B1) and the internal nodes with the same indices, one thread
 // per leaf/node:
@@ -1199,10 +1143,10 @@ __global__ __launch_bounds__(64) void k_group_tables(float* __restrict__ table, 
 // LDS inside this window; a search that would leave it runs wave-wide in
 // global memory)
 #ifndef RT_REFIT_KEY_MARGIN
-#define RT_REFIT_KEY_MARGIN 1024
+#define RT_REFIT_KEY_MARGIN (RT_REFIT_T >= 512 ? 1024 : 512)  // the window must fit the T-entry table buffer
 #endif
 template <int W>
-__global__ __launch_bounds__(kRefitT, W == 4 ? 8 : 1) void k_topo_refit(const uint32_t* __restrict__ keys_g,
+__global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restrict__ keys_g,
                                                         const uint32_t* __restrict__ svals,
                                                         const float* __restrict__ tris, uint32_t n,
                                                         uint4* __restrict__ topo, uint32_t* __restrict__ parent,
@@ -1214,8 +1158,7 @@ __global__ __launch_bounds__(kRefitT, W == 4 ? 8 : 1) void k_topo_refit(const ui
                                                         uint32_t block0 = 0,
                                                         const uint32_t* __restrict__ flags_src = nullptr,
                                                         uint32_t* __restrict__ flags_dst = nullptr,
-                                                        const uint32_t* __restrict__ bstart = nullptr,
-                                                        uint32_t* __restrict__ group_ctr = nullptr) {
+                                                        const uint32_t* __restrict__ bstart = nullptr) {
     constexpr int T = kRefitT, NW = T / 64, KW = RT_REFIT_KEY_MARGIN;
     // the build's verdict words (zero[kZDense ..]), final once the sort
     // kernels have run, to the host's mapped pinned copy: no copy launch
@@ -1274,18 +1217,7 @@ __global__ __launch_bounds__(kRefitT, W == 4 ? 8 : 1) void k_topo_refit(const ui
         const bool need_pre = (has_int && tp.w == k && tp.z < B0) || (k == n - 1 && B0 > 0);
         if (need_suf) store_aabb(sufbuf, k, suf);
         if (need_pre) store_aabb(prebuf, k, pre);
-        if (k == B1 - 1) {
-            if (group_ctr) {  // read by the group's last block (maybe on another XCD): write-through
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    __hip_atomic_store(totals + (uint64_t)gb * 6 + c, pre.lo[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    __hip_atomic_store(totals + (uint64_t)gb * 6 + 3 + c, pre.hi[c], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            } else {
-                store_aabb(totals, gb, pre);
-            }
-        }
+        if (k == B1 - 1) store_aabb(totals, gb, pre);
         if (has_int && (tp.z < B0 || tp.w >= B1)) {
             cslot = atomicAdd(&s_ncross, 1u);  // LDS
             topo[k] = tp;
@@ -1348,37 +1280,9 @@ __global__ __launch_bounds__(kRefitT, W == 4 ? 8 : 1) void k_topo_refit(const ui
 #pragma unroll
         for (int i = 0; i < W; ++i)
             slot[i] = node[i] == RT_SENT ? T + tid : node[i] >= L0 ? node[i] - L0 - B0 : T + node[i] - B0;
-#ifdef RT_EXP_SKIP_WIDE  // timing experiment only (wrong output): write one local record in RT_EXP_SKIP_WIDE
-        if (k % RT_EXP_SKIP_WIDE == 0)
-#endif
         store_wide<W>(wnodes, k, bx, node, [&](int i) { return s_box[slot[i]]; }, L0);
     }
     RT_STAMP(5);
-    if (group_ctr) {  // uniform: the single-GPU build, every block of the grid
-        // the crossing stage's group tables, by the group's last block to get here
-        __shared__ uint32_t s_last;
-        const uint32_t m = (n + T - 1) / T, g = gb / kGroupBlocks;
-        const uint32_t gsize = min(kGroupBlocks, m - g * kGroupBlocks);
-        drain_vm_stores();  // this block's write-through total is acknowledged before its arrival
-        __syncthreads();
-        if (tid == 0)
-            s_last = __hip_atomic_fetch_add(group_ctr + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1;
-        __syncthreads();
-        if (s_last && wv == 0) {  // block-uniform branch, one wave
-            const uint32_t b = g * kGroupBlocks + lane;
-            Aabb t = aabb_empty();
-            if (b < m) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    t.lo[c] = __hip_atomic_load(totals + (uint64_t)b * 6 + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    t.hi[c] = __hip_atomic_load(totals + (uint64_t)b * 6 + 3 + c, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            group_tables_wave(totals, m, g, t);
-            if (lane == 0) __hip_atomic_store(group_ctr + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next build
-        }
-    }
 }
 
 // Global sparse table over the m per-block totals (more than
@@ -1423,6 +1327,51 @@ __global__ __launch_bounds__(256) void k_sparse_far(float* __restrict__ table, u
             if (j < m) aabb_union(a, load_aabb(near, j));
         }
         store_aabb(table + (uint64_t)lv * m * 6, b, a);
+    }
+}
+
+// Group tables (r05, the default crossing path up to kLdsTreeMaxBlocks
+// groups): the m per-block totals (table level 0, written by k_topo_refit)
+// in groups of kGroupBlocks = 64 blocks, one wave per group:
+//   levels 1..5  U totals [b, b + 2^k) inside the group (range queries of
+//                fewer than 64 blocks: two entries of one level),
+//   level  6     U totals [group start, b]  (in-group prefix),
+//   level  7     U totals [b, group end]    (in-group suffix),
+//   level  8     the group totals ([ng] entries),
+// at table + k * m * 6.  A middle-block range [bl, br) that crosses groups is
+// then gsuf[bl] U (groups strictly between, an LDS segment tree over <= 2048
+// group totals in each k_refit_cross block) U gpre[br - 1].  This replaces the
+// global sparse table (k_sparse_near + k_sparse_far, whose top levels loop
+// over up to 2^(L-9) entries each: 21 us at 10M with 512-leaf blocks, ~4x
+// that with 256) and the per-block LDS tree over up to 2048 block totals
+// (98 KB of LDS in each of the crossing kernel's blocks) with one wave per 64
+// blocks.  min/max are exact, so every box is the same union.  (Folding
+// this into k_topo_refit -- the last block of each group computing its
+// tables behind write-through totals and an arrival counter -- cost the
+// refit kernel what it saved in launches: 1M build 139.5 -> 140.7 us, 10M
+// 1123.7 -> 1122.7 us; profiles/ab_group_fold_r05.log.  Not kept.)
+constexpr uint32_t kGroupBlocks = 64;
+__global__ __launch_bounds__(64) void k_group_tables(float* __restrict__ table, uint32_t m) {
+    const uint32_t g = blockIdx.x, l = threadIdx.x, b = g * kGroupBlocks + l;
+    const bool ok = b < m;
+    const Aabb t = ok ? load_aabb(table, b) : aabb_empty();
+    Aabb pre = t, suf = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) { shfl_up_aabb(pre, o); shfl_down_aabb(suf, o); }
+    if (ok) {
+        store_aabb(table + 6ull * m * 6, b, pre);
+        store_aabb(table + 7ull * m * 6, b, suf);
+    }
+    if (l == 0) store_aabb(table + 8ull * m * 6, g, suf);  // lane 0's suffix = the whole group
+    Aabb v = t;
+#pragma unroll
+    for (int k = 1; k <= 5; ++k) {
+        const int h = 1 << (k - 1);
+        Aabb u;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) { u.lo[c] = __shfl_down(v.lo[c], h, 64); u.hi[c] = __shfl_down(v.hi[c], h, 64); }
+        if ((int)l + h < 64) aabb_union(v, u);  // entries past the group end are never queried
+        if (ok) store_aabb(table + (uint64_t)k * m * 6, b, v);
     }
 }
 
@@ -1702,17 +1651,14 @@ hipError_t alloc_build(BuildBufs& b, uint32_t n) {
     RT_ALLOC(b.partials, (uint64_t)bounds_grid((uint32_t)N) * 24);
     RT_ALLOC(b.params, sizeof(BuildParams));
     RT_ALLOC(b.zero, (uint64_t)kZAlloc * 4);
-    const uint64_t ngroups = cdiv(b.m_blocks, kGroupBlocks);
-    RT_ALLOC(b.gctr, ngroups * 4);
 #undef RT_ALLOC
     if ((e = hipMemset(b.zero, 0, (uint64_t)kZAlloc * 4)) != hipSuccess) { free_build(b); return e; }
-    if ((e = hipMemset(b.gctr, 0, ngroups * 4)) != hipSuccess) { free_build(b); return e; }
     return hipSuccess;
 }
 
 void free_build(BuildBufs& b) {
     void* ps[] = {b.tris, b.keys[0], b.keys[1], b.vals[0], b.vals[1], b.nodes, b.tri_s, b.parent, b.topo, b.wnodes,
-                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.bstart, b.partials, b.params, b.zero, b.gctr};
+                  b.prebuf, b.sufbuf, b.table, b.cross, b.counts, b.bstart, b.partials, b.params, b.zero};
     for (void* p : ps)
         if (p) (void)hipFree(p);
     b = BuildBufs{};
@@ -1799,9 +1745,8 @@ static uint32_t cross_grid(uint32_t m, uint32_t floor_blocks) {
     return std::min<uint32_t>(4096u, std::max<uint32_t>(floor_blocks, cdiv(RT_XGRID_PER_BLOCK * m, 256)));
 }
 
-// tables_done: k_topo_refit already computed the group tables (single-GPU builds)
 static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
-                                hipStream_t s, bool tables_done = false) {
+                                hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     if (m <= 1) return hipGetLastError();
     const uint32_t ng = cdiv(m, kGroupBlocks);
@@ -1811,7 +1756,7 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
         const size_t lds = 2ull * P * sizeof(Aabb);
         const hipError_t e = ensure_cross_attr();
         if (e != hipSuccess) return e;
-        if (!tables_done) RT_KLAUNCH(k_group_tables, dim3(ng), dim3(kGroupBlocks), 0, s, b.table, m);
+        RT_KLAUNCH(k_group_tables, dim3(ng), dim3(kGroupBlocks), 0, s, b.table, m);
         RT_KLAUNCH(k_refit_cross<1>, dim3(cross_grid(m, RT_CROSS_GRID)), dim3(256), lds, s, b.topo, b.prebuf, b.sufbuf,
                    b.table, m, b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     } else {
@@ -1832,36 +1777,28 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
 
 // K4 + K5 + K6-local + K7w-local (k_topo_refit) over sorted keys/vals in
 // keys[0]/vals[0]; expects the crossing-list counters zeroed (K0 does it).
-// group_ctr (nullable): fold the group tables into k_topo_refit -- only when
-// the launch covers every block (the single-GPU build)
 static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
                                      uint32_t block0, uint32_t nblocks, hipStream_t s,
-                                     uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr,
-                                     uint32_t* group_ctr = nullptr) {
+                                     uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr) {
     const uint32_t* fsrc = host_flags ? b.zero + kZDense : nullptr;
     const uint32_t m = cdiv(n, kRefitT);
     if (arity == 8)
         RT_KLAUNCH(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart,
-                           group_ctr);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart);
     else
         RT_KLAUNCH(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart,
-                           group_ctr);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart);
     return hipGetLastError();
 }
-// the single-GPU builds fold the group tables into k_topo_refit
-static bool fold_groups(uint32_t n) { return n && cdiv(cdiv(n, kRefitT), kGroupBlocks) <= (uint32_t)kLdsTreeMaxBlocks; }
 
 // bstart (nullable): the [1025] bucket starts of the keys' top 10 bits (an
 // MSB or gather sort wrote them), for the long-range nodes' closed form
 static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
                                     hipStream_t s, uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr) {
     if (!n) return hipSuccess;
-    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s, host_flags, bstart,
-                              fold_groups(n) ? b.gctr : nullptr);
+    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s, host_flags, bstart);
 }
 
 hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
@@ -1869,7 +1806,7 @@ hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
     hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
     if (e != hipSuccess) return e;
     if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
-    return n ? launch_cross(b, n, cfg.wide_collapse, b.warity, s, fold_groups(n)) : hipSuccess;
+    return n ? launch_cross(b, n, cfg.wide_collapse, b.warity, s) : hipSuccess;
 }
 
 // ------------------------------------------- distributed build
@@ -2054,7 +1991,7 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     const uint32_t* bst = (kind != 0 && !probe) ? b.bstart : nullptr;
     if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s, host_flags, bst)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
-    if (n && (e = launch_cross(b, n, cfg.wide_collapse, b.warity, s, fold_groups(n))) != hipSuccess) return e;
+    if (n && (e = launch_cross(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
     if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K4/K6 (records written with the boxes)
     return hipSuccess;

@@ -87,8 +87,11 @@ constexpr uint32_t kMsbMaxN = 512u * kSortTile;
 // and 1024-thread bucket sorts of up to 12288 keys (sort_kernels.hip); a
 // uniform soup's buckets hold n/1024 +- a few sigma keys
 constexpr uint32_t kMsbBigMaxN = 12u * 1000u * 1000u;
+// leaves per k_topo_refit block: 256 since r05 (with the group-table crossing
+// stage, 10M build 1123.7 -> 1103.2 us, 1M 139.5 -> 138.7 us;
+// profiles/ab_refit_t256_r05.log); 512 = the r04 layout (tools/build_exp.sh)
 #ifndef RT_REFIT_T
-#define RT_REFIT_T 512  // A/B builds only (tools/build_exp.sh)
+#define RT_REFIT_T 256
 #endif
 constexpr int kRefitT = RT_REFIT_T;                     // leaves per refit block
 constexpr int kLdsTreeMaxBlocks = 2048;                // K6t LDS segment-tree capacity

@@ -29,9 +29,7 @@ struct BuildBufs {
     uint32_t* bstart = nullptr;     // [1025] MSB bucket starts
     float* prebuf = nullptr;        // n x 6: block-prefix AABB at crossing ends
     float* sufbuf = nullptr;        // n x 6: block-suffix AABB at crossing ends
-    float* table = nullptr;         // refit-block totals + the crossing stage's group tables (or the global
-                                    // sparse table above kLdsTreeMaxBlocks groups), levels x M x 6
-    uint32_t* gctr = nullptr;       // [groups] k_topo_refit's per-group arrival counters (self-resetting)
+    float* table = nullptr;         // sparse table over refit-block totals, levels x M x 6
     uint32_t* cross = nullptr;      // crossing internal nodes (list)
     float* partials = nullptr;      // K0 per-block partial bounds
     BuildParams* params = nullptr;  // lo/hi/inv

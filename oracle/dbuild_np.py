@@ -11,7 +11,7 @@ device phase computes on the rank's share:
   keys     -- §9.3 Morton codes of the slice against the global box, the
               slice sorted by (key, index), its top-10-bit bucket histogram;
   sort     -- the received (key, index) pairs sorted stably (§9.4);
-  subtrees -- for the rank's 512-leaf refit blocks: leaf nodes and leaf
+  subtrees -- for the rank's 256-leaf refit blocks: leaf nodes and leaf
               triangle records, the topology of the internal nodes there
               (§9.5, §9.6), boxes of the nodes whose range lies inside one
               block, the per-block prefix/suffix/total boxes and the list of
@@ -31,7 +31,7 @@ from gpu_raytracer_amd.dist import dbuild_shares_of
 from oracle import oracle as O
 from oracle import oracle_np as N
 
-T = 512  # leaves per refit block (kRefitT)
+T = 256  # leaves per refit block (kRefitT)
 
 
 def _union(lo, hi):
