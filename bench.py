@@ -375,6 +375,32 @@ def rank_emulation(R, S, scene, key, torch, dev, frames=6, drop=2, ranks=EMU_RAN
     return out
 
 
+def build_stage_rooflines(pmc, n):
+    """Per build stage, from the committed profile of the
+    same command (profiles/pmc_summary.json build_stages, tools/pmc_summary.py):
+    its rocprof time per build, the SURVEY.md §8(d) bytes it stands for
+    (K0 + K1 + K2 84 B/prim, K3 64, K4-K7 256 for k_topo_refit; the crossing
+    stage's K6/K7 share of the crossing nodes is inside the 256), the measured
+    HBM bytes (2 x FETCH_SIZE + WRITE_SIZE), and both as fractions of 8 TB/s.
+    `limiter` = the stage with the most time."""
+    st = (pmc or {}).get("build_stages") or {}
+    out = {}
+    for k, v in st.items():
+        us, hb, bpp = v.get("us"), v.get("hbm_bytes"), v.get("algo_bytes_per_prim")
+        if not us:
+            continue
+        algo = bpp * n if bpp else None
+        out[k] = {"us": round(us, 2),
+                  "algo_bytes": algo, "algo_bytes_per_prim": bpp,
+                  "frac": round(algo / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if algo else None,
+                  "traffic": hb,
+                  "hbm_frac_measured": round(hb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4) if hb else None,
+                  "traffic_vs_algo": round(hb / algo, 3) if hb and algo else None}
+    if out:
+        out["limiter"] = max((k for k in out), key=lambda k: out[k]["us"])
+    return out or None
+
+
 def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None, emulate=False):
     """One N=1 line for another BASELINE config (untimed by the step
     contract): build + full-frame trace, static camera, with its row-major
@@ -414,6 +440,7 @@ def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None, emulat
             "trace_ms_row_major": round(cold, 4), "build_ms": round(bd, 4),
             "build_mprims_per_s": round(cfg.n / (bd * 1e-3) / 1e6, 2),
             "build_roofline_frac": round(BUILD_BYTES_PER_PRIM * cfg.n / (bd * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "build_stage_rooflines": build_stage_rooflines(pmc, cfg.n),
             "kernel_bytes_per_launch": kb,
             # requested bytes mostly hit L2/MALL (they can exceed the HBM peak),
             # so they are priced against the aggregate L2 bandwidth
@@ -708,7 +735,8 @@ def main():
                                   "profile); achieved/peak/frac are that resource's. algo_bytes_binary_model = "
                                   "SURVEY.md §8(d) 32/node + 36/tri + 16/ray over the §9.7 binary traversal (node "
                                   "visits the wide kernel does not make: not a roofline of this kernel)"),
-            "roofline_build": {"bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
+            "roofline_build": {"kernels": build_stage_rooflines(pmc, n_tris),
+                               "bound": "hbm", "achieved": round(build_gbs, 1), "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(build_gbs / HBM_PEAK_GBS, 4),
                                "bytes_per_prim": BUILD_BYTES_PER_PRIM,
                                "traffic": pmc.get("build_hbm_bytes") if pmc else None,

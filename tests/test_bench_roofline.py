@@ -43,3 +43,20 @@ def test_committed_profiles_give_fracs_at_most_one():
         r = bench.roofline_of(1.8e9, us * 1e-3, e)
         for k in ("frac", "hbm_frac", "l2_frac", "issue_frac"):
             assert r[k] is None or 0.0 <= r[k] <= 1.0, (e["config"], k, r[k])
+
+
+def test_build_stage_rooflines():
+    """Per-stage build roofline: algorithmic bytes from
+    the §8(d) share, measured bytes and fractions of 8 TB/s, the limiter."""
+    import bench
+    pmc = {"build_stages": {"topo_refit": {"us": 80.0, "hbm_bytes": 3.2e8, "algo_bytes_per_prim": 256},
+                            "crossing": {"us": 15.0, "hbm_bytes": 2.0e7, "algo_bytes_per_prim": 0},
+                            "k0_k1": {"us": 20.0, "hbm_bytes": 8.0e7, "algo_bytes_per_prim": 84}}}
+    r = bench.build_stage_rooflines(pmc, 1_000_000)
+    assert r["limiter"] == "topo_refit"
+    t = r["topo_refit"]
+    assert abs(t["frac"] - 256e6 / 80e-6 / 8e12) < 1e-3
+    assert abs(t["hbm_frac_measured"] - 3.2e8 / 80e-6 / 8e12) < 1e-3
+    assert abs(t["traffic_vs_algo"] - 3.2e8 / 256e6) < 1e-3
+    assert r["crossing"]["frac"] is None and r["crossing"]["traffic"] == 2.0e7
+    assert bench.build_stage_rooflines(None, 10) is None

@@ -26,7 +26,16 @@ from collections import defaultdict
 BUILD = ("k_bounds", "k_morton", "k_msb_scan", "k_msb_scatter", "k_bucket_sort", "k_tile_hist", "k_scatter",
          "k_scan_tiles", "k_topo_refit", "k_refit_cross", "k_wide_cross", "k_sparse_level", "k_sparse_near", "k_sparse_far", "k_bounds_final",
          "k_msb_chunk_sum", "k_msb_chunk_apply", "k_msb_scatter_big", "k_bucket_sort_big",
-         "k_morton_tb", "k_bucket_gather", "k_bucket_dense", "k_digit_hist")
+         "k_morton_tb", "k_bucket_gather", "k_bucket_dense", "k_digit_hist", "k_group_tables")
+# the build's stages for the per-kernel roofline (bench.py roofline_build.kernels), with the
+# SURVEY.md §8(d) bytes per prim each stands for: K0 36 + K1 44 + K2 4; K3 64; K4-K7 256 (local
+# nodes in k_topo_refit, crossing nodes in the crossing stage, which the model does not split)
+STAGE_OF = {"k_bounds": "k0_k1", "k_morton": "k0_k1", "k_morton_tb": "k0_k1", "k_bounds_final": "k0_k1",
+            "k_topo_refit": "topo_refit",
+            "k_refit_cross": "crossing", "k_wide_cross": "crossing", "k_group_tables": "crossing",
+            "k_sparse_near": "crossing", "k_sparse_far": "crossing", "k_sparse_level": "crossing"}
+STAGE_ALGO_BPP = {"k0_k1": 84, "sort": 64, "topo_refit": 256, "crossing": 0}
+TRACE = ("k_trace", "k_trace_sl")
 
 
 def short(name):
@@ -58,19 +67,24 @@ def dispatches(pattern, counter=None):
 
 def frames(seq, warmup):
     """Split a dispatch sequence into timed frames: per frame the trace launch
-    (tile order + trace) and the build kernels before it."""
+    (tile order + trace + the heavy-ray pass and its resolve) and the build
+    kernels before it (also summed per build stage, STAGE_OF)."""
     fr, build = [], []
+    stages = defaultdict(float)
     pend_order = None
     for _, k, v in seq:
         b = base(k)
         if b in BUILD:
             build.append(v)
+            stages[STAGE_OF.get(b, "sort")] += v
         elif b == "k_tile_order":
             pend_order = v
-        elif b == "k_trace":
-            fr.append({"trace": v, "order": pend_order or 0.0, "coop": 0.0, "build": sum(build), "trace_name": k})
+        elif b in TRACE:
+            fr.append({"trace": v, "order": pend_order or 0.0, "coop": 0.0, "build": sum(build), "trace_name": k,
+                       "stages": dict(stages)})
             build, pend_order = [], None
-        elif b == "k_trace_coop" and fr:
+            stages = defaultdict(float)
+        elif b in ("k_trace_coop", "k_coop_resolve") and fr:
             fr[-1]["coop"] += v
     return fr[warmup:]
 
@@ -96,6 +110,10 @@ def main():
         return (mean([x["trace"] + x["coop"] + x["order"] for x in f]), mean([x["trace"] + x["coop"] for x in f]),
                 mean([x["build"] for x in f]))
 
+    def per_stage(fr):
+        keys = sorted({k for x in fr for k in x["stages"]})
+        return {k: mean([x["stages"].get(k, 0.0) for x in fr]) for k in keys}
+
     fetch = per_frame("fetch", "FETCH_SIZE")
     write = per_frame("write", "WRITE_SIZE")
     valu = per_frame("sq", "SQ_INSTS_VALU")
@@ -106,6 +124,14 @@ def main():
     thr = per_frame("sq", "SQ_THREAD_CYCLES_VALU")
     act = per_frame("sq", "SQ_ACTIVE_INST_VALU")
 
+    st_us = per_stage(ft)
+    st_f = per_stage(frames(dispatches(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE"),
+                            warmup))
+    st_w = per_stage(frames(dispatches(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE"),
+                            warmup))
+    build_stages = {k: {"us": st_us[k], "hbm_bytes": (2 * st_f[k] + st_w[k]) * 1024
+                        if k in st_f and k in st_w else None, "algo_bytes_per_prim": STAGE_ALGO_BPP.get(k)}
+                    for k in st_us}
     hbm = 2 * fetch[0] * 1024 + write[0] * 1024 if fetch[0] is not None and write[0] is not None else None
     bhbm = 2 * fetch[2] * 1024 + write[2] * 1024 if fetch[2] is not None and write[2] is not None else None
     cyc = grbm[1] / 8 if grbm[1] else None
@@ -120,7 +146,7 @@ def main():
         "build_kernel_sum_ms": build_us / 1e3
         if build_us is not None else None,
         "hbm_bytes_per_launch": hbm, "fetch_kib_raw": fetch[0], "write_kib": write[0],
-        "build_hbm_bytes": bhbm,
+        "build_hbm_bytes": bhbm, "build_stages": build_stages,
         "valu_insts_per_launch": valu[1], "cycles_per_launch": cyc,
         "cycles_vs_duration_at_2p4ghz": cyc / (trace_us * 2400.0) if cyc and trace_us else None,
         "waves": waves[1], "wait_any_frac": wait[1] / wcyc[1] if wait[1] and wcyc[1] else None,
@@ -155,6 +181,9 @@ def main():
          f"- trace kernels `{kname}` + k_trace_coop: {trace_us:.2f} us (k_trace_coop {coop_us:.2f}); "
          f"k_tile_order {order_us:.2f} us" if trace_us else "- none",
          f"- build kernels (sum): {build_us:.2f} us" if build_us else "",
+         ("- build stages (per build: us, PMC HBM bytes): " + "; ".join(
+             f"{k} {v['us']:.2f} us {v['hbm_bytes']:.4g} B" for k, v in build_stages.items()
+             if v["hbm_bytes"] is not None)) if build_stages else "",
          f"- HBM bytes per trace launch (PMC): {hbm:.4g}; per build: {bhbm:.4g}" if hbm and bhbm else "",
          f"- VALU wave-instructions per trace launch: {valu[1]:.4g}; cycles (GRBM/8): {cyc:.4g}; "
          f"issue fraction {valu[1] / (512 * cyc):.3f}" if valu[1] and cyc else "",
