@@ -1348,8 +1348,11 @@ __global__ __launch_bounds__(256) void k_sparse_far(float* __restrict__ table, u
 // blocks.  min/max are exact, so every box is the same union.  (Folding
 // this into k_topo_refit -- the last block of each group computing its
 // tables behind write-through totals and an arrival counter -- cost the
-// refit kernel what it saved in launches: 1M build 139.5 -> 140.7 us, 10M
-// 1123.7 -> 1122.7 us; profiles/ab_group_fold_r05.log.  Not kept.)
+// refit kernel what it saved in launches, whether the blocks arrived at
+// their end (1M build 139.5 -> 140.7 us, 10M 1123.7 -> 1122.7 us) or right
+// after publishing their totals (1M 140.6 -> 140.0 / 141.3 us, 10M 1126.9 ->
+// 1145.5 us; the folded kernel also needs 58 VGPRs instead of 52);
+// profiles/ab_group_fold_r05.log.  Not kept.)
 constexpr uint32_t kGroupBlocks = 64;
 __global__ __launch_bounds__(64) void k_group_tables(float* __restrict__ table, uint32_t m) {
     const uint32_t g = blockIdx.x, l = threadIdx.x, b = g * kGroupBlocks + l;

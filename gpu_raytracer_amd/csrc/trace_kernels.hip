@@ -1085,7 +1085,9 @@ struct SlShape {
     static constexpr uint32_t TH = PW / TW, TPR = 16 / TW, UPT = 256 / PW;          // rows, blocks per row, units per tile
 };
 
-template <bool PACKED, int NT, int S>
+// MTF: Moller-Trumbore first (wide_step) -- one rank's tiles by default
+// (trace.sl_mtf), the box test first for full frames
+template <bool PACKED, int NT, int S, bool MTF = PACKED>
 __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __restrict__ nodes,
                                                                  const uint4* __restrict__ wnodes, uint32_t wcap,
                                                                  const float4* __restrict__ tri_s, uint32_t n,
@@ -1130,7 +1132,7 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
         uint32_t cn = 0, ct = 0, qslot = 0;
         const WideMem M = wide_mem<4>(wnodes, tri_s, n);
         while (st == 0) {
-            st = wide_step<false, NT, false, PACKED, true, 4>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
+            st = wide_step<false, NT, false, MTF, true, 4>(R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16,
                                                             s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct, false, &M);
             if (coop_cap != 0 && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
         }
@@ -2463,8 +2465,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         const uint32_t grid = (uint32_t)((uint64_t)nb * 4 * spp / (nt / 64));
         const uint32_t wc = stack_cap_for(cfg, 4, nt);
 #define RT_SL(P, NT, S_)                                                                                           \
-    RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
-               nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits)
+    if (P && !cfg.sl_mtf)                                                                                          \
+        RT_KLAUNCH((k_trace_sl<P, NT, S_, false>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, \
+                   h, rank, nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits);                          \
+    else                                                                                                           \
+        RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
+                   nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits)
 #define RT_SL_S(P, NT)                  \
     switch (spp) {                      \
         case 2: RT_SL(P, NT, 2); break;   \

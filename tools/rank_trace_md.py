@@ -38,9 +38,8 @@ def main():
     fr = frames_of(list(csv.DictReader(open(path))))
     assert len(fr) >= nf * (P + 1), (len(fr), nf, P)
     groups = [("full", fr[:nf])] + [(f"rank {r}", fr[nf * (r + 1): nf * (r + 2)]) for r in range(P)]
-    kern = fr[0]["trace"]["Kernel_Name"].split("(")[0]
-    print(f"| {kern.replace('void ', '')}: | trace kernel us | queue pass us | order us | frame span us | grid |")
-    print("|---|---|---|---|---|---|")
+    print("| frames | trace kernel | trace kernel us | queue pass us | order us | frame span us | grid |")
+    print("|---|---|---|---|---|---|---|")
     spans = []
     for name, g in groups:
         g = g[drop:]
@@ -52,7 +51,8 @@ def main():
         if name != "full":
             spans.append(sp)
         grid = int(g[0]["trace"]["Grid_Size_X"]) // int(g[0]["trace"]["Workgroup_Size_X"])
-        print(f"| {name} | {tr:.1f} | {q:.1f} | {o:.1f} | {sp:.1f} | {grid} blocks |")
+        kern = g[0]["trace"]["Kernel_Name"].split("(")[0].replace("void ", "").replace("rt::", "")
+        print(f"| {name} | `{kern}` | {tr:.1f} | {q:.1f} | {o:.1f} | {sp:.1f} | {grid} x {g[0]['trace']['Workgroup_Size_X']} |")
     print(f"\nmax rank span {max(spans):.1f} us, mean {np.mean(spans):.1f} us")
 
 
