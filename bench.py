@@ -401,38 +401,42 @@ def build_stage_rooflines(pmc, n):
     return out or None
 
 
-def other_config(R, S, key, torch, dev, steps=8, warmup=2, pmc_json=None, emulate=False):
+def other_config(R, S, key, torch, dev, steps=20, warmup=3, pmc_json=None, emulate=False):
     """One N=1 line for another BASELINE config (untimed by the step
-    contract): build + full-frame trace, static camera, with its row-major
-    (cold) time and the kernel's own byte rate."""
+    contract): build + full-frame trace per step on the same orbiting camera
+    as the headline (so it is the frame `bench.py --only-timed --config k`
+    profiles: profiles/pmc_summary.json), with its row-major (cold) time and
+    the kernel's own byte rate (its record/triangle counters averaged over
+    the timed cameras)."""
     cfg = S.CONFIGS[key]
     view = S.VIEWS[cfg.scene]
     w, h, spp = cfg.w, cfg.h, cfg.spp
     scene = make_scene(R, S, cfg)
     scene.set_device(dev.index or 0)
-    cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+    cams = [R.camera_look_at(orbit_view(view, i), view.at, view.up, view.vfov, w, h) for i in range(warmup + steps)]
     img = torch.zeros(w * h, dtype=torch.int32, device=dev)
     hits = torch.empty(w * h * spp * 4, dtype=torch.float32, device=dev)
     b, t = [], []
     for i in range(warmup + steps):
         bm = scene.build()
-        tm = scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
+        tm = scene.render_device(cams[i], w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(), timed=True)
         if i >= warmup:
             b.append(bm)
             t.append(tm)
     R.config_set("trace.tile_order", 0)
-    cold = float(np.median([scene.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(),
-                                                timed=True) for _ in range(4)]))
+    cold = float(np.median([scene.render_device(c, w, h, spp, d_rgba=img.data_ptr(), d_hits=hits.data_ptr(),
+                                                timed=True) for c in cams[warmup:warmup + 4]]))
     R.config_set("trace.tile_order", 1)
-    wk = scene.render_work(cam, w, h, spp)
+    wks = [scene.render_work(c, w, h, spp) for c in cams[warmup::max(1, steps // 4)]]
     rays = w * h * spp
-    kb = 64.0 * float(wk[0]) + 48.0 * float(wk[1]) + 16.0 * rays + 4.0 * w * h
+    kb = float(np.mean([64.0 * float(wk[0]) + 48.0 * float(wk[1]) for wk in wks])) + 16.0 * rays + 4.0 * w * h
     tr, bd = float(np.mean(t)), float(np.mean(b))
     del img, hits
     emu = rank_emulation(R, S, scene, key, torch, dev) if emulate else None
     scene.close()
     pmc = load_pmc(pmc_json, cfg.name, 1) if pmc_json else None
     return {"workload": f"{cfg.name} {w}x{h}x{spp} (BASELINE.json configs[{key - 1}])", "n_tris": cfg.n,
+            "camera": f"orbiting {ORBIT_DEG} deg/step, {steps} timed steps after {warmup} (the profiled frames)",
             "roofline": roofline_of(kb, tr, pmc),
             "pmc_source": (os.path.relpath(pmc_json, ROOT) + f" [{pmc.get('tree', '?')}]") if pmc else None,
             "n_gpus": 1, "value": round(rays / (tr * 1e-3) / 1e6, 2), "unit": "Mrays/s",
