@@ -170,6 +170,7 @@ struct TraceConfig {
     uint32_t wg_tiles = 64;     // same, for one rank's tiles of a multi-GPU frame (nranks > 1)
     uint32_t nt_hits = 1;       // nontemporal hit-record stores: 1 = frames of >= 2 spp (default), 2 = always,
                                 // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged)
+    uint32_t sl_fold = 1;       // k_trace_sl full frames: 1 = block 0 sorts the next frame's tile order (no k_tile_order)
     uint32_t sl_mtf = 1;        // k_trace_sl on one rank's tiles: 1 = Moller-Trumbore before the leaf box test
     uint32_t spp_lanes = 2;     // samples in lanes (k_trace_sl) for 2..16 (power of two) spp: 2 = full frames and
                                 // one rank's tiles (default), 1 = tiles only, 0 = off (a lane loops over its samples)

@@ -843,6 +843,76 @@ __device__ __forceinline__ void tile_order_block(uint32_t* __restrict__ cost, ui
     }
 }
 
+// The same counting sort for any nb (no per-thread bucket registers): pass 1
+// folds the running mean and builds the histogram, pass 2 re-derives each
+// tile's bucket from the mean it stored (ema[i], or the cost itself without
+// one: the map read is not written while this runs) and clears the cost.
+// Used by the samples-in-lanes full frames (4K: 32400 tiles), loads batched
+// by UNR per thread so a pass is nb / (NTH * UNR) memory round trips.
+template <int NTH, int UNR>
+__device__ __forceinline__ void tile_order_loop(uint32_t* __restrict__ cost, uint32_t nb,
+                                                uint32_t* __restrict__ order, uint32_t* s_hist, uint32_t* s_sum,
+                                                uint32_t* __restrict__ ema) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    for (uint32_t j = tid; j < 256; j += NTH) s_hist[j] = 0u;
+    __syncthreads();
+    for (uint32_t i0 = tid; i0 < nb; i0 += NTH * UNR) {
+        uint32_t c[UNR], m[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t i = i0 + u * NTH;
+            c[u] = i < nb ? cost[i] : 0u;
+            m[u] = i < nb && ema ? ema[i] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t i = i0 + u * NTH;
+            if (i < nb) {
+                uint32_t k = c[u];
+                if (ema) {
+                    k = (uint32_t)(((uint64_t)m[u] + k) >> 1);
+                    ema[i] = k;
+                }
+                atomicAdd(&s_hist[255u - cost_bucket(k)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    // exclusive scan of 256 buckets: 4 waves of 64 (as tile_order_block)
+    static_assert(NTH >= 256, "one thread per bucket");
+    const uint32_t hv = tid < 256 ? s_hist[tid] : 0u;
+    uint32_t hx = hv;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(hx, o, 64);
+        if (lane >= (uint32_t)o) hx += y;
+    }
+    if (tid < 256 && lane == 63) s_sum[wv] = hx;
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t pre = 0;
+        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
+        s_hist[tid] = pre + hx - hv;
+    }
+    __syncthreads();
+    for (uint32_t i0 = tid; i0 < nb; i0 += NTH * UNR) {
+        uint32_t k[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t i = i0 + u * NTH;
+            k[u] = i < nb ? (ema ? ema[i] : cost[i]) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+            const uint32_t i = i0 + u * NTH;
+            if (i < nb) {
+                order[atomicAdd(&s_hist[255u - cost_bucket(k[u])], 1u)] = i;
+                cost[i] = 0u;
+            }
+        }
+    }
+}
+
 // Full frames: the next frame's tile order sorted by one extra block of
 // this frame's k_trace (the grid's last block, dispatched when the frame's
 // tail is already running) from the previous frame's costs folded into the
@@ -1096,12 +1166,28 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
                                                                  float4* __restrict__ hits, uint32_t* __restrict__ rgba,
                                                                  const uint32_t* __restrict__ order,
                                                                  uint32_t* __restrict__ cost_out, uint32_t coop_cap,
-                                                                 CoopQ cq, uint32_t nt_hits) {
+                                                                 CoopQ cq, uint32_t nt_hits,
+                                                                 OrderFold fold = OrderFold{}) {
     using SH = SlShape<S>;
     constexpr uint32_t kStackWords = (StackOf<4, NT>::v + 1) * NT;
     __shared__ uint32_t s_ref[kStackWords];
     __shared__ uint16_t s_tn[kStackWords];
-    const uint32_t gw = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);  // global unit (wave) id
+    // full frames: block 0 sorts the next frame's tile order (OrderFold) and
+    // the units start at block 1.  The first block rather than the last: a
+    // 4K map takes this block tens of us, hidden under the frame's bulk, not
+    // added to its tail.
+    uint32_t bid = blockIdx.x;
+    if constexpr (!PACKED && NT == 256) {
+        if (fold.out) {
+            if (bid == 0) {  // uniform: the whole block sorts and leaves
+                static_assert(kStackWords >= 256 + 16, "tile_order_loop's LDS");
+                tile_order_loop<256, 8>(fold.cost, fold.nb, fold.out, s_ref, s_ref + 256, fold.ema);
+                return;
+            }
+            --bid;
+        }
+    }
+    const uint32_t gw = bid * (NT / 64) + (threadIdx.x >> 6);  // global unit (wave) id
     const uint32_t ti = gw / SH::UPT, q = gw % SH::UPT;
     const uint32_t slot = order ? order[ti] : ti;
     const uint32_t t = rank + slot * nranks;
@@ -2371,8 +2457,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     const uint32_t sl_cap = !sl || !hits || !sched || !sched->coop_q ? 0u
                             : coop_cap_for_sl(nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap);
     const uint32_t coop_cap = sl ? sl_cap : coop_cap0;
+    // (k_trace's extra block holds its costs in registers: nb <= 8192; k_trace_sl's block 0 loops, any nb)
     const bool can_fold = RT_ORDER_FOLD && sched && nranks == 1 && !packed && !small && wide && !counters &&
-                          !cfg.order_override && coop_cap == 0 && nb <= 256 * kFoldPerThread && !sl;
+                          !cfg.order_override && coop_cap == 0 &&
+                          (sl ? cfg.sl_fold != 0 : nb <= 256 * kFoldPerThread);
     OrderFold fold;
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
@@ -2462,15 +2550,15 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     }
     if (sl) {
         const uint32_t nt = small ? 64u : 256u;
-        const uint32_t grid = (uint32_t)((uint64_t)nb * 4 * spp / (nt / 64));
+        const uint32_t grid = (uint32_t)((uint64_t)nb * 4 * spp / (nt / 64)) + (fold.out ? 1u : 0u);
         const uint32_t wc = stack_cap_for(cfg, 4, nt);
 #define RT_SL(P, NT, S_)                                                                                           \
     if (P && !cfg.sl_mtf)                                                                                          \
         RT_KLAUNCH((k_trace_sl<P, NT, S_, false>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, \
-                   h, rank, nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits);                          \
+                   h, rank, nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits, fold);                    \
     else                                                                                                           \
         RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
-                   nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits)
+                   nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits, fold)
 #define RT_SL_S(P, NT)                  \
     switch (spp) {                      \
         case 2: RT_SL(P, NT, 2); break;   \

@@ -186,3 +186,31 @@ def test_spp_lanes_equals_loop_kernel(R, cfg):
             assert np.array_equal(outs[0][r][1], outs[1][r][1]), r
         assert np.array_equal(full[0][0], full[2][0])
         assert np.array_equal(full[0][1], full[2][1])
+
+
+def test_spp_lanes_folded_order_large_frames(R, cfg):
+    """k_trace_sl full frames sort the next frame's tile order in their block
+    0 (trace.sl_fold, a loop over any tile count): 9216 tiles, five frames
+    (the order is sorted in frame 2 on, used from frame 3), each identical to
+    the loop kernel's frame -- a tile the order dropped or repeated would
+    leave its pixels unwritten (device-only comparison)."""
+    import torch
+    w, h, spp = 2048, 1152, 2
+    cam = _cam(R, w, h)
+    with R.Scene.generate_soup(300_000, 3) as s:
+        s.build()
+        ref = None
+        for mode, fold in ((0, 1), (2, 0), (2, 1)):
+            cfg("trace.spp_lanes", mode, 2)
+            cfg("trace.sl_fold", fold, 1)
+            for f in range(5):
+                img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+                hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
+                s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr())
+                torch.cuda.synchronize()
+                got = (img.cpu().numpy().copy(), hb.cpu().numpy().view(np.uint32).copy())
+                if ref is None:
+                    ref = got
+                    assert np.count_nonzero(ref[0]) == w * h  # alpha 255 everywhere
+                assert np.array_equal(got[0], ref[0]), (mode, fold, f)
+                assert np.array_equal(got[1], ref[1]), (mode, fold, f)

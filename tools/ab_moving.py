@@ -2,7 +2,8 @@
 headline workload: soup-1M 1080p, eye orbiting 0.25 deg per frame), full
 frames on one GPU; each configuration renders the whole sequence in turn,
 interleaved over rounds; reports the mean event-timed trace per frame.
-usage: python tools/ab_moving.py [rounds] [frames] name:knob=v,knob=v ...  (or name@knob=v,...)"""
+usage: python tools/ab_moving.py [rounds] [frames] name:knob=v,knob=v ...  (or name@knob=v,...)
+AB_CONFIG=<k> runs BASELINE configs[k-1] (its scene and frame shape) instead of 3."""
 import os
 import sys
 
@@ -21,10 +22,10 @@ configs = [("base", {})]
 for a in sys.argv[3:]:
     name, kv = a.split(":", 1) if ":" in a else a.split("@", 1)
     configs.append((name, {k: int(v) for k, v in (x.split("=") for x in kv.split(",") if x)}))
-cfg = S.CONFIGS[3]
+cfg = S.CONFIGS[int(os.environ.get("AB_CONFIG", "3"))]
 view = S.VIEWS[cfg.scene]
 w, h, spp = cfg.w, cfg.h, cfg.spp
-scene = R.Scene.generate_soup(1_000_000, 1)
+scene = bench.make_scene(R, S, cfg)
 scene.build()
 cams = [R.camera_look_at(bench.orbit_view(view, i), view.at, view.up, view.vfov, w, h) for i in range(frames + 2)]
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
@@ -46,7 +47,8 @@ for _ in range(rounds):
         res[name].append(float(np.mean(t)))
         for k in kv:  # back to the library defaults
             R.config_set(k, {"trace.coop_cap": -1, "trace.tile_order": 1, "trace.px_sort": 1, "trace.wg": 256,
-                             "trace.buf_loads": 1, "trace.coop_lanes": 32, "trace.coop_cap_tiles": -1}.get(k, 0))
+                             "trace.buf_loads": 1, "trace.coop_lanes": 32, "trace.coop_cap_tiles": -1,
+                             "trace.spp_lanes": 2, "trace.sl_fold": 1, "trace.sl_mtf": 1, "trace.nt_hits": 1}.get(k, 0))
 for name, _ in configs:
     print(f"{name:<22s} mean trace {np.median(res[name]):.4f} ms  (rounds: {' '.join(f'{x:.4f}' for x in res[name])})",
           flush=True)
