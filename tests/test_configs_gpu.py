@@ -29,6 +29,7 @@ def _tiled_image(R, s, cam, w, h, spp, P):
     import torch
     tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
     slabs = torch.zeros((P, max(tmax, 1) * 256), dtype=torch.int32, device="cuda")
+    torch.cuda.synchronize()  # the zero fill (torch's stream) before the scene's stream writes
     for r in range(P):
         s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr())
     s.sync()

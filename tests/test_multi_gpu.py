@@ -148,6 +148,7 @@ def test_caller_stream_ordering(R, oracle):
     _, er = _oracle_frame(oracle, tris, w, h, spp)
     a, b = torch.cuda.Stream(), torch.cuda.Stream()
     img = [torch.zeros(w * h, dtype=torch.int32, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()  # the zero fill (torch's stream) before the scene's stream writes
     s = R.Scene.from_soup(tris)
     s.build()
     cam = _cam(R, w, h)

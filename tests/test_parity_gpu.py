@@ -483,6 +483,7 @@ def test_tiled_render_matches_full(R, oracle):
         for P in (1, 2, 3, 8):
             tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
             slabs = torch.zeros((P, max(tmax, 1) * 256), dtype=torch.int32, device="cuda")
+            torch.cuda.synchronize()  # the zero fill (torch's stream) before the scene's stream writes
             for r in range(P):
                 s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr())
             s.sync()
@@ -571,6 +572,7 @@ def _successive_frames(R, oracle, s_tris, exp):
             R.config_set("trace.wg_tiles", wg)
             try:
                 slabs = torch.zeros((P, tmax * 256), dtype=torch.int32, device="cuda")
+                torch.cuda.synchronize()  # the zero fill (torch's stream) before the scene's stream writes
                 for r in range(P):
                     first = None
                     for frame in range(3):

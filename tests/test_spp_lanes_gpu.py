@@ -166,6 +166,7 @@ def test_spp_lanes_equals_loop_kernel(R, cfg):
                 nb = R.tiles_for_rank(w, h, r, P)
                 slab = torch.zeros(nb * 256, dtype=torch.int32, device="cuda")
                 sh = torch.zeros(nb * 256 * spp * 4, dtype=torch.float32, device="cuda")
+                torch.cuda.synchronize()  # the zero fills, before the scene's stream writes
                 for _ in range(2):
                     s.render_tiles_device(cam, w, h, spp, r, P, slab.data_ptr(), sh.data_ptr())
                 torch.cuda.synchronize()
@@ -176,6 +177,7 @@ def test_spp_lanes_equals_loop_kernel(R, cfg):
             R.config_set("trace.spp_lanes", mode)
             img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
             hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
+            torch.cuda.synchronize()
             for _ in range(2):
                 s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr())
             torch.cuda.synchronize()
@@ -206,7 +208,9 @@ def test_spp_lanes_folded_order_large_frames(R, cfg):
             for f in range(5):
                 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
                 hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
-                s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr())
+                # on torch's stream, behind the zero fills (the scene's own stream would not wait for them)
+                s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr(),
+                                stream=torch.cuda.current_stream().cuda_stream)
                 torch.cuda.synchronize()
                 got = (img.cpu().numpy().copy(), hb.cpu().numpy().view(np.uint32).copy())
                 if ref is None:
