@@ -208,13 +208,30 @@ def test_spp_lanes_folded_order_large_frames(R, cfg):
             for f in range(5):
                 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
                 hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
-                # on torch's stream, behind the zero fills (the scene's own stream would not wait for them)
-                s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr(),
-                                stream=torch.cuda.current_stream().cuda_stream)
+                # the zero fills run on torch's stream, which the scene's stream does not wait for (and
+                # torch's default stream has handle 0, i.e. "the scene's stream" to render_device)
+                torch.cuda.synchronize()
+                s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr())
                 torch.cuda.synchronize()
                 got = (img.cpu().numpy().copy(), hb.cpu().numpy().view(np.uint32).copy())
                 if ref is None:
                     ref = got
                     assert np.count_nonzero(ref[0]) == w * h  # alpha 255 everywhere
-                assert np.array_equal(got[0], ref[0]), (mode, fold, f)
-                assert np.array_equal(got[1], ref[1]), (mode, fold, f)
+                if not np.array_equal(got[0], ref[0]):
+                    d = np.nonzero(got[0] != ref[0])[0]
+                    tiles = np.unique((d // w // 16) * 128 + (d % w) // 16)
+                    pytest.fail(f"mode {mode} fold {fold} frame {f}: {d.size} pixels differ in {tiles.size} tiles "
+                                f"{tiles[:8].tolist()}; first {[(int(p % w), int(p // w)) for p in d[:6]]}: got "
+                                f"{[hex(int(v) & 0xFFFFFFFF) for v in got[0][d[:6]]]} expected "
+                                f"{[hex(int(v) & 0xFFFFFFFF) for v in ref[0][d[:6]]]}; hit records of the first: got "
+                                f"{got[1].reshape(-1, 4)[d[0] * spp:(d[0] + 1) * spp].tolist()} expected "
+                                f"{ref[1].reshape(-1, 4)[d[0] * spp:(d[0] + 1) * spp].tolist()}")
+                if not np.array_equal(got[1], ref[1]):
+                    d = np.nonzero(got[1] != ref[1])[0]
+                    rec = np.unique(d // 4)
+                    px = rec // spp
+                    pytest.fail(f"mode {mode} fold {fold} frame {f}: {d.size} words in {rec.size} hit records differ "
+                                f"(fields {np.bincount(d % 4, minlength=4).tolist()}); first records "
+                                f"{[(int(r), int(p % w), int(p // w)) for r, p in zip(rec[:6], px[:6])]}: got "
+                                f"{got[1].reshape(-1, 4)[rec[:3]].tolist()} expected {ref[1].reshape(-1, 4)[rec[:3]].tolist()}; "
+                                f"distinct tiles {np.unique((px // w // 16) * 128 + (px % w) // 16).size}")
