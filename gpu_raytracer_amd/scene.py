@@ -38,6 +38,20 @@ def camera_array(cam: rt_camera) -> np.ndarray:
     return np.array([list(cam.eye), list(cam.w00), list(cam.du), list(cam.dv)], dtype=np.float32)
 
 
+# hipStreamLegacy: the HIP null stream.  Stream handles are ints as torch
+# gives them (torch.cuda.current_stream().cuda_stream), and torch's default
+# stream IS the null stream, handle 0 -- which the C ABI's NULL would read as
+# "the scene's own stream", unordered with the caller's work.  So None selects
+# the scene's stream and an explicit 0 the null stream.
+HIP_STREAM_LEGACY = 1
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    return C.c_void_p(int(stream) if int(stream) != 0 else HIP_STREAM_LEGACY)
+
+
 @dataclass
 class BuildTimes:
     bounds: float
@@ -203,12 +217,12 @@ class Scene:
         return hb, rb, ms.value
 
     def render_shadow_device(self, cam, w, h, spp, light, ambient, d_rgba: int = 0, d_hits: int = 0,
-                             stream: int = 0, timed: bool = False):
+                             stream: int | None = None, timed: bool = False):
         L = np.ascontiguousarray(light, np.float32).reshape(3)
         ms = C.c_double()
         call("rt_render_shadow_device", self._h, C.byref(cam), _p(L), float(ambient), w, h, spp,
              C.c_void_p(d_hits) if d_hits else None, C.c_void_p(d_rgba) if d_rgba else None,
-             C.c_void_p(stream) if stream else None, C.byref(ms) if timed else None)
+             _stream(stream), C.byref(ms) if timed else None)
         return ms.value if timed else None
 
     def render_shadow_work(self, cam, w, h, spp, light, ambient) -> np.ndarray:
@@ -229,12 +243,12 @@ class Scene:
         return hb, rb, ms.value
 
     def render_path_device(self, cam, w, h, spp, light, sky, max_depth, d_rgba: int = 0, d_hits: int = 0,
-                           stream: int = 0, timed: bool = False):
+                           stream: int | None = None, timed: bool = False):
         L = np.ascontiguousarray(light, np.float32).reshape(3)
         ms = C.c_double()
         call("rt_render_path_device", self._h, C.byref(cam), _p(L), float(sky), int(max_depth), w, h, spp,
              C.c_void_p(d_hits) if d_hits else None, C.c_void_p(d_rgba) if d_rgba else None,
-             C.c_void_p(stream) if stream else None, C.byref(ms) if timed else None)
+             _stream(stream), C.byref(ms) if timed else None)
         return ms.value if timed else None
 
     def render_path_work(self, cam, w, h, spp, light, sky, max_depth) -> np.ndarray:
@@ -301,12 +315,14 @@ class Scene:
         call("rt_render_work", self._h, C.byref(cam), w, h, spp, _p(c))
         return c
 
-    def render_device(self, cam, w, h, spp, d_rgba: int = 0, d_hits: int = 0, stream: int = 0,
+    def render_device(self, cam, w, h, spp, d_rgba: int = 0, d_hits: int = 0, stream: int | None = None,
                       timed: bool = False):
-        """Full-image render into device buffers (device pointers as ints)."""
+        """Full-image render into device buffers (device pointers as ints) on
+        `stream` (None: the scene's own stream; an int handle, 0 = the null
+        stream, e.g. torch.cuda.current_stream().cuda_stream)."""
         ms = C.c_double()
         call("rt_render_device", self._h, C.byref(cam), w, h, spp, C.c_void_p(d_hits) if d_hits else None,
-             C.c_void_p(d_rgba) if d_rgba else None, C.c_void_p(stream) if stream else None,
+             C.c_void_p(d_rgba) if d_rgba else None, _stream(stream),
              C.byref(ms) if timed else None)
         return ms.value if timed else None
 
@@ -330,10 +346,10 @@ class Scene:
         return out
 
     def render_tiles_device(self, cam, w, h, spp, rank, nranks, d_rgba: int, d_hits: int = 0,
-                            stream: int = 0, timed: bool = False):
+                            stream: int | None = None, timed: bool = False):
         ms = C.c_double()
         call("rt_render_tiles_device", self._h, C.byref(cam), w, h, spp, rank, nranks, C.c_void_p(d_rgba),
-             C.c_void_p(d_hits) if d_hits else None, C.c_void_p(stream) if stream else None,
+             C.c_void_p(d_hits) if d_hits else None, _stream(stream),
              C.byref(ms) if timed else None)
         return ms.value if timed else None
 

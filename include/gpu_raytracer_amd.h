@@ -210,14 +210,16 @@ rt_status rt_render_work(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t
                          uint32_t spp, uint64_t counters_out[2]);
 /* Device-resident render of the full image into caller device buffers
  * (d_hits: w*h*spp records or NULL; d_rgba: w*h*4 bytes or NULL) on `stream`
- * (NULL = the scene's stream).  Asynchronous unless ms_out != NULL, in which
- * case the trace kernel is bracketed by hipEvents and waited for. */
+ * (NULL = the scene's own non-blocking stream, unordered with the caller's
+ * other work; the HIP null stream, e.g. torch's default stream, is selected
+ * with hipStreamLegacy, (void*)1).  Asynchronous unless ms_out != NULL, in
+ * which case the trace kernel is bracketed by hipEvents and waited for. */
 rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, uint32_t spp,
                            void* d_hits, void* d_rgba, void* stream, double* ms_out);
 
 /* ---- image-tile sharding: 16x16-pixel tiles, tile t goes
- * to rank t mod nranks.  Device pointers; stream = hipStream_t or NULL for the
- * scene's stream.  packed_rgba: rt_tiles_for_rank() * 1024 bytes;
+ * to rank t mod nranks.  Device pointers; stream = hipStream_t (hipStreamLegacy
+ * for the null stream) or NULL for the scene's stream.  packed_rgba: rt_tiles_for_rank() * 1024 bytes;
  * packed_hits (nullable): tiles * 256 * spp records. */
 uint32_t rt_tiles_for_rank(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks);
 rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h,

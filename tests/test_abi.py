@@ -311,3 +311,13 @@ def test_wide8_size_cap():
         m = re.search(r"#define RT_WIDE8_MAX_N (\d+)u", f.read())
     cap = int(m.group(1))
     assert (cap - 1) * 96 <= 2**32 - 1 < cap * 96
+
+
+def test_stream_handles():
+    """Python stream arguments: None = the scene's own stream (NULL), an
+    explicit 0 (torch's default stream) = the HIP null stream
+    (hipStreamLegacy), any other handle passed through."""
+    from gpu_raytracer_amd.scene import HIP_STREAM_LEGACY, _stream
+    assert _stream(None) is None
+    assert _stream(0).value == HIP_STREAM_LEGACY == 1
+    assert _stream(0xABC0).value == 0xABC0

@@ -160,3 +160,32 @@ def test_caller_stream_ordering(R, oracle):
     torch.cuda.synchronize()
     for i in range(4):
         assert np.array_equal(img[i].cpu().numpy().view(np.uint8), er), i
+
+
+def test_default_stream_handle_is_the_null_stream(R, oracle):
+    """torch's default stream has handle 0, which the C ABI's NULL would read
+    as the scene's own (non-blocking) stream: the Python layer passes an
+    explicit 0 as hipStreamLegacy, so a render on
+    torch.cuda.current_stream().cuda_stream runs after torch's zero fills of
+    its buffers and before torch's reads of them -- no host sync in between
+    (bench.py's N > 1 frame queues trace, RCCL gather and unpack this way)."""
+    import torch
+    tris = oracle.soup(40000, 8).reshape(-1, 9)
+    w, h, spp = 640, 360, 2
+    eh, er = _oracle_frame(oracle, tris, w, h, spp)
+    cur = torch.cuda.current_stream()
+    assert cur.cuda_stream == 0  # the case this test is about
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        cam = _cam(R, w, h)
+        for _ in range(3):
+            img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+            hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
+            s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), d_hits=hb.data_ptr(), stream=cur.cuda_stream)
+            img2, hb2 = img.clone(), hb.clone()  # torch's reads, queued behind the render
+            img.fill_(0)
+            hb.fill_(0)
+            torch.cuda.synchronize()
+            assert np.array_equal(img2.cpu().numpy().view(np.uint8), er)
+            prim = hb2.view(-1, 4)[:, 3].view(torch.int32).cpu().numpy().view(np.uint32)
+            assert np.array_equal(prim, eh["prim"])
