@@ -189,3 +189,30 @@ def test_default_stream_handle_is_the_null_stream(R, oracle):
             assert np.array_equal(img2.cpu().numpy().view(np.uint8), er)
             prim = hb2.view(-1, 4)[:, 3].view(torch.int32).cpu().numpy().view(np.uint32)
             assert np.array_equal(prim, eh["prim"])
+
+
+def test_tiles_on_the_null_stream(R, oracle):
+    """bench.py's N > 1 frame: rt_render_tiles_device on torch's default
+    stream (handle 0 -> hipStreamLegacy), then an unpack on the same stream,
+    no host sync between -- for three ranks of a P = 3 frame, three frames
+    each (tile order, heavy-ray queue): the unpacked image == the oracle's."""
+    import torch
+    tris = oracle.soup(40000, 9).reshape(-1, 9)
+    w, h, spp, P = 250, 138, 1, 3
+    _, er = _oracle_frame(oracle, tris, w, h, spp)
+    cur = torch.cuda.current_stream()
+    tmax = max(R.tiles_for_rank(w, h, r, P) for r in range(P))
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        cam = _cam(R, w, h)
+        for _ in range(3):
+            slabs = torch.zeros((P, tmax * 256), dtype=torch.int32, device="cuda")
+            hits = torch.zeros((P, tmax * 256 * spp * 4), dtype=torch.float32, device="cuda")
+            for r in range(P):
+                s.render_tiles_device(cam, w, h, spp, r, P, slabs[r].data_ptr(), hits[r].data_ptr(),
+                                      stream=cur.cuda_stream)
+            img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
+            R.unpack_tiles_device(slabs.data_ptr(), tmax, w, h, P, img.data_ptr(), 0, cur.cuda_stream)
+            got = img.clone()
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint8), er)

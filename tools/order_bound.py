@@ -23,8 +23,7 @@ s = R.Scene.generate_soup(1_000_000, 1)
 s.build()
 cams = [R.camera_look_at(bench.orbit_view(view, i), view.at, view.up, view.vfov, w, h) for i in range(frames + 2)]
 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
-res = {"stale": [], "same_cam": [], "same_cam_tiles_only": [], "row_major": [], "stale_steps": [],
-       "same_cam_steps": []}
+res = {"stale": [], "same_cam": [], "same_cam_tiles_only": [], "row_major": []}
 for _ in range(rounds):
     R.config_set("trace.tile_order", 1)
     for c in cams[:2]:
@@ -45,19 +44,6 @@ for _ in range(rounds):
     R.config_set("trace.tile_order", 0)
     res["row_major"].append(np.mean([s.render_device(c, w, h, spp, d_rgba=img.data_ptr(), timed=True) for c in cams[2:]]))
     R.config_set("trace.tile_order", 1)
-    R.config_set("trace.order_steps", 1)  # tile costs = the waves' largest lane step counts
-    for c in cams[:2]:
-        s.render_device(c, w, h, spp, d_rgba=img.data_ptr(), timed=True)
-    res["stale_steps"].append(np.mean([s.render_device(c, w, h, spp, d_rgba=img.data_ptr(), timed=True)
-                                       for c in cams[2:]]))
-    R.config_set("trace.px_sort", 0)
-    t = []
-    for c in cams[2:]:
-        s.render_device(c, w, h, spp, d_rgba=img.data_ptr(), timed=True)
-        t.append(s.render_device(c, w, h, spp, d_rgba=img.data_ptr(), timed=True))
-    res["same_cam_steps"].append(np.mean(t))
-    R.config_set("trace.px_sort", 1)
-    R.config_set("trace.order_steps", 0)
     R.config_set("trace.tile_order", 1)
 for k, v in res.items():
     print(f"{k:10s} {np.median(v):.4f} ms  (rounds: {' '.join(f'{x:.4f}' for x in v)})", flush=True)
