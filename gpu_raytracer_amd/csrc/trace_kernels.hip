@@ -550,8 +550,8 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// A hit record store.  nt (trace.nt_hits): nontemporal -- a multi-spp
-// frame's hit records (530 MB at 4Kx4 or 1080p x 16) stream to HBM while the
+// A hit record store.  nt (trace.nt_hits): nontemporal -- a frame's hit
+// records (530 MB at 4Kx4 or 1080p x 16, 33 MB at 1080p1) stream to HBM while the
 // trace, which uses a few % of HBM bandwidth, runs, instead of staying dirty
 // in L2 / the MALL until the next build's soup read evicts them (DESIGN.md
 // "(d)", the 10M K0 read floor).
@@ -2531,7 +2531,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
     const bool buf = n <= kBufMaxN && cfg.buf_loads;
-    // nontemporal hit records: trace.nt_hits 1 = frames of >= 2 spp, 2 = always, 0 = never; 3 = multi-spp
+    // nontemporal hit records: trace.nt_hits 2 = always (default), 1 = frames of >= 2 spp, 0 = never; 3 = multi-spp
     // hits and RGBA (A/B: the kernels' nt_hits > 1 also streams the RGBA stores)
     const uint32_t nt_hits = (cfg.nt_hits == 2 || ((cfg.nt_hits == 1 || cfg.nt_hits == 3) && spp >= 2))
                                  ? (cfg.nt_hits == 3 ? 2u : 1u) : 0u;
