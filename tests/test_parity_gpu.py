@@ -660,3 +660,28 @@ def test_crossing_ranges_at_group_boundaries(R, oracle):
     lf = nodes[n - 1:]
     assert np.array_equal(lf["a"], vals) and np.array_equal(lf["esc"], esc[n - 1:])
     assert np.array_equal(bits(lf["lo"]), bits(blo)) and np.array_equal(bits(lf["hi"]), bits(bhi))
+
+
+@pytest.mark.parametrize("spp", [1, 2])
+def test_hit_store_modes(R, oracle, spp):
+    """trace.nt_hits 0 (plain stores), 1 (nontemporal for >= 2 spp), 2 (all
+    frames, the default), 3 (hits and RGBA): the same hits and image."""
+    from gpu_raytracer_amd.scenes import SOUP_VIEW
+    tris = soup(oracle, 30000, 44)
+    exp = oracle.build(tris)
+    w, h = 130, 74
+    ocam = oracle.camera_look_at(SOUP_VIEW.eye, SOUP_VIEW.at, SOUP_VIEW.up, SOUP_VIEW.vfov, w, h)
+    eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
+    er = oracle.shade(eh, w, h, spp)
+    try:
+        with R.Scene.from_soup(tris) as s:
+            s.build()
+            cam = _cam(R, SOUP_VIEW, w, h)
+            for mode in (0, 1, 2, 3):
+                R.config_set("trace.nt_hits", mode)
+                hits, rgba, _ = s.render(cam, w, h, spp)
+                assert np.array_equal(rgba, er), mode
+                for f in ("t", "u", "v", "prim"):
+                    assert np.array_equal(bits(hits[f]), bits(eh[f])), (mode, f)
+    finally:
+        R.config_set("trace.nt_hits", 2)
