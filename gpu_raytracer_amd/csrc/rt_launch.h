@@ -171,7 +171,8 @@ struct TraceConfig {
     uint32_t nt_hits = 2;       // nontemporal hit-record stores: 2 = always (default), 1 = frames of >= 2 spp,
                                 // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged;
                                 // the 1M build after a 1080p1 frame 140.3 -> 137.7 us, profiles/ab_nt_hits_1spp_r05.log)
-    uint32_t sl_fold = 1;       // k_trace_sl full frames: 1 = block 0 sorts the next frame's tile order (no k_tile_order)
+    uint32_t sl_fold = 1;       // k_trace_sl (full frames, one rank's tiles): 1 = block 0 sorts the next frame's tile
+                                // order (no k_tile_order launch)
     uint32_t sl_mtf = 1;        // k_trace_sl on one rank's tiles: 1 = Moller-Trumbore before the leaf box test
     uint32_t spp_lanes = 2;     // samples in lanes (k_trace_sl) for 2..16 (power of two) spp: 2 = full frames and
                                 // one rank's tiles (default), 1 = tiles only, 0 = off (a lane loops over its samples)

@@ -878,21 +878,37 @@ __device__ __forceinline__ void tile_order_loop(uint32_t* __restrict__ cost, uin
         }
     }
     __syncthreads();
-    // exclusive scan of 256 buckets: 4 waves of 64 (as tile_order_block)
-    static_assert(NTH >= 256, "one thread per bucket");
-    const uint32_t hv = tid < 256 ? s_hist[tid] : 0u;
-    uint32_t hx = hv;
+    // exclusive scan of 256 buckets: 4 waves of 64 (as tile_order_block), or
+    // one wave of 64 with 4 consecutive buckets per lane (64-thread blocks)
+    static_assert(NTH == 64 || NTH >= 256, "one wave or >= one thread per bucket");
+    if constexpr (NTH == 64) {
+        uint32_t v[4], sum = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(hx, o, 64);
-        if (lane >= (uint32_t)o) hx += y;
-    }
-    if (tid < 256 && lane == 63) s_sum[wv] = hx;
-    __syncthreads();
-    if (tid < 256) {
-        uint32_t pre = 0;
-        for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
-        s_hist[tid] = pre + hx - hv;
+        for (int j = 0; j < 4; ++j) { v[j] = s_hist[4 * tid + j]; sum += v[j]; }
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= (uint32_t)o) x += y;
+        }
+        uint32_t run = x - sum;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { s_hist[4 * tid + j] = run; run += v[j]; }
+    } else {
+        const uint32_t hv = tid < 256 ? s_hist[tid] : 0u;
+        uint32_t hx = hv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(hx, o, 64);
+            if (lane >= (uint32_t)o) hx += y;
+        }
+        if (tid < 256 && lane == 63) s_sum[wv] = hx;
+        __syncthreads();
+        if (tid < 256) {
+            uint32_t pre = 0;
+            for (uint32_t k = 0; k < wv; ++k) pre += s_sum[k];
+            s_hist[tid] = pre + hx - hv;
+        }
     }
     __syncthreads();
     for (uint32_t i0 = tid; i0 < nb; i0 += NTH * UNR) {
@@ -1172,20 +1188,18 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
     constexpr uint32_t kStackWords = (StackOf<4, NT>::v + 1) * NT;
     __shared__ uint32_t s_ref[kStackWords];
     __shared__ uint16_t s_tn[kStackWords];
-    // full frames: block 0 sorts the next frame's tile order (OrderFold) and
-    // the units start at block 1.  The first block rather than the last: a
-    // 4K map takes this block tens of us, hidden under the frame's bulk, not
-    // added to its tail.
+    // block 0 sorts the next frame's tile order (OrderFold; full frames and
+    // one rank's tiles) and the units start at block 1.  The first block
+    // rather than the last: a 4K map takes this block tens of us, hidden
+    // under the frame's bulk, not added to its tail.
     uint32_t bid = blockIdx.x;
-    if constexpr (!PACKED && NT == 256) {
-        if (fold.out) {
-            if (bid == 0) {  // uniform: the whole block sorts and leaves
-                static_assert(kStackWords >= 256 + 16, "tile_order_loop's LDS");
-                tile_order_loop<256, 8>(fold.cost, fold.nb, fold.out, s_ref, s_ref + 256, fold.ema);
-                return;
-            }
-            --bid;
+    if (fold.out) {
+        if (bid == 0) {  // uniform: the whole block sorts and leaves
+            static_assert(kStackWords >= 256 + 16, "tile_order_loop's LDS");
+            tile_order_loop<NT, 8>(fold.cost, fold.nb, fold.out, s_ref, s_ref + 256, fold.ema);
+            return;
         }
+        --bid;
     }
     const uint32_t gw = bid * (NT / 64) + (threadIdx.x >> 6);  // global unit (wave) id
     const uint32_t ti = gw / SH::UPT, q = gw % SH::UPT;
@@ -2457,10 +2471,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     const uint32_t sl_cap = !sl || !hits || !sched || !sched->coop_q ? 0u
                             : coop_cap_for_sl(nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap);
     const uint32_t coop_cap = sl ? sl_cap : coop_cap0;
-    // (k_trace's extra block holds its costs in registers: nb <= 8192; k_trace_sl's block 0 loops, any nb)
-    const bool can_fold = RT_ORDER_FOLD && sched && nranks == 1 && !packed && !small && wide && !counters &&
-                          !cfg.order_override && coop_cap == 0 &&
-                          (sl ? cfg.sl_fold != 0 : nb <= 256 * kFoldPerThread);
+    // (k_trace's extra block holds its costs in registers: nb <= 8192, full frames; k_trace_sl's block 0
+    // loops, any nb, full frames and one rank's tiles)
+    const bool can_fold = RT_ORDER_FOLD && sched && wide && !counters && !cfg.order_override && coop_cap == 0 &&
+                          (sl ? cfg.sl_fold != 0 : nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread);
     OrderFold fold;
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)

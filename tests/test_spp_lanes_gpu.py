@@ -68,14 +68,15 @@ def scene30k(oracle):
 def test_spp_lanes_tiles(R, oracle, cfg, scene30k, spp, P, cap):
     """Emulated P-rank frames through k_trace_sl: queue off (cap 0), every
     sample queued after 1 step (most pixels resolved from hits), and a cap
-    that queues a fraction; two successive frames (tile order on)."""
+    that queues a fraction; three successive frames (tile order on: with the
+    queue off, block 0 of the second frame sorts the order the third uses)."""
     w, h = 70, 45
     eh, er = _frame(oracle, scene30k, w, h, spp)
     cfg("render.emulate", 1, 0)
     cfg("trace.coop_cap_tiles", cap, -1)
     with R.Scene.from_soup(scene30k) as s:
         s.build()
-        for frame in range(2):
+        for frame in range(3):
             hits, rgba, _ = s.render(_cam(R, w, h), w, h, spp, ngpus=P)
             assert np.array_equal(rgba, er), (spp, P, cap, frame)
             assert _same_hits(hits, eh), (spp, P, cap, frame)
@@ -167,7 +168,7 @@ def test_spp_lanes_equals_loop_kernel(R, cfg):
                 slab = torch.zeros(nb * 256, dtype=torch.int32, device="cuda")
                 sh = torch.zeros(nb * 256 * spp * 4, dtype=torch.float32, device="cuda")
                 torch.cuda.synchronize()  # the zero fills, before the scene's stream writes
-                for _ in range(2):
+                for _ in range(3):  # the third frame runs the order sorted in the second's block 0
                     s.render_tiles_device(cam, w, h, spp, r, P, slab.data_ptr(), sh.data_ptr())
                 torch.cuda.synchronize()
                 got.append((slab.cpu().numpy().copy(), sh.cpu().numpy().view(np.uint32).copy()))
