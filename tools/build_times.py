@@ -4,7 +4,8 @@ usage: python tools/build_times.py [n] [reps] [key=v,key=v,...]
   from tools/build_exp.sh; default: the in-tree library, or $RT_LIB).
   $RT_CFG adds knobs the same way.  BT_TRACE=1: a 1080p frame of the soup
   (hits + RGBA written, as bench.py's step) is traced before every timed
-  build, so each build starts with the trace's data in the caches."""
+  build, so each build starts with the trace's data in the caches.
+  BT_SCENE=bunny|sponza: that BASELINE substitute scene instead of the soup (n ignored)."""
 import os
 import sys
 
@@ -28,7 +29,12 @@ import gpu_raytracer_amd as R  # noqa: E402
 R.config_set("timing.event_fence", int(os.environ.get("RT_EVENT_FENCE", "0")))
 for k, v in knobs:
     R.config_set(k, v)
-s = R.Scene.generate_soup(n, 1)
+if os.environ.get("BT_SCENE"):
+    from gpu_raytracer_amd import scenes as _S
+    s = R.Scene.from_soup(_S.tris_for(os.environ["BT_SCENE"]))
+    n = s.num_tris
+else:
+    s = R.Scene.generate_soup(n, 1)
 between = lambda: None  # noqa: E731
 if os.environ.get("BT_TRACE", "0") != "0":
     # BT_TRACE=1: the 1080p1 frame; BT_TRACE=c<k>: the frame of scenes.CONFIGS[k] (c5: 3840x2160x4)
