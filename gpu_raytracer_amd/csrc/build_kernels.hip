@@ -1877,12 +1877,14 @@ hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s) {
 // The build's sort for this n and config: 0 = the 4-pass LSB sort, 1 = the
 // MSB scatter + bucket sort, 2 = the tile-bucketed gather sort (the default).
 // A scene whose first MSB/gather build found a bucket beyond one block's LDS
-// sort (sort_mode 2 for that sort) keeps the LSB sort.
+// sort (sort_mode 2 for that sort) keeps the LSB sort; one whose gather probe
+// found clustered bins only (gather_off) moves on to the MSB sort.
 uint32_t build_sort_kind(const BuildBufs& b, uint32_t n, const TraceConfig& cfg) {
     if (n < 2 || n > kMsbBigMaxN || cfg.sort_msb == 0) return 0;
     if (cfg.sort_msb == 2 && !gather_sort_fits(n)) return 0;
-    if (b.sort_mode == 2 && b.sort_mode_of == cfg.sort_msb) return 0;
-    return cfg.sort_msb;
+    const uint32_t want = cfg.sort_msb == 2 && b.gather_off ? 1u : cfg.sort_msb;  // clustered bins: MSB
+    if (b.sort_mode == 2 && b.sort_mode_of == want) return 0;
+    return want;
 }
 
 // block shapes of K1-TB (a 4096-key tile on 512 threads x 8 triangles, or

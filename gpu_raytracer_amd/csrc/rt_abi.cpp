@@ -497,9 +497,14 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
             }
             r->times.lsb_redo = 1u;
         } else if (r->msb_probe) {  // the scene's first build with this sort ran both sorts gated on its verdict
-            const bool lsb = hf[0] != 0 || (r->msb_probe == 2 && hf[rt::kZGatherFlags - rt::kZDense] != 0);
-            r->bufs.sort_mode = lsb ? 2u : 1u;
-            r->bufs.sort_mode_of = r->msb_probe;
+            const bool dense = hf[0] != 0;
+            const bool clustered = r->msb_probe == 2 && hf[rt::kZGatherFlags - rt::kZDense] != 0;
+            if (clustered && !dense) {
+                r->bufs.gather_off = 1u;  // the next build probes the MSB sort (BuildBufs::gather_off)
+            } else {
+                r->bufs.sort_mode = dense || clustered ? 2u : 1u;
+                r->bufs.sort_mode_of = r->msb_probe;
+            }
             r->msb_probe = 0;
         }
         r->times.sort_kind = rt::build_sort_kind(r->bufs, s->n, cfg);

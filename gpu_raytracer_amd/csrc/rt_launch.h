@@ -44,6 +44,12 @@ struct BuildBufs {
     // global memory, ~10x the build); a scene's triangles never change
     uint32_t sort_mode = 0;
     uint32_t sort_mode_of = 0;  // the sort (build.sort 1 or 2) whose probe build set sort_mode
+    // the gather sort's probe found clustered bins (a bin of more than
+    // kGatherBinFast keys, ranked in O(bin^2)) but no bucket beyond its LDS:
+    // later builds use the MSB bucket sort instead, with its own verdict
+    // (its LDS radix passes have no per-bin cost; r05: the bunny substitute's
+    // 70K-tri build 105 -> 84 us, profiles/ab_gather_clustered_r05.log)
+    uint32_t gather_off = 0;
 };
 // keys one MSB bucket may hold for the LDS bucket sort at this n
 uint32_t msb_bucket_cap(uint32_t n);

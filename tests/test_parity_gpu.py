@@ -368,6 +368,28 @@ def test_clustered_scene_switches_sort(R, oracle, n, sort):
     assert max(ms) < 1.0 * n / 1e6, ms
 
 
+def test_clustered_bins_move_to_msb(R, oracle):
+    """The bunny substitute (70K triangles; the poles of its lat-long sphere
+    crowd thousands of them into a few fine cells): its gather-sort probe
+    finds clustered bins (more than 64 keys in a bin, ranked in O(bin^2)) but
+    no bucket beyond the block's LDS, so the scene moves on to the MSB bucket
+    sort (BuildBufs::gather_off), whose own probe keeps it -- every build
+    equals the oracle."""
+    from gpu_raytracer_amd import scenes as S
+    t = np.ascontiguousarray(S.tris_for("bunny"), np.float32).reshape(-1, 9)
+    exp = oracle.build(t)
+    kinds = []
+    with R.Scene.from_soup(t) as s:
+        for _ in range(3):
+            s.build()
+            kinds.append(s.build_times().sort_kind)
+            got = s.read_bvh()
+            assert np.array_equal(got["keys"], exp["keys"])
+            assert np.array_equal(got["vals"], exp["vals"])
+            assert np.array_equal(got["nodes"].view(np.uint32), exp["nodes"].view(np.uint32))
+    assert kinds == [1, 1, 1], kinds
+
+
 def test_build_repeat_and_rebuild(R, oracle):
     """Control words are re-armed between builds (zeroed per build)."""
     tris = soup(oracle, 70000, 2)
