@@ -444,7 +444,7 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
             if (first_err == RT_OK) first_err = st;
             continue;
         }
-        const uint32_t* hf = r->h_flag;  // [0] dense, [1] clustered bins, [2] bucket overflow, [5] barrier timeout
+        const uint32_t* hf = r->h_flag;  // [0] dense, [1] clustered bins, [2] bucket overflow, [3] skewed, [5] barrier timeout
         r->times.fused_fallback = 0u;
         r->times.lsb_redo = 0u;
         if (r->fused && hf[rt::kZFuseErr - rt::kZDense]) {
@@ -499,7 +499,8 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         } else if (r->msb_probe) {  // the scene's first build with this sort ran both sorts gated on its verdict
             const bool dense = hf[0] != 0;
             const bool clustered = r->msb_probe == 2 && hf[rt::kZGatherFlags - rt::kZDense] != 0;
-            if (clustered && !dense) {
+            const bool skewed = r->msb_probe == 2 && hf[rt::kZGatherSkew - rt::kZDense] != 0;
+            if ((clustered || skewed) && !dense) {
                 r->bufs.gather_off = 1u;  // the next build probes the MSB sort (BuildBufs::gather_off)
             } else {
                 r->bufs.sort_mode = dense || clustered ? 2u : 1u;

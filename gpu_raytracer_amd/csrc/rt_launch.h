@@ -45,10 +45,12 @@ struct BuildBufs {
     uint32_t sort_mode = 0;
     uint32_t sort_mode_of = 0;  // the sort (build.sort 1 or 2) whose probe build set sort_mode
     // the gather sort's probe found clustered bins (a bin of more than
-    // kGatherBinFast keys, ranked in O(bin^2)) but no bucket beyond its LDS:
-    // later builds use the MSB bucket sort instead, with its own verdict
-    // (its LDS radix passes have no per-bin cost; r05: the bunny substitute's
-    // 70K-tri build 105 -> 84 us, profiles/ab_gather_clustered_r05.log)
+    // kGatherBinFast keys, ranked in O(bin^2)) or a skewed bucket (over 4x
+    // the mean: one block sorts it while the others idle), but no bucket
+    // beyond its LDS: later builds use the MSB bucket sort instead, with its
+    // own verdict (its LDS radix passes have no per-bin cost, and it spreads
+    // a big bucket; r05: the bunny substitute's 70K-tri build 105 -> 82 us,
+    // profiles/sort_verdict_r05.log)
     uint32_t gather_off = 0;
 };
 // keys one MSB bucket may hold for the LDS bucket sort at this n
@@ -67,6 +69,7 @@ constexpr uint32_t kCrossShards = 16;
 constexpr uint32_t kZHist4 = 1056;      // [4][256] digit histograms of a probe build's LSB leg
 constexpr uint32_t kZDense = 2080;      // a probe build's verdict (k_msb_scan / k_bucket_dense write it)
 constexpr uint32_t kZGatherFlags = 2081;  // [2] k_bucket_gather: clustered bins, bucket overflow
+constexpr uint32_t kZGatherSkew = 2083;   // k_bucket_dense: the largest bucket > 4x the mean (a probe build)
 constexpr uint32_t kZEnd = 2084;        // words zeroed by K0 every build
 // past kZEnd, never zeroed by a build: the fused K0+K1's grid barrier
 // (self-resetting) and its timeout flag (cleared by the host when it sees it)

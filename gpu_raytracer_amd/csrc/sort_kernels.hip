@@ -998,10 +998,22 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
 
 // A probe build's verdict for the gather sort: 1 when some bucket holds more
 // than cap keys (the LSB sort then runs), else 0.
-__global__ __launch_bounds__(1024) void k_bucket_dense(const uint32_t* __restrict__ ghist, uint32_t cap,
+// dense[0]: a bucket beyond the gather block's LDS (the LSB leg runs);
+// dense[3]: skewed -- the largest bucket holds more than 4x the mean (and
+// over 256 keys), so one block sorts it while the others idle: the host
+// moves the scene to the MSB sort (BuildBufs::gather_off), which spreads it
+__global__ __launch_bounds__(1024) void k_bucket_dense(const uint32_t* __restrict__ ghist, uint32_t cap, uint32_t n,
                                                        uint32_t* __restrict__ dense) {
-    const int big = __syncthreads_or(ghist[threadIdx.x] > cap);
-    if (threadIdx.x == 0) dense[0] = big ? 1u : 0u;
+    __shared__ uint32_t s_max;
+    if (threadIdx.x == 0) s_max = 0u;
+    const uint32_t v = ghist[threadIdx.x];
+    const int big = __syncthreads_or(v > cap);  // (also orders s_max's init)
+    atomicMax(&s_max, v);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        dense[0] = big ? 1u : 0u;
+        dense[3] = !big && s_max > 256u && (uint64_t)s_max * kMsbBuckets > 4ull * n ? 1u : 0u;
+    }
 }
 
 // ================================================================ launchers
@@ -1178,7 +1190,7 @@ hipError_t launch_sort_gather(const uint32_t* words, const uint32_t* tb, uint32_
     if (!gather_sort_fits(n)) return hipErrorInvalidValue;
     const uint32_t nt = sort_tiles(n);
     const GatherShape gs = gather_shape(n);
-    if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), dense);
+    if (dense) RT_KLAUNCH(k_bucket_dense, dim3(1), dim3(kMsbBuckets), 0, s, ghist, (uint32_t)(gs.nt * gs.p), n, dense);
     const Gate g{dense, 0u};
     if (gs.nt * gs.p == 2048 && gs.nt == 256) return gather_launch<256, 8>(words, tb, nt, kout, vout, flags, bstart, s, g);
 #if RT_GATHER_SMALL_NT == 512

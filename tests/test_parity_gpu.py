@@ -368,15 +368,17 @@ def test_clustered_scene_switches_sort(R, oracle, n, sort):
     assert max(ms) < 1.0 * n / 1e6, ms
 
 
-def test_clustered_bins_move_to_msb(R, oracle):
+@pytest.mark.parametrize("scene", ["bunny", "sponza"])
+def test_clustered_bins_move_to_msb(R, oracle, scene):
     """The bunny substitute (70K triangles; the poles of its lat-long sphere
     crowd thousands of them into a few fine cells): its gather-sort probe
-    finds clustered bins (more than 64 keys in a bin, ranked in O(bin^2)) but
-    no bucket beyond the block's LDS, so the scene moves on to the MSB bucket
-    sort (BuildBufs::gather_off), whose own probe keeps it -- every build
-    equals the oracle."""
+    finds clustered bins (more than 64 keys in a bin, ranked in O(bin^2));
+    the Sponza substitute (262K): a skewed bucket (2048 keys against a mean
+    of 256).  Neither has a bucket beyond the block's LDS, so each scene moves
+    on to the MSB bucket sort (BuildBufs::gather_off), whose own probe keeps
+    it -- every build equals the oracle."""
     from gpu_raytracer_amd import scenes as S
-    t = np.ascontiguousarray(S.tris_for("bunny"), np.float32).reshape(-1, 9)
+    t = np.ascontiguousarray(S.tris_for(scene), np.float32).reshape(-1, 9)
     exp = oracle.build(t)
     kinds = []
     with R.Scene.from_soup(t) as s:
