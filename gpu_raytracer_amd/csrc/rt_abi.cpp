@@ -622,6 +622,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.nt_hits" && value >= 0 && value <= 3) c.nt_hits = (uint32_t)value;
     else if (k == "trace.sl_mtf" && (value == 0 || value == 1)) c.sl_mtf = (uint32_t)value;
     else if (k == "trace.sl_fold" && (value == 0 || value == 1)) c.sl_fold = (uint32_t)value;
+    else if (k == "trace.coop_order" && (value == 0 || value == 1)) c.coop_order = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
     else if (k == "build.fuse_k01" && value >= 0 && value <= 2) c.fuse_k01 = (uint32_t)value;

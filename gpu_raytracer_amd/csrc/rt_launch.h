@@ -180,6 +180,8 @@ struct TraceConfig {
     uint32_t nt_hits = 2;       // nontemporal hit-record stores: 2 = always (default), 1 = frames of >= 2 spp,
                                 // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged;
                                 // the 1M build after a 1080p1 frame 140.3 -> 137.7 us, profiles/ab_nt_hits_1spp_r05.log)
+    uint32_t coop_order = 1;    // queue on: 1 = k_trace_coop's block 0 sorts this frame's costs into the next order,
+                                // 0 = k_trace's extra block folds the previous frame's (as with the queue off)
     uint32_t sl_fold = 1;       // k_trace_sl (full frames, one rank's tiles): 1 = block 0 sorts the next frame's tile
                                 // order (no k_tile_order launch)
     uint32_t sl_mtf = 1;        // k_trace_sl on one rank's tiles: 1 = Moller-Trumbore before the leaf box test

@@ -2473,8 +2473,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     const uint32_t coop_cap = sl ? sl_cap : coop_cap0;
     // (k_trace's extra block holds its costs in registers: nb <= 8192, full frames; k_trace_sl's block 0
     // loops, any nb, full frames and one rank's tiles)
-    const bool can_fold = RT_ORDER_FOLD && sched && wide && !counters && !cfg.order_override && coop_cap == 0 &&
-                          (sl ? cfg.sl_fold != 0 : nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread);
+    // (with the heavy-ray queue on, k_trace_coop's block 0 sorts this frame's costs instead, unless
+    // trace.coop_order = 0)
+    const bool can_fold = RT_ORDER_FOLD && sched && wide && !counters && !cfg.order_override &&
+                          (sl ? cfg.sl_fold != 0 && coop_cap == 0
+                              : nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread &&
+                                    (coop_cap == 0 || !cfg.coop_order));
     OrderFold fold;
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
@@ -2630,7 +2634,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             cgrid = r;
         }
         // block 0 sorts this frame's cost map into the next frame's tile order
-        const bool ord = cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
+        const bool ord = !fold.out && cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
         uint32_t* ord_cost = ord ? cost_out : nullptr;
         uint32_t* ord_out = ord ? sched->order : nullptr;
         uint32_t* ord_ema = ord ? sched->cost_ema : nullptr;
