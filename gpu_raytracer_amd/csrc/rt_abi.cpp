@@ -281,6 +281,14 @@ void replica_free(Replica& r) {
     (void)hipSetDevice(r.device);
     if (r.last_stream) (void)hipEventSynchronize(r.last);  // device work on a caller stream
     (void)hipStreamSynchronize(r.stream);
+    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side
+        if (!o->sched.side) continue;
+        (void)hipStreamSynchronize(o->sched.side);
+        (void)hipEventDestroy(o->sched.ev_traced);
+        (void)hipEventDestroy(o->sched.ev_sorted);
+        (void)hipStreamDestroy(o->sched.side);
+        o->sched.side = nullptr;
+    }
     rt::free_build(r.bufs);
     rt::free_path(r.path);
     for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.ord.d, r.ord_diag.d, r.d_slab, r.d_slab_hits, r.d_recv,
@@ -547,7 +555,16 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
     const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
     const size_t qoff = (maps + 255) & ~size_t(255);
     const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
+    if (!r.sched.side) {  // trace.order_side's stream and events (on the caller's current device)
+        HIPR(hipStreamCreateWithFlags(&r.sched.side, hipStreamNonBlocking));
+        HIPR(hipEventCreateWithFlags(&r.sched.ev_traced, hipEventDisableTiming | hipEventDisableSystemFence));
+        HIPR(hipEventCreateWithFlags(&r.sched.ev_sorted, hipEventDisableTiming | hipEventDisableSystemFence));
+    }
     if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
+        if (r.sched.side_pending) {  // a side sort still writing the maps about to be replaced
+            HIPR(hipEventSynchronize(r.sched.ev_sorted));
+            r.sched.side_pending = false;
+        }
         std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
         RTR(grow(&r.d, &r.cap, need));
         uint32_t* b = static_cast<uint32_t*>(r.d);
@@ -623,6 +640,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.sl_mtf" && (value == 0 || value == 1)) c.sl_mtf = (uint32_t)value;
     else if (k == "trace.sl_fold" && (value == 0 || value == 1)) c.sl_fold = (uint32_t)value;
     else if (k == "trace.coop_order" && (value == 0 || value == 1)) c.coop_order = (uint32_t)value;
+    else if (k == "trace.order_side" && (value == 0 || value == 1)) c.order_side = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
     else if (k == "build.fuse_k01" && value >= 0 && value <= 2) c.fuse_k01 = (uint32_t)value;

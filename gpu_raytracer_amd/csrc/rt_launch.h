@@ -180,6 +180,8 @@ struct TraceConfig {
     uint32_t nt_hits = 2;       // nontemporal hit-record stores: 2 = always (default), 1 = frames of >= 2 spp,
                                 // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged;
                                 // the 1M build after a 1080p1 frame 140.3 -> 137.7 us, profiles/ab_nt_hits_1spp_r05.log)
+    uint32_t order_side = 1;    // queue on: 1 = the next order sorted on a side stream (TileSched::side), not in
+                                // k_trace_coop's block 0 (its critical path when the queue is short)
     uint32_t coop_order = 1;    // queue on: 1 = k_trace_coop's block 0 sorts this frame's costs into the next order,
                                 // 0 = k_trace's extra block folds the previous frame's (as with the queue off)
     uint32_t sl_fold = 1;       // k_trace_sl (full frames, one rank's tiles): 1 = block 0 sorts the next frame's tile
@@ -271,6 +273,13 @@ struct TileSched {
     bool have_prev = false;
     bool order_ready = false;       // `order` for this frame already sorted by the previous frame's k_trace_coop
     bool fresh = true;              // maps (re)allocated: clear both before the first launch
+    // trace.order_side: with the heavy-ray queue on, the next frame's order
+    // is sorted by k_tile_order on this side stream once k_trace is done
+    // (ev_traced), beside k_trace_coop and whatever follows; the next frame's
+    // launch waits for ev_sorted.  Created by the owner (rt_abi.cpp sched_for).
+    hipStream_t side = nullptr;
+    hipEvent_t ev_traced = nullptr, ev_sorted = nullptr;
+    bool side_pending = false;      // ev_sorted not yet waited for
 };
 // The process-wide knobs (rt_config_set).  Every launcher works on one
 // consistent copy taken under the config lock, so a concurrent rt_config_set

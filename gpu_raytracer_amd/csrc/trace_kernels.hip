@@ -2480,6 +2480,11 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
                               : nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread &&
                                     (coop_cap == 0 || !cfg.coop_order));
     OrderFold fold;
+    if (sched && sched->side_pending) {  // the previous frame's order, sorted on the side stream
+        const hipError_t we = hipStreamWaitEvent(s, sched->ev_sorted, 0);
+        if (we != hipSuccess) return we;
+        sched->side_pending = false;
+    }
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
             hipError_t me = hipMemsetAsync(sched->cost_prev, 0, (size_t)nb * 4, s);
@@ -2634,7 +2639,19 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             cgrid = r;
         }
         // block 0 sorts this frame's cost map into the next frame's tile order
-        const bool ord = !fold.out && cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
+        bool ord = !fold.out && cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
+        if (ord && cfg.order_side && sched->side) {
+            // this frame's costs are final when k_trace is: sort them into the next order on the side
+            // stream (k_trace_coop then runs the queue only)
+            hipError_t se = hipEventRecord(sched->ev_traced, s);
+            if (se == hipSuccess) se = hipStreamWaitEvent(sched->side, sched->ev_traced, 0);
+            if (se != hipSuccess) return se;
+            RT_KLAUNCH(k_tile_order, dim3(1), dim3(1024), 0, sched->side, cost_out, nb, sched->order, sched->cost_ema);
+            if ((se = hipEventRecord(sched->ev_sorted, sched->side)) != hipSuccess) return se;
+            sched->side_pending = true;
+            sched->order_ready = true;
+            ord = false;
+        }
         uint32_t* ord_cost = ord ? cost_out : nullptr;
         uint32_t* ord_out = ord ? sched->order : nullptr;
         uint32_t* ord_ema = ord ? sched->cost_ema : nullptr;
