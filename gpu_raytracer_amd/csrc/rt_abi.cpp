@@ -88,7 +88,8 @@ struct Replica {
     // a trace on a caller stream is still reading, and the tile-order maps
     // are written and read in launch order.
     hipEvent_t last = nullptr;
-    hipStream_t last_stream = nullptr;  // stream `last` was recorded on (nullptr: none)
+    hipStream_t last_stream = nullptr;  // stream `last` was recorded on (when last_pending; 0 = the null stream)
+    bool last_pending = false;          // device work on a caller stream not yet ordered before the replica's own
     // distributed build (rt_dbuild_*): pair scratch and the crossing lists
     uint32_t* dk[2] = {nullptr, nullptr};
     uint32_t* dv[2] = {nullptr, nullptr};
@@ -279,7 +280,7 @@ rt_status replica_init(Replica& r) {
 void replica_free(Replica& r) {
     if (!r.stream) return;
     (void)hipSetDevice(r.device);
-    if (r.last_stream) (void)hipEventSynchronize(r.last);  // device work on a caller stream
+    if (r.last_pending) (void)hipEventSynchronize(r.last);  // device work on a caller stream
     (void)hipStreamSynchronize(r.stream);
     for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side
         if (!o->sched.side) continue;
@@ -342,24 +343,25 @@ Replica* primary_built(const rt_scene* s) {
 // Before device work on stream hs: order it after this replica's previous
 // device work when that ran on another stream.
 rt_status order_before(Replica& r, hipStream_t hs) {
-    if (r.last_stream && r.last_stream != hs) HIPR(hipStreamWaitEvent(hs, r.last, 0));
+    if (r.last_pending && r.last_stream != hs) HIPR(hipStreamWaitEvent(hs, r.last, 0));
     return RT_OK;
 }
 // After device work on a caller stream hs: remember it (see Replica::last).
 rt_status order_after(Replica& r, hipStream_t hs) {
     if (hs == r.stream) {
-        r.last_stream = nullptr;  // the replica's own stream orders itself
+        r.last_pending = false;  // the replica's own stream orders itself
         return RT_OK;
     }
     HIPR(hipEventRecord(r.last, hs));
     r.last_stream = hs;
+    r.last_pending = true;
     return RT_OK;
 }
 // Before the replica's own stream rewrites or frees its buffers.
 rt_status join_caller_work(Replica& r) {
-    if (r.last_stream) {
+    if (r.last_pending) {
         HIPR(hipStreamWaitEvent(r.stream, r.last, 0));
-        r.last_stream = nullptr;
+        r.last_pending = false;
     }
     return RT_OK;
 }
@@ -779,7 +781,7 @@ rt_status rt_scene_sync(rt_scene* s) {
     for (auto& r : s->reps) {
         if (!r->stream) continue;
         HIPR(hipSetDevice(r->device));
-        if (r->last_stream) HIPR(hipEventSynchronize(r->last));
+        if (r->last_pending) HIPR(hipEventSynchronize(r->last));
         HIPR(hipStreamSynchronize(r->stream));
     }
     return RT_OK;
@@ -871,7 +873,7 @@ rt_status rt_bvh_read(const rt_scene* s, rt_node* nodes, uint32_t* keys, uint32_
     Replica* r = primary_built(s);
     if (!r) return fail(RT_EINVAL, "scene not built");
     HIPR(hipSetDevice(r->device));
-    if (r->last_stream) HIPR(hipEventSynchronize(r->last));
+    if (r->last_pending) HIPR(hipEventSynchronize(r->last));
     HIPR(hipStreamSynchronize(r->stream));
     const size_t n = s->n, tot = n ? 2 * n - 1 : 0;
     RTR(materialize_leaves(*r, s->n));
@@ -1305,7 +1307,7 @@ rt_status rt_render(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h, u
 namespace {
 template <class F>
 rt_status device_launch(Replica& r, void* stream, double* ms_out, const char* what, F&& fn) {
-    hipStream_t hs = stream ? (hipStream_t)stream : r.stream;
+    hipStream_t hs = stream ? rt::hip_stream((hipStream_t)stream) : r.stream;
     HIPR(hipSetDevice(r.device));
     RTR(order_before(r, hs));
     if (ms_out) HIPR(hipEventRecord(r.r0, hs));
@@ -1527,7 +1529,7 @@ rt_status rt_render_step_map(rt_scene* s, uint32_t w, uint32_t h, uint32_t spp, 
     const size_t nb = rt::tiles_for_rank(w, h, rank, nranks);
     if (count < nb * 256) return fail(RT_EINVAL, "step map buffer too small");
     HIPR(hipSetDevice(r->device));
-    if (r->last_stream) HIPR(hipEventSynchronize(r->last));
+    if (r->last_pending) HIPR(hipEventSynchronize(r->last));
     HIPR(hipStreamSynchronize(r->stream));
     HIPR(hipMemcpy(out, r->ord.sched.px_prev, nb * 256 * sizeof(uint16_t), hipMemcpyDeviceToHost));
     return RT_OK;
@@ -1580,7 +1582,7 @@ rt_status rt_unpack_tiles_device(const void* d_slabs, uint32_t tiles_per_slab, u
                                  uint32_t nranks, void* d_rgba, int device, void* stream) {
     if (!d_slabs || !d_rgba || !w || !h || !nranks) return fail(RT_EINVAL, "bad arguments");
     RTR(ensure_device(device));
-    hipError_t e = rt::launch_unpack(d_slabs, tiles_per_slab, w, h, nranks, d_rgba, (hipStream_t)stream);
+    hipError_t e = rt::launch_unpack(d_slabs, tiles_per_slab, w, h, nranks, d_rgba, rt::hip_stream((hipStream_t)stream));
     if (e != hipSuccess) return hip_fail(e, "launch_unpack");
     return RT_OK;
 }

@@ -281,6 +281,11 @@ struct TileSched {
     hipEvent_t ev_traced = nullptr, ev_sorted = nullptr;
     bool side_pending = false;      // ev_sorted not yet waited for
 };
+// The HIP handle for a stream argument: the ABI's hipStreamLegacy (the null
+// stream, torch's default) is passed to HIP as 0, which every HIP call takes
+// (hipStreamWaitEvent on the legacy handle itself does not).
+inline hipStream_t hip_stream(hipStream_t s) { return s == hipStreamLegacy ? nullptr : s; }
+
 // The process-wide knobs (rt_config_set).  Every launcher works on one
 // consistent copy taken under the config lock, so a concurrent rt_config_set
 // on another thread never tears a launch's settings.
