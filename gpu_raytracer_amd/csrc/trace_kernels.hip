@@ -2481,8 +2481,14 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
                                     (coop_cap == 0 || !cfg.coop_order));
     OrderFold fold;
     if (sched && sched->side_pending) {  // the previous frame's order, sorted on the side stream
-        const hipError_t we = hipStreamWaitEvent(s, sched->ev_sorted, 0);
-        if (we != hipSuccess) return we;
+        // (a cross-queue wait costs the frame a few us even when the sort is long done: only when it is not)
+        const hipError_t qe = hipEventQuery(sched->ev_sorted);
+        if (qe == hipErrorNotReady) {
+            const hipError_t we = hipStreamWaitEvent(s, sched->ev_sorted, 0);
+            if (we != hipSuccess) return we;
+        } else if (qe != hipSuccess) {
+            return qe;
+        }
         sched->side_pending = false;
     }
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
