@@ -180,8 +180,9 @@ struct TraceConfig {
     uint32_t nt_hits = 2;       // nontemporal hit-record stores: 2 = always (default), 1 = frames of >= 2 spp,
                                 // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged;
                                 // the 1M build after a 1080p1 frame 140.3 -> 137.7 us, profiles/ab_nt_hits_1spp_r05.log)
-    uint32_t order_side = 1;    // queue on: 1 = the next order sorted on a side stream (TileSched::side), not in
-                                // k_trace_coop's block 0 (its critical path when the queue is short)
+    uint32_t order_side = 0;    // queue on: 1 = the next order sorted on a side stream (TileSched::side), not in
+                                // k_trace_coop's block 0 (its critical path when the queue is short: bunny substitute
+                                // -3 to -7 %, soup-1M +1 %, profiles/ab_order_side_r05.log; off by default)
     uint32_t coop_order = 1;    // queue on: 1 = k_trace_coop's block 0 sorts this frame's costs into the next order,
                                 // 0 = k_trace's extra block folds the previous frame's (as with the queue off)
     uint32_t sl_fold = 1;       // k_trace_sl (full frames, one rank's tiles): 1 = block 0 sorts the next frame's tile
