@@ -214,3 +214,40 @@ def test_orbit_frame_8_ranks_1m(R, oracle, cfg):
             hits, rgba, _ = s.render(cam, w, h, 1, ngpus=P)
             assert np.array_equal(rgba, er), P
             assert _same_hits(hits, eh), P
+
+
+@pytest.mark.parametrize("side,coop_order", [(1, 1), (0, 0), (1, 0)])
+def test_order_paths_with_queue(R, oracle, cfg, side, coop_order):
+    """Where the next tile order of a queue-on frame is sorted: k_trace_coop's
+    block 0 (the default), a k_tile_order on the side stream after k_trace
+    (trace.order_side), or k_trace's fold block from the previous frame's
+    costs (trace.coop_order 0) -- four successive frames each, full frames
+    and one rank's tiles (P = 3), and full frames on torch's default stream
+    with no host sync between them: every frame == the oracle."""
+    import torch
+    V = _soup_view()
+    tris = oracle.soup(40000, 12).reshape(-1, 9)
+    w, h, spp = 210, 118, 1
+    eh, er = _frame(oracle, tris, V, w, h, spp)
+    cfg("trace.order_side", side, 0)
+    cfg("trace.coop_order", coop_order, 1)
+    cfg("trace.coop_cap", 16, -1)
+    cfg("trace.coop_cap_tiles", 24, -1)
+    cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
+    with R.Scene.from_soup(tris) as s:
+        s.build()
+        for frame in range(4):
+            hits, rgba, _ = s.render(cam, w, h, spp)
+            assert np.array_equal(rgba, er), ("full", frame)
+            assert _same_hits(hits, eh), ("full", frame)
+        cfg("render.emulate", 1, 0)
+        for frame in range(4):
+            hits, rgba, _ = s.render(cam, w, h, spp, ngpus=3)
+            assert np.array_equal(rgba, er), ("tiles", frame)
+        cur = torch.cuda.current_stream()
+        imgs = [torch.zeros(w * h, dtype=torch.int32, device="cuda") for _ in range(4)]
+        for img in imgs:
+            s.render_device(cam, w, h, spp, d_rgba=img.data_ptr(), stream=cur.cuda_stream)
+        torch.cuda.synchronize()
+        for i, img in enumerate(imgs):
+            assert np.array_equal(img.cpu().numpy().view(np.uint8), er), ("null stream", i)
