@@ -282,9 +282,7 @@ void replica_free(Replica& r) {
     (void)hipSetDevice(r.device);
     if (r.last_pending) (void)hipEventSynchronize(r.last);  // device work on a caller stream
     (void)hipStreamSynchronize(r.stream);
-    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side, trace.coop_order auto
-        if (o->sched.q_host) (void)hipHostFree(o->sched.q_host);
-        o->sched.q_host = o->sched.q_dev = nullptr;
+    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side
         if (!o->sched.side) continue;
         (void)hipStreamSynchronize(o->sched.side);
         (void)hipEventDestroy(o->sched.ev_traced);
@@ -564,18 +562,12 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
         HIPR(hipEventCreateWithFlags(&r.sched.ev_traced, hipEventDisableTiming | hipEventDisableSystemFence));
         HIPR(hipEventCreateWithFlags(&r.sched.ev_sorted, hipEventDisableTiming | hipEventDisableSystemFence));
     }
-    if (!r.sched.q_host) {  // trace.coop_order auto's queue-length word
-        HIPR(hipHostMalloc(reinterpret_cast<void**>(&r.sched.q_host), 64, hipHostMallocMapped));
-        HIPR(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.sched.q_dev), r.sched.q_host, 0));
-        *r.sched.q_host = ~0u;
-    }
     if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
         if (r.sched.side_pending) {  // a side sort still writing the maps about to be replaced
             HIPR(hipEventSynchronize(r.sched.ev_sorted));
             r.sched.side_pending = false;
         }
         std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
-        __atomic_store_n(r.sched.q_host, ~0u, __ATOMIC_RELAXED);  // a new shape: its queue length not yet known
         RTR(grow(&r.d, &r.cap, need));
         uint32_t* b = static_cast<uint32_t*>(r.d);
         r.sched.order = b;
@@ -649,7 +641,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.nt_hits" && value >= 0 && value <= 3) c.nt_hits = (uint32_t)value;
     else if (k == "trace.sl_mtf" && (value == 0 || value == 1)) c.sl_mtf = (uint32_t)value;
     else if (k == "trace.sl_fold" && (value == 0 || value == 1)) c.sl_fold = (uint32_t)value;
-    else if (k == "trace.coop_order" && value >= 0 && value <= 2) c.coop_order = (uint32_t)value;
+    else if (k == "trace.coop_order" && (value == 0 || value == 1)) c.coop_order = (uint32_t)value;
     else if (k == "trace.order_side" && (value == 0 || value == 1)) c.order_side = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;

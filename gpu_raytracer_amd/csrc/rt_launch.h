@@ -183,9 +183,8 @@ struct TraceConfig {
     uint32_t order_side = 0;    // queue on: 1 = the next order sorted on a side stream (TileSched::side), not in
                                 // k_trace_coop's block 0 (its critical path when the queue is short: bunny substitute
                                 // -3 to -7 %, soup-1M +1 %, profiles/ab_order_side_r05.log; off by default)
-    uint32_t coop_order = 2;    // queue on: 1 = k_trace_coop's block 0 sorts this frame's costs into the next order,
-                                // 0 = k_trace's extra block folds the previous frame's (as with the queue off),
-                                // 2 (default) = 0 when the previous frame queued < kShortQueue rays, else 1
+    uint32_t coop_order = 1;    // queue on: 1 = k_trace_coop's block 0 sorts this frame's costs into the next order,
+                                // 0 = k_trace's extra block folds the previous frame's (as with the queue off)
     uint32_t sl_fold = 1;       // k_trace_sl (full frames, one rank's tiles): 1 = block 0 sorts the next frame's tile
                                 // order (no k_tile_order launch)
     uint32_t sl_mtf = 1;        // k_trace_sl on one rank's tiles: 1 = Moller-Trumbore before the leaf box test
@@ -282,10 +281,6 @@ struct TileSched {
     hipStream_t side = nullptr;
     hipEvent_t ev_traced = nullptr, ev_sorted = nullptr;
     bool side_pending = false;      // ev_sorted not yet waited for
-    // trace.coop_order auto: the queue length k_trace_coop reported for the
-    // latest frame that ran it (mapped pinned host word; ~0u = not yet known)
-    uint32_t* q_host = nullptr;
-    uint32_t* q_dev = nullptr;
 };
 // The HIP handle for a stream argument: the ABI's hipStreamLegacy (the null
 // stream, torch's default) is passed to HIP as 0, which every HIP call takes

@@ -1516,11 +1516,6 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // launch (8-11 us, all of it latency) leaves the next frame's critical path
 // -- and leaves the queue to the other blocks.
 constexpr uint32_t kOrderInCoop = 256 * 32;  // up to 8192 tiles: a 1080p full frame has 8160
-// trace.coop_order auto: a frame whose predecessor queued fewer heavy rays
-// than this folds its order in k_trace (the queue pass is then ~6 us against
-// the ~12-us sort in its block 0: the bunny substitute queues ~20 rays, the
-// 1M soup ~10K; profiles/ab_order_side_r05.log)
-constexpr uint32_t kShortQueue = 256;
 template <bool COUNT, bool PACKED, int G, int WA = 4>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
@@ -1529,8 +1524,7 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                                                     unsigned long long* __restrict__ counters,
                                                     uint32_t* __restrict__ ord_cost = nullptr, uint32_t ord_nb = 0,
                                                     uint32_t* __restrict__ ord_out = nullptr,
-                                                    uint32_t* __restrict__ ord_ema = nullptr,
-                                                    uint32_t* __restrict__ q_count = nullptr) {
+                                                    uint32_t* __restrict__ ord_ema = nullptr) {
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
@@ -1562,8 +1556,6 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     }
     __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
-    // this frame's queue length to the host's mapped word (trace.coop_order auto): the last block
-    if (q_count && blockIdx.x == gridDim.x - 1 && threadIdx.x < 1) q_count[threadIdx.x] = cnt;
     uint32_t cn = 0, ct = 0;
     for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
         // queued ray e lives in the last non-empty shard whose prefix is <= e
@@ -2482,14 +2474,11 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // (k_trace's extra block holds its costs in registers: nb <= 8192, full frames; k_trace_sl's block 0
     // loops, any nb, full frames and one rank's tiles)
     // (with the heavy-ray queue on, k_trace_coop's block 0 sorts this frame's costs instead, unless
-    // trace.coop_order = 0, or 2 (auto, the default) and the previous frame queued fewer than
-    // kShortQueue rays: then that sort, not the queue, would be the pass's critical path)
-    const bool short_queue = cfg.coop_order == 2 && sched && sched->q_host &&
-                             __atomic_load_n(sched->q_host, __ATOMIC_RELAXED) < kShortQueue;
+    // trace.coop_order = 0)
     const bool can_fold = RT_ORDER_FOLD && sched && wide && !counters && !cfg.order_override &&
                           (sl ? cfg.sl_fold != 0 && coop_cap == 0
                               : nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread &&
-                                    (coop_cap == 0 || cfg.coop_order == 0 || short_queue));
+                                    (coop_cap == 0 || !cfg.coop_order));
     OrderFold fold;
     if (sched && sched->side_pending) {  // the previous frame's order, sorted on the side stream
         // (a cross-queue wait costs the frame a few us even when the sort is long done: only when it is not)
@@ -2675,10 +2664,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
 #define RT_COOP_G(C, P, G)                                                                                        \
     if (warity == 8)                                                                                               \
         RT_KLAUNCH((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema, sched->q_dev);                \
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema);                               \
     else                                                                                                           \
         RT_KLAUNCH((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema, sched->q_dev)
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema)
 #define RT_COOP(C, P)                  \
     if (cfg.coop_lanes == 16) {        \
         RT_COOP_G(C, P, 16);           \

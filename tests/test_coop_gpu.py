@@ -216,7 +216,7 @@ def test_orbit_frame_8_ranks_1m(R, oracle, cfg):
             assert _same_hits(hits, eh), P
 
 
-@pytest.mark.parametrize("side,coop_order", [(1, 1), (0, 0), (1, 0), (0, 2), (1, 2)])
+@pytest.mark.parametrize("side,coop_order", [(1, 1), (0, 0), (1, 0)])
 def test_order_paths_with_queue(R, oracle, cfg, side, coop_order):
     """Where the next tile order of a queue-on frame is sorted: k_trace_coop's
     block 0 (the default), a k_tile_order on the side stream after k_trace
@@ -230,7 +230,7 @@ def test_order_paths_with_queue(R, oracle, cfg, side, coop_order):
     w, h, spp = 210, 118, 1
     eh, er = _frame(oracle, tris, V, w, h, spp)
     cfg("trace.order_side", side, 0)
-    cfg("trace.coop_order", coop_order, 2)
+    cfg("trace.coop_order", coop_order, 1)
     cfg("trace.coop_cap", 16, -1)
     cfg("trace.coop_cap_tiles", 24, -1)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
