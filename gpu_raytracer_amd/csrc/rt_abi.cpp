@@ -282,7 +282,9 @@ void replica_free(Replica& r) {
     (void)hipSetDevice(r.device);
     if (r.last_pending) (void)hipEventSynchronize(r.last);  // device work on a caller stream
     (void)hipStreamSynchronize(r.stream);
-    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side
+    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side, trace.coop_skip
+        if (o->sched.q_host) (void)hipHostFree(o->sched.q_host);
+        o->sched.q_host = o->sched.q_dev = nullptr;
         if (!o->sched.side) continue;
         (void)hipStreamSynchronize(o->sched.side);
         (void)hipEventDestroy(o->sched.ev_traced);
@@ -562,12 +564,19 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
         HIPR(hipEventCreateWithFlags(&r.sched.ev_traced, hipEventDisableTiming | hipEventDisableSystemFence));
         HIPR(hipEventCreateWithFlags(&r.sched.ev_sorted, hipEventDisableTiming | hipEventDisableSystemFence));
     }
+    if (!r.sched.q_host) {  // trace.coop_skip's queue-length word
+        HIPR(hipHostMalloc(reinterpret_cast<void**>(&r.sched.q_host), 64, hipHostMallocMapped));
+        HIPR(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.sched.q_dev), r.sched.q_host, 0));
+        __atomic_store_n(r.sched.q_host, ~0u, __ATOMIC_RELAXED);
+    }
     if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
         if (r.sched.side_pending) {  // a side sort still writing the maps about to be replaced
             HIPR(hipEventSynchronize(r.sched.ev_sorted));
             r.sched.side_pending = false;
         }
         std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
+        __atomic_store_n(r.sched.q_host, ~0u, __ATOMIC_RELAXED);  // a new shape: its queue length not yet known
+        r.sched.q_frames = 0;
         RTR(grow(&r.d, &r.cap, need));
         uint32_t* b = static_cast<uint32_t*>(r.d);
         r.sched.order = b;
@@ -643,6 +652,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "trace.sl_fold" && (value == 0 || value == 1)) c.sl_fold = (uint32_t)value;
     else if (k == "trace.coop_order" && (value == 0 || value == 1)) c.coop_order = (uint32_t)value;
     else if (k == "trace.order_side" && (value == 0 || value == 1)) c.order_side = (uint32_t)value;
+    else if (k == "trace.coop_skip" && (value == 0 || value == 1)) c.coop_skip = (uint32_t)value;
     else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
     else if (k == "build.fuse_k01" && value >= 0 && value <= 2) c.fuse_k01 = (uint32_t)value;

@@ -180,6 +180,8 @@ struct TraceConfig {
     uint32_t nt_hits = 2;       // nontemporal hit-record stores: 2 = always (default), 1 = frames of >= 2 spp,
                                 // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged;
                                 // the 1M build after a 1080p1 frame 140.3 -> 137.7 us, profiles/ab_nt_hits_1spp_r05.log)
+    uint32_t coop_skip = 1;     // automatic caps: 1 = skip the queue for a shape whose last queue-on frame queued
+                                // < kQueueSkip rays (re-probing every kQueueProbe-th frame); 0 = never
     uint32_t order_side = 0;    // queue on: 1 = the next order sorted on a side stream (TileSched::side), not in
                                 // k_trace_coop's block 0 (its critical path when the queue is short: bunny substitute
                                 // -3 to -7 %, soup-1M +1 %, profiles/ab_order_side_r05.log; off by default)
@@ -281,6 +283,12 @@ struct TileSched {
     hipStream_t side = nullptr;
     hipEvent_t ev_traced = nullptr, ev_sorted = nullptr;
     bool side_pending = false;      // ev_sorted not yet waited for
+    // trace.coop_skip: the queue length k_trace_coop reported for the latest
+    // queue-on frame of this shape (mapped pinned host word; ~0u = not yet
+    // known), and the queue-off frames since
+    uint32_t* q_host = nullptr;
+    uint32_t* q_dev = nullptr;
+    uint32_t q_frames = 0;
 };
 // The HIP handle for a stream argument: the ABI's hipStreamLegacy (the null
 // stream, torch's default) is passed to HIP as 0, which every HIP call takes

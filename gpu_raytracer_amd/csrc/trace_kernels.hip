@@ -1516,6 +1516,10 @@ __device__ __forceinline__ void coop_trace(const char* __restrict__ nodes, const
 // launch (8-11 us, all of it latency) leaves the next frame's critical path
 // -- and leaves the queue to the other blocks.
 constexpr uint32_t kOrderInCoop = 256 * 32;  // up to 8192 tiles: a 1080p full frame has 8160
+// trace.coop_skip: the bunny substitute queues 0-5 rays a frame at the 96-step
+// cap, the 1M soup 4500-6500 (profiles/ab_coop_skip_r05.log)
+constexpr uint32_t kQueueSkip = 64;
+constexpr uint32_t kQueueProbe = 16;
 template <bool COUNT, bool PACKED, int G, int WA = 4>
 __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                                                     const float4* __restrict__ tri_s, uint32_t n, Cam cam,
@@ -1524,7 +1528,8 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
                                                     unsigned long long* __restrict__ counters,
                                                     uint32_t* __restrict__ ord_cost = nullptr, uint32_t ord_nb = 0,
                                                     uint32_t* __restrict__ ord_out = nullptr,
-                                                    uint32_t* __restrict__ ord_ema = nullptr) {
+                                                    uint32_t* __restrict__ ord_ema = nullptr,
+                                                    uint32_t* __restrict__ q_count = nullptr) {
     constexpr uint32_t NG = CoopCfg<G, WA>::groups;
     __shared__ CoopLds<G, WA> s_l[NG];
     static_assert(kCoopShards == 64, "one shard per lane");
@@ -1556,6 +1561,8 @@ __global__ __launch_bounds__(256) void k_trace_coop(const void* __restrict__ nod
     }
     __syncthreads();
     const uint32_t cnt = __builtin_amdgcn_readlane(incl, 63);
+    // this frame's queue length to the host's mapped word (trace.coop_skip): the last block
+    if (q_count && blockIdx.x == gridDim.x - 1 && threadIdx.x < 1) q_count[threadIdx.x] = cnt;
     uint32_t cn = 0, ct = 0;
     for (uint32_t e = (blockIdx.x - b0) * NG + grp; e < cnt; e += (gridDim.x - b0) * NG) {
         // queued ray e lives in the last non-empty shard whose prefix is <= e
@@ -2458,10 +2465,22 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // next frame's order is sorted by an extra block of this launch
     // (OrderFold) instead of a k_tile_order launch ahead of it
     // heavy rays to k_trace_coop (DESIGN.md "Cooperative heavy rays")
-    const uint32_t coop_cap0 =
+    uint32_t coop_cap0 =
         wide && sched && sched->coop_q && n <= kBufMaxN
             ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : coop_cap_for_frame(cfg.coop_cap, spp, small))
             : 0u;
+    // trace.coop_skip: with the automatic cap, a frame shape whose last queue-on frame queued fewer than
+    // kQueueSkip rays runs without the queue (its pass would be all launch and order sort), re-probing
+    // every kQueueProbe-th frame (an explicit cap always runs the queue)
+    const bool cap_auto = (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) == kCoopCapAuto;
+    if (coop_cap0 && cap_auto && cfg.coop_skip && sched->q_host) {
+        if (__atomic_load_n(sched->q_host, __ATOMIC_RELAXED) < kQueueSkip && sched->q_frames + 1 < kQueueProbe) {
+            coop_cap0 = 0u;
+            ++sched->q_frames;
+        } else {
+            sched->q_frames = 0;
+        }
+    }
     // samples in lanes (k_trace_sl): multi-spp tiles and full frames (trace.spp_lanes = 2, the default;
     // 1 = tiles only)
     const bool sl = spp >= 2 && spp <= 16 && (spp & (spp - 1)) == 0 && wide && warity == 4 && !counters &&
@@ -2664,10 +2683,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
 #define RT_COOP_G(C, P, G)                                                                                        \
     if (warity == 8)                                                                                               \
         RT_KLAUNCH((k_trace_coop<C, P, G, 8>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema);                               \
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema, sched->q_dev);                \
     else                                                                                                           \
         RT_KLAUNCH((k_trace_coop<C, P, G, 4>), dim3(cgrid), dim3(256), 0, s, nodes, wnodes, tris, n, cam, w, \
-                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema)
+                           spp, cq, H, R, counters, ord_cost, nb, ord_out, ord_ema, sched->q_dev)
 #define RT_COOP(C, P)                  \
     if (cfg.coop_lanes == 16) {        \
         RT_COOP_G(C, P, 16);           \

@@ -251,3 +251,23 @@ def test_order_paths_with_queue(R, oracle, cfg, side, coop_order):
         torch.cuda.synchronize()
         for i, img in enumerate(imgs):
             assert np.array_equal(img.cpu().numpy().view(np.uint8), er), ("null stream", i)
+
+
+def test_coop_skip_probe_frames(R, oracle, cfg):
+    """trace.coop_skip (automatic caps): a shape whose queue-on frame queued
+    fewer than 64 rays runs its next 15 frames without the queue (the order
+    folded in k_trace), then probes with it again; a heavy shape keeps it.
+    20 frames of a light scene (the bunny substitute's sphere) and of a soup,
+    every one == the oracle."""
+    from gpu_raytracer_amd import scenes as S
+    for tris, view in ((np.ascontiguousarray(S.tris_for("bunny"), np.float32).reshape(-1, 9), S.VIEWS["bunny"]),
+                       (oracle.soup(40000, 13).reshape(-1, 9), _soup_view())):
+        w, h, spp = 160, 96, 1
+        eh, er = _frame(oracle, tris, view, w, h, spp)
+        cam = R.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
+        with R.Scene.from_soup(tris) as s:
+            s.build()
+            for frame in range(20):
+                hits, rgba, _ = s.render(cam, w, h, spp)
+                assert np.array_equal(rgba, er), frame
+                assert _same_hits(hits, eh), frame
