@@ -559,7 +559,7 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
     const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
     const size_t qoff = (maps + 255) & ~size_t(255);
     const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
-    if (!r.sched.side) {  // trace.order_side's stream and events (on the caller's current device)
+    if (!r.sched.side && cfg.order_side) {  // trace.order_side's stream and events (on the caller's current device)
         HIPR(hipStreamCreateWithFlags(&r.sched.side, hipStreamNonBlocking));
         HIPR(hipEventCreateWithFlags(&r.sched.ev_traced, hipEventDisableTiming | hipEventDisableSystemFence));
         HIPR(hipEventCreateWithFlags(&r.sched.ev_sorted, hipEventDisableTiming | hipEventDisableSystemFence));
