@@ -69,4 +69,4 @@ for k, v in (("build.wide_arity", 4), ("trace.variant", 0), ("trace.stack_cap", 
              ("trace.coop_order", 1), ("trace.sl_fold", 1), ("trace.spp_lanes", 2), ("trace.nt_hits", 2),
              ("trace.wg", 256), ("render.emulate", 0)):
     R.config_set(k, v)
-print(f"done: {iters} scenes x 2 frames, {bad} mismatching renders", flush=True)
+print(f"done: {iters} scenes x 3 frames, {bad} mismatching renders", flush=True)
