@@ -1381,7 +1381,10 @@ __global__ __launch_bounds__(64) void k_group_tables(float* __restrict__ table, 
 // K6 for the crossing nodes: box = suffix(l) U middle block totals U
 // prefix(r).  MODE 1: the group tables above (ng <= kLdsTreeMaxBlocks);
 // MODE 0: the global sparse table (levels built by k_sparse_near /
-// k_sparse_far) for larger m.
+// k_sparse_far) for larger m; MODE 2 (m <= kSmallTreeBlocks: n <= 262K at
+// 256-leaf blocks): each block's LDS segment tree over all m block totals
+// (<= 48 KB), so no group-table launch -- the small scenes' crossing stage
+// is three launches of a few us each, mostly latency.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ topo,
                                                      const float* __restrict__ prebuf, const float* __restrict__ sufbuf,
@@ -1409,15 +1412,15 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
     // off the critical path)
     const uint32_t q0 = blockIdx.x * 256 + threadIdx.x;
     uint32_t i0 = q0 < count ? node_of(q0) : 0u;
-    const uint32_t ng = (m + kGroupBlocks - 1) / kGroupBlocks;
+    const uint32_t ng = MODE == 2 ? m : (m + kGroupBlocks - 1) / kGroupBlocks;  // the tree's leaves
     uint32_t P = 1;
     while (P < ng) P <<= 1;
-    const float* gtot = table + 8ull * m * 6;
-    if (MODE == 1) {
+    const float* gtot = MODE == 2 ? table : table + 8ull * m * 6;  // block totals / group totals
+    if (MODE >= 1) {
         for (uint32_t j = threadIdx.x; j < P; j += 256) tree[P + j] = j < ng ? load_aabb(gtot, j) : aabb_empty();
     }
     uint4 tp0 = q0 < count ? topo[i0] : make_uint4(0u, 0u, 0u, 0u);
-    if (MODE == 1) {
+    if (MODE >= 1) {
         __syncthreads();
         for (uint32_t len = P >> 1; len >= 1; len >>= 1) {
             for (uint32_t j = threadIdx.x; j < len; j += 256) {
@@ -1437,7 +1440,15 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
         aabb_union(box, load_aabb(prebuf, r));
         const uint32_t bl = l / T + 1, br = r / T;  // middle blocks [bl, br)
         if (bl < br) {
-            if (MODE == 1) {
+            if (MODE == 2) {
+                uint32_t a = bl + P, b = br + P;  // blocks [bl, br)
+                while (a < b) {
+                    if (a & 1) aabb_union(box, tree[a++]);
+                    if (b & 1) aabb_union(box, tree[--b]);
+                    a >>= 1;
+                    b >>= 1;
+                }
+            } else if (MODE == 1) {
                 const uint32_t gl = bl / kGroupBlocks, gr = (br - 1) / kGroupBlocks;
                 // inside one group and shorter than it: two entries of one in-group level (0..5); a
                 // whole group (64 blocks) takes the other branch, as its suffix U prefix
@@ -1609,6 +1620,7 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
 
 template __global__ void k_refit_cross<1>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
 template __global__ void k_refit_cross<0>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
+template __global__ void k_refit_cross<2>(const uint4*, const float*, const float*, const float*, uint32_t, const uint32_t*, const uint32_t*, uint32_t, void*, uint32_t);
 
 // ================================================================ launchers
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
@@ -1744,6 +1756,8 @@ static hipError_t ensure_cross_attr() {
 #ifndef RT_XGRID_PER_BLOCK
 #define RT_XGRID_PER_BLOCK 12
 #endif
+// MODE 2 of k_refit_cross up to this many refit blocks (2 x 1024 x 24 B = 48 KB of LDS per block)
+constexpr uint32_t kSmallTreeBlocks = 1024;
 static uint32_t cross_grid(uint32_t m, uint32_t floor_blocks) {
     return std::min<uint32_t>(4096u, std::max<uint32_t>(floor_blocks, cdiv(RT_XGRID_PER_BLOCK * m, 256)));
 }
@@ -1753,7 +1767,12 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
     const uint32_t m = cdiv(n, kRefitT);
     if (m <= 1) return hipGetLastError();
     const uint32_t ng = cdiv(m, kGroupBlocks);
-    if (ng <= (uint32_t)kLdsTreeMaxBlocks) {
+    if (m <= kSmallTreeBlocks && config_snapshot().cross_small) {  // every block total in each block's LDS tree
+        uint32_t P = 1;
+        while (P < m) P <<= 1;
+        RT_KLAUNCH(k_refit_cross<2>, dim3(cross_grid(m, RT_CROSS_GRID)), dim3(256), 2ull * P * sizeof(Aabb), s, b.topo,
+                   b.prebuf, b.sufbuf, b.table, m, b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
+    } else if (ng <= (uint32_t)kLdsTreeMaxBlocks) {
         uint32_t P = 1;
         while (P < ng) P <<= 1;
         const size_t lds = 2ull * P * sizeof(Aabb);

@@ -659,6 +659,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
     else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;
+    else if (k == "build.cross_small" && (value == 0 || value == 1)) c.cross_small = (uint32_t)value;
     else if (k == "timing.event_fence" && (value == 0 || value == 1)) c.event_fence = (uint32_t)value;
     else if (k == "path.wavefront" && (value == 0 || value == 1)) c.path_wave = (uint32_t)value;
     else if (k == "path.wg" && (value == 64 || value == 256)) c.path_wg = (uint32_t)value;

@@ -228,6 +228,8 @@ struct TraceConfig {
     uint32_t lds_scribble = 0;    // debug.lds_scribble: before every kernel launch, fill the LDS of the
                                   // CUs with a fresh pseudo-random pattern, so a kernel that reads LDS
                                   // it did not write gives a different (wrong) result every launch
+    uint32_t cross_small = 1;   // build.cross_small: 1 = up to 1024 refit blocks, the crossing boxes from one LDS tree over
+                                // every block total (no group-table launch); 0 = the group tables at every size
     uint32_t force_lsb_redo = 0;  // debug.force_lsb_redo: treat every gather-sort build as if a bucket
                                   // had overflowed (tests the host's discard-and-redo branch)
 };

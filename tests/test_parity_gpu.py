@@ -653,7 +653,14 @@ def test_crossing_ranges_at_group_boundaries(R, oracle):
         keys[segs[j]:segs[j + 1]] = (j << 24) | np.arange(segs[j + 1] - segs[j], dtype=np.uint32)
     vals = np.arange(n, dtype=np.uint32)
     tris = soup(oracle, n, 5)
+    # 547 refit blocks: the small-scene LDS tree (build.cross_small) and the group tables it replaces
+    R.config_set("build.cross_small", 0)
+    try:
+        nodes_groups = R.stage_refit(keys, vals, tris)
+    finally:
+        R.config_set("build.cross_small", 1)
     nodes = R.stage_refit(keys, vals, tris)
+    assert np.array_equal(nodes.view(np.uint32), nodes_groups.view(np.uint32))
     left, right, rlo, rhi, parent = oracle.karras(keys)
     esc = oracle.escape(n, left, right, parent)
     t = tris.reshape(n, 3, 3)
