@@ -761,7 +761,13 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
 // [128x, 128x + 128), i.e. one contiguous eighth of every tile's runs and of
 // every table row, which its own L2 then serves to its 128 blocks.
 constexpr uint32_t kGatherMaxTilesPerThread = 4;  // runs (tiles) per thread in step 1
-constexpr uint32_t kGatherBinFast = 64;           // bins above this many keys flag the scene as clustered
+#ifndef RT_GATHER_SKEW
+#define RT_GATHER_SKEW 4  // k_bucket_dense's skew verdict: largest bucket > this x the mean (0: off)
+#endif
+#ifndef RT_GATHER_BIN_FAST
+#define RT_GATHER_BIN_FAST 64
+#endif
+constexpr uint32_t kGatherBinFast = RT_GATHER_BIN_FAST;  // bins above this many keys flag the scene as clustered
 
 // tiles (runs per bucket) the block's LDS holds: NT * 4, less for the
 // 12- and 16-key-per-thread shapes, whose buckets take 96 / 128 KB (n <= 12.05M)
@@ -1012,7 +1018,7 @@ __global__ __launch_bounds__(1024) void k_bucket_dense(const uint32_t* __restric
     __syncthreads();
     if (threadIdx.x == 0) {
         dense[0] = big ? 1u : 0u;
-        dense[3] = !big && s_max > 256u && (uint64_t)s_max * kMsbBuckets > 4ull * n ? 1u : 0u;
+        dense[3] = RT_GATHER_SKEW && !big && s_max > 256u && (uint64_t)s_max * kMsbBuckets > (uint64_t)RT_GATHER_SKEW * n ? 1u : 0u;
     }
 }
 
