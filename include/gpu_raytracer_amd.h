@@ -349,9 +349,23 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * queued and finished by a whole wave (k_trace_coop, DESIGN.md "Cooperative
  * heavy rays"); 0 = off; -1 = auto, the defaults: for full frames 96 steps
  * at 1 spp on 256-thread tiles (off otherwise) and, for one rank's tiles of a
- * multi-GPU frame, by rank count (88 steps for P = 2, 80 for P >= 3);
+ * multi-GPU frame, by rank count (88 steps for P = 2, 80 for P = 3..4, 72
+ * above); samples-in-lanes frames run without it unless a cap is given;
  * "trace.coop_max" queue entries per frame shape
- * (default 65536; rays beyond it keep tracing alone).  "build.stage_events"
+ * (default 65536; rays beyond it keep tracing alone); "trace.coop_skip" 1
+ * (default) / 0: with an automatic cap, a frame shape whose last queue-on
+ * frame queued fewer than 64 rays runs without the queue, re-probing every
+ * 16th frame; "trace.coop_order" 1 (default) / 0 and "trace.order_side" 0
+ * (default) / 1: where a queue-on frame sorts the next tile order
+ * (k_trace_coop's block 0 / folded in k_trace from the previous frame's
+ * costs; a k_tile_order on a side stream).  "trace.spp_lanes" 2 (default) /
+ * 1 / 0: 2..16 spp (a power of two) traced one ray per lane, a pixel's
+ * samples in adjacent lanes, for full frames and one rank's tiles / tiles
+ * only / never; "trace.sl_fold" 1 (default) / 0: those frames sort the next
+ * tile order in their block 0; "trace.sl_mtf" 1 (default) / 0: their
+ * rank-tile kernel tests a leaf's triangle before its box; "trace.nt_hits"
+ * 2 (default) / 1 / 0 / 3: hit records stored nontemporally for every frame
+ * / frames of >= 2 spp / never / + the RGBA words.  "build.stage_events"
  * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
  * 0/1: timing events of scenes created afterwards record with the
  * system-scope fence (default 0: no L2 writeback at each record).
@@ -359,13 +373,19 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * K1 sorts each 4096-key tile by the top 10 key bits, then one block per
  * bucket gathers its runs and sorts them in LDS), 1 = the r01-r03 MSB
  * scatter + bucket sort, 0 = the 4-pass LSB radix sort; a scene whose first
- * build finds a bucket beyond one block's LDS sort keeps the LSB sort.
+ * build finds a bucket beyond one block's LDS sort keeps the LSB sort, and
+ * one whose gather probe finds clustered bins or a skewed bucket moves on
+ * to the MSB sort.  "build.cross_small" 1 (default) / 0: scenes of up to
+ * 1024 refit blocks take the crossing nodes' boxes from one LDS tree over
+ * all block totals instead of the group tables.
  * "build.fuse_k01" 1 (default) / 0: with the gather sort, K0 (bounds) and K1
  * (Morton) as one launch whose blocks meet at a grid barrier, when every sort
  * tile's block fits the device at once (n up to ~1M) and no other such build
  * runs on the device; else two launches.  2 (test only): fused even when the
- * grid cannot be co-resident -- the barrier's bounded waits give up, and the
- * build fails with RT_EDEVICE instead of hanging.
+ * grid cannot be co-resident -- the barrier's bounded waits give up and the
+ * build is redone with two launches (rt_build_times.fused_fallback) instead
+ * of hanging.  "debug.force_lsb_redo" 0/1 (tests): take the gather-overflow
+ * branch, i.e. redo the build with the LSB sort.
  * "debug.poison" 0/1: every device buffer the library allocates from then on
  * is filled with 0xFF bytes before first use, so reading a byte no kernel
  * wrote gives the same (wrong) value every run instead of allocator luck.
