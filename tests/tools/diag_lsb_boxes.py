@@ -1,11 +1,11 @@
 """Diagnostic: which node boxes differ from the oracle after an LSB-sorted
 build (build.sort = 0) of the 1M soup -- local or crossing nodes, and the
 range lengths / block positions of the bad ones.  RT_LIB selects a library.
-usage: python tools/diag_lsb_boxes.py [n] [refit_leaves]"""
+usage: python tests/tools/diag_lsb_boxes.py [n] [refit_leaves]"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 

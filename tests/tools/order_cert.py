@@ -1,5 +1,5 @@
 """VERDICT r04 item 6 -- the stop rule for a certified nearest-first pass
-(CPU model, tools/order_sim.c osim_hazards).  For every primary ray of the
+(CPU model, tests/tools/order_sim.c osim_hazards).  For every primary ray of the
 soup-1M 1080p frame: the subtrees a nearest-first traversal culls only by
 its current best t (§9.7, whose tb is larger there, may enter them).  A sound
 certificate has to bound Moller-Trumbore's t error for every triangle in each
@@ -8,7 +8,7 @@ plane (1/|d.n|), so it needs each subtree's normal cone, and only a subtree
 of very few triangles has a cone that excludes grazing.  Printed: for all
 rays and for the heavy rays (the ~1 % whose §9.7 traversal is longest -- the
 ones the queue takes), how many have NO such subtree larger than k leaves.
-    python tools/order_cert.py [n]"""
+    python tests/tools/order_cert.py [n]"""
 import ctypes as C
 import os
 import subprocess
@@ -17,7 +17,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
 from gpu_raytracer_amd import scenes as S  # noqa: E402
@@ -28,7 +28,7 @@ def main():
     so = "/tmp/libosim.so"
     O.lib()
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-o", so,
-                    os.path.join(ROOT, "tools/order_sim.c"), "-L", os.path.join(ROOT, "oracle/build"), "-loracle",
+                    os.path.join(ROOT, "tests/tools/order_sim.c"), "-L", os.path.join(ROOT, "oracle/build"), "-loracle",
                     "-lm", "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
     tris = O.soup(n, 1)

@@ -1,9 +1,9 @@
-"""Design experiment (CPU model, tools/order_sim.c): node fetches per primary
+"""Design experiment (CPU model, tests/tools/order_sim.c): node fetches per primary
 ray of §9.7's fixed preorder against a nearest-first traversal of the same
 binary BVH, per ray and per 8x8 wave (its slowest lane), and how often the
 nearest-first answer differs from §9.7's.
 
-    python tools/order_sim.py [n] [rows]
+    python tests/tools/order_sim.py [n] [rows]
 """
 import ctypes as C
 import os
@@ -13,7 +13,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
 from gpu_raytracer_amd import scenes as S  # noqa: E402
@@ -24,7 +24,7 @@ def main():
     so = "/tmp/libosim.so"
     O.lib()
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-o", so,
-                    os.path.join(ROOT, "tools/order_sim.c"), "-L", os.path.join(ROOT, "oracle/build"), "-loracle",
+                    os.path.join(ROOT, "tests/tools/order_sim.c"), "-L", os.path.join(ROOT, "oracle/build"), "-loracle",
                     "-lm", "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
     tris = O.soup(n, 1)

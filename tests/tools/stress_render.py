@@ -3,12 +3,12 @@ traversal variant, stack cap, sort and frame shape (1-16 spp), the queue,
 order and store knobs, full frames or emulated ranks, rendered fresh and on
 successive frames; any hit or pixel that differs from the oracle is
 reported.
-usage: python tools/stress_render.py [iterations] [seed]"""
+usage: python tests/tools/stress_render.py [iterations] [seed]"""
 import os
 import sys
 import time
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import gpu_raytracer_amd as R  # noqa: E402

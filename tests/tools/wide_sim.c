@@ -7,7 +7,7 @@
  * trace_kernels.hip) processes at most one record and one leaf.  Boxes are
  * the exact binary boxes (the GPU's quantized boxes only add entries).
  *
- * Build: gcc -O2 -shared -fPIC -o /tmp/libwsim.so tools/wide_sim.c -L oracle/build -loracle -lm
+ * Build: gcc -O2 -shared -fPIC -o /tmp/libwsim.so tests/tools/wide_sim.c -L oracle/build -loracle -lm
  */
 #include <math.h>
 #include <stdint.h>

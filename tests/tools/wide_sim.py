@@ -1,8 +1,8 @@
 """Step counts of the wide traversal for K-ary greedy cuts (CPU model,
-tools/wide_sim.c): how much an 8-wide record would shorten the heavy rays'
+tests/tools/wide_sim.c): how much an 8-wide record would shorten the heavy rays'
 dependent chains.  Design experiment; uses the oracle's build.
 
-    python tools/wide_sim.py [n] [K ...]
+    python tests/tools/wide_sim.py [n] [K ...]
 """
 import ctypes as C
 import os
@@ -12,7 +12,7 @@ from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 from oracle import oracle as O  # noqa: E402
 from gpu_raytracer_amd import scenes as S  # noqa: E402
@@ -23,7 +23,7 @@ def main():
     ks = [k for k in sys.argv[2:]] or ["4", "8"]  # K, or K:sah:ci:cl (SAH-optimal cut)
     so = "/tmp/libwsim.so"
     O.lib()
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tests/tools/wide_sim.c"),
                     "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
@@ -75,7 +75,7 @@ def waves(n=1_000_000, policies=((0, 0), (4, 16), (4, 24), (4, 32), (6, 24), (8,
     """Wave model of leaf deferral (wsim_waves): steps, block counts, VALU."""
     so = "/tmp/libwsim.so"
     O.lib()
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tests/tools/wide_sim.c"),
                     "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
@@ -113,7 +113,7 @@ def compact(n=1_000_000, policies=((0, 0), (16, 8), (24, 8), (32, 8), (24, 16), 
     """Wave-compaction model (wsim_compact): pass 1 until < A lanes live, pass 2 packed."""
     so = "/tmp/libwsim.so"
     O.lib()
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tests/tools/wide_sim.c"),
                     "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
@@ -151,7 +151,7 @@ def chain(n=1_000_000, K=4):
     """Top-of-stack prefetch model (wsim_chain): steps whose data would already be there."""
     so = "/tmp/libwsim.so"
     O.lib()
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tests/tools/wide_sim.c"),
                     "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
@@ -191,7 +191,7 @@ def merge(n=1_000_000, policies=((0, 0), (32, 8), (40, 8), (48, 8), (64, 8), (32
     """In-block wave merging model (wsim_merge)."""
     so = "/tmp/libwsim.so"
     O.lib()
-    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tools/wide_sim.c"),
+    subprocess.run(["gcc", "-O2", "-shared", "-fPIC", "-o", so, os.path.join(ROOT, "tests/tools/wide_sim.c"),
                     "-L", os.path.join(ROOT, "oracle/build"), "-loracle", "-lm",
                     "-Wl,-rpath," + os.path.join(ROOT, "oracle/build")], check=True)
     L = C.CDLL(so)
