@@ -1,7 +1,7 @@
 """Which sort each build of a scene ends up with (rt_build_times.sort_kind:
 0 LSB, 1 MSB, 2 gather) and its event-timed total, for the BASELINE
 substitute scenes and the soup, under each build.sort setting; plus the
-scene's top-10-bit bucket and fine-bin maxima from the oracle's keys (what the
+scene's top-10-bit bucket and fine-bin maxima from the built BVH's sorted keys (what the
 gather probe's verdicts look at: bucket > its LDS capacity = dense, a bin of
 more than 64 keys = clustered).
 usage: python tools/sort_verdict.py [builds=5]"""
