@@ -427,11 +427,21 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
     // Every replica is synchronized and checked before anything returns
     // (an early return left later replicas' flags unread while
     // their fused grids could still run after the gates were released).
+    // (the synchronize loop itself must not return early either:
+    // an error on one replica is recorded and the others are still waited for,
+    // so no fused grid outlives the gates released on return)
     rt_status first_err = RT_OK;
     double worst = 0.0;
-    for (Replica* r : targets) {
-        HIPR(hipSetDevice(r->device));
-        HIPR(hipStreamSynchronize(r->stream));
+    std::vector<char> synced(targets.size(), 0);
+    for (size_t i = 0; i < targets.size(); ++i) {
+        Replica* r = targets[i];
+        hipError_t e = hipSetDevice(r->device);
+        if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+        if (e != hipSuccess) {
+            if (first_err == RT_OK) first_err = hip_fail(e, "synchronize build");
+            continue;
+        }
+        synced[i] = 1;
     }
     // stage times of the build just synchronized; the total is what this
     // call spent on the replica: a discarded build's time is added to its redo
@@ -450,8 +460,13 @@ rt_status build_replicas(rt_scene* s, const std::vector<Replica*>& targets, doub
         r->times.total = spent_before + tot;
         return RT_OK;
     };
-    for (Replica* r : targets) {
-        HIPR(hipSetDevice(r->device));
+    for (size_t ri = 0; ri < targets.size(); ++ri) {
+        Replica* r = targets[ri];
+        if (!synced[ri]) continue;  // its error is already recorded
+        if (rt_status st = hip_status(hipSetDevice(r->device), "hipSetDevice"); st != RT_OK) {
+            if (first_err == RT_OK) first_err = st;
+            continue;
+        }
         if (rt_status st = read_times(r, 0.0); st != RT_OK) {
             if (first_err == RT_OK) first_err = st;
             continue;
