@@ -36,7 +36,7 @@ EXPORTED = [
     "rt_scene_from_soup", "rt_scene_load_obj", "rt_scene_generate_soup", "rt_scene_load_soup",
     "rt_scene_save_soup", "rt_bvh_save", "rt_bvh_load", "rt_scene_num_tris",
     "rt_scene_get_tris", "rt_scene_set_device", "rt_scene_free", "rt_camera_look_at", "rt_bvh_build",
-    "rt_bvh_build_times", "rt_bvh_read", "rt_bvh_read_wide", "rt_bvh_wide_arity", "rt_render", "rt_render_timed", "rt_render_counters",
+    "rt_bvh_build_times", "rt_bvh_build_times_sized", "rt_bvh_read", "rt_bvh_read_wide", "rt_bvh_wide_arity", "rt_render", "rt_render_timed", "rt_render_counters",
     "rt_render_work", "rt_render_device",
     "rt_render_shadow", "rt_render_shadow_device", "rt_render_shadow_work",
     "rt_render_path", "rt_render_path_device", "rt_render_path_work",
@@ -108,6 +108,7 @@ def lib() -> C.CDLL:
         "rt_bvh_build": [P, i32, u32, C.POINTER(dbl)],
         "rt_bvh_replicas": [P, u32, P, C.POINTER(u32)],
         "rt_bvh_build_times": [P, C.POINTER(rt_build_times)],
+        "rt_bvh_build_times_sized": [P, C.POINTER(rt_build_times), C.c_size_t],
         "rt_bvh_read": [P, P, P, P, P, P],
         "rt_bvh_read_wide": [P, P],
         "rt_bvh_wide_arity": [P, C.POINTER(u32)],

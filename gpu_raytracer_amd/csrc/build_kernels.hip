@@ -1051,12 +1051,11 @@ __device__ __forceinline__ void store_wide(uint4* __restrict__ wnodes, uint32_t 
     }
 }
 
-// The record's entries (4 slots, RT_SENT-padded); topo_of(i) gives internal
-// node i's topology word, box_of_node(i) its box.  collapse = 0: X's
-// children, each internal child replaced by its two children.
-//
-// collapse = 1 (default): greedy instead of fixed depth -- starting from
-// {left, right}, twice replace the internal entry with the largest box
+// The record's entries (W slots, RT_SENT-padded); topo_of(i) gives internal
+// node i's topology word, box_of_node(i) its box.  The greedy cut (r01; the
+// fixed two-level cut, build.wide_collapse = 0, was removed in r06 --
+// profiles/ab_collapse_r01.log, profiles/rejected_knobs_r06.patch): starting
+// from {left, right}, W - 2 times replace the internal entry with the largest box
 // surface (first in preorder on ties) by its two children.  Any such set is
 // a preorder cut of X's subtree (each entry a descendant, their subtrees
 // partitioning X's leaves, listed in preorder), which is all the trace's
@@ -1069,10 +1068,10 @@ __device__ __forceinline__ float half_area(const Aabb& b) {
 
 template <int W, typename TopoOf, typename BoxOfNode>
 __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoOf topo_of, BoxOfNode box_of_node,
-                                             uint32_t collapse, uint32_t (&node)[W]) {
+                                             uint32_t (&node)[W]) {
     uint32_t l, r;
     kids_of(tx, L0, l, r);
-    if (collapse == 1 || W != 4) {
+    {
         // W - 2 greedy replacements; ar[] caches the entries' surfaces
         // (internal entries only; leaves and empty slots are never picked)
         float ar[W];
@@ -1111,16 +1110,7 @@ __device__ __forceinline__ void wide_entries(const uint4& tx, uint32_t L0, TopoO
 #pragma unroll
             for (int i = 0; i < W; ++i) { node[i] = nn[i]; ar[i] = na[i]; }
         }
-        return;
     }
-    uint32_t a0 = l, a1 = RT_SENT, b0 = r, b1 = RT_SENT;
-    if (l < L0) kids_of(topo_of(l), L0, a0, a1);
-    if (r < L0) kids_of(topo_of(r), L0, b0, b1);
-    // preorder, packed to the front: a0 [a1] b0 [b1]
-    node[0] = a0;
-    node[1] = a1 != RT_SENT ? a1 : b0;
-    node[2] = a1 != RT_SENT ? b0 : b1;
-    node[3 % W] = a1 != RT_SENT ? b1 : RT_SENT;
 }
 
 // K4 + K6 local + K7w local, fused.  One block = kRefitT consecutive sorted
@@ -1154,7 +1144,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
                                                         float* __restrict__ prebuf, float* __restrict__ sufbuf,
                                                         float* __restrict__ totals, uint32_t* __restrict__ cross,
                                                         uint32_t* cross_ctr, uint32_t cross_cap,
-                                                        uint4* __restrict__ wnodes, uint32_t collapse,
+                                                        uint4* __restrict__ wnodes,
                                                         uint32_t block0 = 0,
                                                         const uint32_t* __restrict__ flags_src = nullptr,
                                                         uint32_t* __restrict__ flags_dst = nullptr,
@@ -1275,7 +1265,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         uint32_t node[W];
         // every descendant of a local node is local: topology and boxes in LDS
         wide_entries<W>(tp, L0, [&](uint32_t i) { return s_topo[i - B0]; },
-                        [&](uint32_t i) { return s_box[T + i - B0]; }, collapse, node);
+                        [&](uint32_t i) { return s_box[T + i - B0]; }, node);
         uint32_t slot[W];
 #pragma unroll
         for (int i = 0; i < W; ++i)
@@ -1481,7 +1471,7 @@ __global__ __launch_bounds__(256) void k_refit_cross(const uint4* __restrict__ t
     }
 }
 
-// The greedy cut of wide_entries (collapse = 1) for a record built from
+// The greedy cut of wide_entries for a record built from
 // global memory (k_wide_cross), with each entry's box and topology cached
 // from ONE load of its record -- an internal entry's 32-B node record holds
 // both (topo_of_node), a leaf entry's triangle record gives its box -- so the
@@ -1589,7 +1579,7 @@ template <int W>
 __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ topo, const uint32_t* __restrict__ cross,
                                                     const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
                                                     const void* __restrict__ nodes, const float4* __restrict__ tri_s,
-                                                    uint32_t n, uint4* __restrict__ wnodes, uint32_t collapse) {
+                                                    uint32_t n, uint4* __restrict__ wnodes) {
     uint32_t pre[kCrossShards + 1];
     pre[0] = 0;
 #pragma unroll
@@ -1602,19 +1592,8 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         for (uint32_t j = 1; j < kCrossShards; ++j) sh += (q >= pre[j]) ? 1u : 0u;
         const uint32_t X = cross[sh * cross_cap + (q - pre[sh])];
         if (X >= L0) continue;
-        const uint4 tx = topo[X];
-        if (collapse == 1 || W != 4) {  // the greedy cut, one record load per entry
-            wide_record_g<W>(X, tx, load_aabb_node(nodes, X), L0, nodes, tri_s, wnodes);
-            continue;
-        }
-        uint32_t node[W];
-        // internal boxes from `nodes`, leaf boxes from the triangle records;
-        // a descendant's children from its node record (k_topo_refit writes
-        // topology words for crossing nodes only)
-        const auto box_of = [&](uint32_t i) { return i >= L0 ? leaf_box(tri_s, i - L0) : load_aabb_node(nodes, i); };
-        wide_entries<W>(tx, L0, [&](uint32_t i) { return topo_of_node(nodes, i, L0); }, box_of, collapse, node);
-        const Aabb bx = load_aabb_node(nodes, X);
-        store_wide<W>(wnodes, X, bx, node, [&](int i) { return box_of(node[i] == RT_SENT ? X : node[i]); }, L0);
+        // the greedy cut, one record load per entry
+        wide_record_g<W>(X, topo[X], load_aabb_node(nodes, X), L0, nodes, tri_s, wnodes);
     }
 }
 
@@ -1762,12 +1741,13 @@ static uint32_t cross_grid(uint32_t m, uint32_t floor_blocks) {
     return std::min<uint32_t>(4096u, std::max<uint32_t>(floor_blocks, cdiv(RT_XGRID_PER_BLOCK * m, 256)));
 }
 
-static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
-                                hipStream_t s) {
+static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t arity, hipStream_t s) {
     const uint32_t m = cdiv(n, kRefitT);
     if (m <= 1) return hipGetLastError();
     const uint32_t ng = cdiv(m, kGroupBlocks);
-    if (m <= kSmallTreeBlocks && config_snapshot().cross_small) {  // every block total in each block's LDS tree
+    // up to kSmallTreeBlocks refit blocks: every block total in each block's LDS tree, no group tables
+    // (r05: bunny/Sponza substitutes' crossing stage 18.1-19.2 -> 15.2-17.2 us, profiles/ab_cross_small_r05.log)
+    if (m <= kSmallTreeBlocks) {
         uint32_t P = 1;
         while (P < m) P <<= 1;
         RT_KLAUNCH(k_refit_cross<2>, dim3(cross_grid(m, RT_CROSS_GRID)), dim3(256), 2ull * P * sizeof(Aabb), s, b.topo,
@@ -1790,16 +1770,16 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t wide_col
     }
     if (arity == 8)
         RT_KLAUNCH(k_wide_cross<8>, dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
+                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes);
     else
         RT_KLAUNCH(k_wide_cross<4>, dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes, wide_collapse);
+                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes);
     return hipGetLastError();
 }
 
 // K4 + K5 + K6-local + K7w-local (k_topo_refit) over sorted keys/vals in
 // keys[0]/vals[0]; expects the crossing-list counters zeroed (K0 does it).
-static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
+static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t arity,
                                      uint32_t block0, uint32_t nblocks, hipStream_t s,
                                      uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr) {
     const uint32_t* fsrc = host_flags ? b.zero + kZDense : nullptr;
@@ -1807,28 +1787,27 @@ static hipError_t launch_topo_blocks(const BuildBufs& b, uint32_t n, uint32_t wi
     if (arity == 8)
         RT_KLAUNCH(k_topo_refit<8>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, block0, fsrc, host_flags, bstart);
     else
         RT_KLAUNCH(k_topo_refit<4>, dim3(nblocks), dim3(kRefitT), 0, s, b.keys[0], b.vals[0], b.tris, n,
                            b.topo, (uint32_t*)nullptr, b.nodes, b.tri_s, b.prebuf, b.sufbuf, b.table, b.cross,
-                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, wide_collapse, block0, fsrc, host_flags, bstart);
+                           b.zero + kZCrossCtr, cross_cap(m), b.wnodes, block0, fsrc, host_flags, bstart);
     return hipGetLastError();
 }
 
 // bstart (nullable): the [1025] bucket starts of the keys' top 10 bits (an
 // MSB or gather sort wrote them), for the long-range nodes' closed form
-static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t wide_collapse, uint32_t arity,
+static hipError_t launch_topo_local(const BuildBufs& b, uint32_t n, uint32_t arity,
                                     hipStream_t s, uint32_t* host_flags = nullptr, const uint32_t* bstart = nullptr) {
     if (!n) return hipSuccess;
-    return launch_topo_blocks(b, n, wide_collapse, arity, 0u, cdiv(n, kRefitT), s, host_flags, bstart);
+    return launch_topo_blocks(b, n, arity, 0u, cdiv(n, kRefitT), s, host_flags, bstart);
 }
 
 hipError_t launch_refit_stage(const BuildBufs& b, uint32_t n, hipStream_t s) {
-    const TraceConfig cfg = config_snapshot();
     hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
     if (e != hipSuccess) return e;
-    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
-    return n ? launch_cross(b, n, cfg.wide_collapse, b.warity, s) : hipSuccess;
+    if ((e = launch_topo_local(b, n, b.warity, s)) != hipSuccess) return e;
+    return n ? launch_cross(b, n, b.warity, s) : hipSuccess;
 }
 
 // ------------------------------------------- distributed build
@@ -1878,10 +1857,9 @@ hipError_t launch_dbuild_sort(uint32_t* keys[2], uint32_t* vals[2], uint32_t cnt
 // K4 + K5 + K6-local + K7w-local over refit blocks [block0, block0 + nblocks)
 // of the full sorted keys/vals in keys[0]/vals[0]
 hipError_t launch_dbuild_subtrees(const BuildBufs& b, uint32_t n, uint32_t block0, uint32_t nblocks, hipStream_t s) {
-    const TraceConfig cfg = config_snapshot();
     hipError_t e = hipMemsetAsync(b.zero + kZCrossCtr, 0, kCrossShards * 4, s);
     if (e != hipSuccess || !n || !nblocks) return e;
-    return launch_topo_blocks(b, n, cfg.wide_collapse, b.warity, block0, nblocks, s);
+    return launch_topo_blocks(b, n, b.warity, block0, nblocks, s);
 }
 
 uint32_t dbuild_cross_cap(uint32_t n) { return cross_cap(cdiv(n ? n : 1, kRefitT)); }
@@ -1890,7 +1868,7 @@ uint32_t refit_blocks(uint32_t n) { return n ? cdiv(n, kRefitT) : 0u; }
 // K6t + K7w of every crossing node, with the crossing list and counters
 // (b.cross / zero + kZCrossCtr) and every share's blocks in place
 hipError_t launch_dbuild_merge(const BuildBufs& b, uint32_t n, hipStream_t s) {
-    return n ? launch_cross(b, n, config_snapshot().wide_collapse, b.warity, s) : hipSuccess;
+    return n ? launch_cross(b, n, b.warity, s) : hipSuccess;
 }
 
 // The build's sort for this n and config: 0 = the 4-pass LSB sort, 1 = the
@@ -2013,9 +1991,9 @@ hipError_t launch_build(const BuildBufs& b, uint32_t n, hipStream_t s, BuildEven
     // bucket starts: written by the MSB/gather sort (a dense probe build's LSB
     // leg leaves them stale: that build searches as before)
     const uint32_t* bst = (kind != 0 && !probe) ? b.bstart : nullptr;
-    if ((e = launch_topo_local(b, n, cfg.wide_collapse, b.warity, s, host_flags, bst)) != hipSuccess) return e;
+    if ((e = launch_topo_local(b, n, b.warity, s, host_flags, bst)) != hipSuccess) return e;
     if ((e = rec(4)) != hipSuccess) return e;
-    if (n && (e = launch_cross(b, n, cfg.wide_collapse, b.warity, s)) != hipSuccess) return e;
+    if (n && (e = launch_cross(b, n, b.warity, s)) != hipSuccess) return e;
     if ((e = rec(5)) != hipSuccess) return e;
     if ((e = rec(6)) != hipSuccess) return e;  // K7w is fused into K4/K6 (records written with the boxes)
     return hipSuccess;

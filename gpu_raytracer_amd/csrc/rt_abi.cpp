@@ -19,6 +19,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -66,7 +67,6 @@ struct Replica {
     void* d_rgba = nullptr;
     size_t rgba_cap = 0;
     unsigned long long* d_ctr = nullptr;
-    uint32_t* d_work = nullptr;  // pool-trace unit counters
     SchedState ord;       // the frames' tile-order state (sched_for)
     SchedState ord_diag;  // scratch state of the counting launches: a diagnostic call never
                           // perturbs the next frame's order
@@ -267,13 +267,12 @@ rt_status replica_init(Replica& r) {
     // at each record, which would add ~4.7 us per event to the GPU timeline
     // between the kernels being timed.  Every host read of results goes
     // through a stream synchronize or a blocking copy.
-    const unsigned fl = rt::config_snapshot().event_fence ? hipEventDefault : hipEventDisableSystemFence;
+    const unsigned fl = hipEventDisableSystemFence;
     for (auto& e : r.ev.e) HIPR(hipEventCreateWithFlags(&e, fl));
     r.ev.valid = true;
     HIPR(hipEventCreateWithFlags(&r.r0, fl));
     HIPR(hipEventCreateWithFlags(&r.r1, fl));
     HIPR(hipEventCreateWithFlags(&r.last, hipEventDisableTiming | hipEventDisableSystemFence));
-    HIPR(rt::dev_alloc(&r.d_work, 4096));  // kPoolCounters x 128 B
     return RT_OK;
 }
 
@@ -282,19 +281,13 @@ void replica_free(Replica& r) {
     (void)hipSetDevice(r.device);
     if (r.last_pending) (void)hipEventSynchronize(r.last);  // device work on a caller stream
     (void)hipStreamSynchronize(r.stream);
-    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // trace.order_side, trace.coop_skip
+    for (SchedState* o : {&r.ord, &r.ord_diag}) {  // the queue-skip words
         if (o->sched.q_host) (void)hipHostFree(o->sched.q_host);
         o->sched.q_host = o->sched.q_dev = nullptr;
-        if (!o->sched.side) continue;
-        (void)hipStreamSynchronize(o->sched.side);
-        (void)hipEventDestroy(o->sched.ev_traced);
-        (void)hipEventDestroy(o->sched.ev_sorted);
-        (void)hipStreamDestroy(o->sched.side);
-        o->sched.side = nullptr;
     }
     rt::free_build(r.bufs);
     rt::free_path(r.path);
-    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, (void*)r.d_work, r.ord.d, r.ord_diag.d, r.d_slab, r.d_slab_hits, r.d_recv,
+    for (void* p : {r.d_hits, r.d_rgba, (void*)r.d_ctr, r.ord.d, r.ord_diag.d, r.d_slab, r.d_slab_hits, r.d_recv,
                     r.d_recv_hits, (void*)r.dk[0], (void*)r.dk[1], (void*)r.dv[0], (void*)r.dv[1], (void*)r.dcross,
                     (void*)r.dcross_all, (void*)r.dboxes})
         if (p) (void)hipFree(p);
@@ -574,21 +567,12 @@ rt_status sched_for(SchedState& r, uint32_t w, uint32_t h, uint32_t spp, uint32_
     const size_t maps = 5ull * nb * 4 + 2ull * nb * 512;
     const size_t qoff = (maps + 255) & ~size_t(255);
     const size_t need = qcap ? qoff + 512 + (size_t)rt::kCoopEntryBytes * qcap : maps;
-    if (!r.sched.side && cfg.order_side) {  // trace.order_side's stream and events (on the caller's current device)
-        HIPR(hipStreamCreateWithFlags(&r.sched.side, hipStreamNonBlocking));
-        HIPR(hipEventCreateWithFlags(&r.sched.ev_traced, hipEventDisableTiming | hipEventDisableSystemFence));
-        HIPR(hipEventCreateWithFlags(&r.sched.ev_sorted, hipEventDisableTiming | hipEventDisableSystemFence));
-    }
-    if (!r.sched.q_host) {  // trace.coop_skip's queue-length word
+    if (!r.sched.q_host) {  // the queue skip's queue-length word
         HIPR(hipHostMalloc(reinterpret_cast<void**>(&r.sched.q_host), 64, hipHostMallocMapped));
         HIPR(hipHostGetDevicePointer(reinterpret_cast<void**>(&r.sched.q_dev), r.sched.q_host, 0));
         __atomic_store_n(r.sched.q_host, ~0u, __ATOMIC_RELAXED);
     }
     if (!same || r.cap < need || r.sched.coop_qcap != qcap) {
-        if (r.sched.side_pending) {  // a side sort still writing the maps about to be replaced
-            HIPR(hipEventSynchronize(r.sched.ev_sorted));
-            r.sched.side_pending = false;
-        }
         std::memset(r.key, 0, sizeof(r.key));  // invalid until the maps exist
         __atomic_store_n(r.sched.q_host, ~0u, __ATOMIC_RELAXED);  // a new shape: its queue length not yet known
         r.sched.q_frames = 0;
@@ -655,27 +639,17 @@ rt_status need_built(rt_scene* s, Replica** out) {
 
 bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
     const std::string k(key);
-    if (k == "trace.variant" && value >= 0 && value <= 2) c.variant = (uint32_t)value;
+    if (k == "trace.variant" && (value == 0 || value == 2)) c.variant = (uint32_t)value;
     else if (k == "trace.stack_cap" && value >= 0 && value <= rt::kWideStackMax) c.stack_cap = (uint32_t)value;
     else if (k == "trace.wg" && (value == 64 || value == 256)) c.wg = (uint32_t)value;
     else if (k == "trace.wg_tiles" && (value == 64 || value == 256)) c.wg_tiles = (uint32_t)value;
     else if (k == "trace.tile_order" && (value == 0 || value == 1)) c.tile_order = (uint32_t)value;
     else if (k == "trace.px_sort" && value >= 0 && value <= 2) c.px_sort = (uint32_t)value;
     else if (k == "trace.spp_lanes" && value >= 0 && value <= 2) c.spp_lanes = (uint32_t)value;
-    else if (k == "trace.nt_hits" && value >= 0 && value <= 3) c.nt_hits = (uint32_t)value;
-    else if (k == "trace.sl_mtf" && (value == 0 || value == 1)) c.sl_mtf = (uint32_t)value;
-    else if (k == "trace.sl_fold" && (value == 0 || value == 1)) c.sl_fold = (uint32_t)value;
-    else if (k == "trace.coop_order" && (value == 0 || value == 1)) c.coop_order = (uint32_t)value;
-    else if (k == "trace.order_side" && (value == 0 || value == 1)) c.order_side = (uint32_t)value;
-    else if (k == "trace.coop_skip" && (value == 0 || value == 1)) c.coop_skip = (uint32_t)value;
-    else if (k == "trace.blocks" && value >= 0 && value <= (1 << 20)) c.blocks = (uint32_t)value;
     else if (k == "build.sort" && value >= 0 && value <= 2) c.sort_msb = (uint32_t)value;
     else if (k == "build.fuse_k01" && value >= 0 && value <= 2) c.fuse_k01 = (uint32_t)value;
-    else if (k == "build.wide_collapse" && (value == 0 || value == 1)) c.wide_collapse = (uint32_t)value;
     else if (k == "build.wide_arity" && (value == 4 || value == 8)) c.wide_arity = (uint32_t)value;
     else if (k == "build.stage_events" && (value == 0 || value == 1)) c.stage_events = (uint32_t)value;
-    else if (k == "build.cross_small" && (value == 0 || value == 1)) c.cross_small = (uint32_t)value;
-    else if (k == "timing.event_fence" && (value == 0 || value == 1)) c.event_fence = (uint32_t)value;
     else if (k == "path.wavefront" && (value == 0 || value == 1)) c.path_wave = (uint32_t)value;
     else if (k == "path.wg" && (value == 64 || value == 256)) c.path_wg = (uint32_t)value;
     else if (k == "path.sort" && value >= 0 && value <= 4) c.path_sort = (uint32_t)value;
@@ -686,7 +660,6 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
         c.coop_cap = value < 0 ? rt::kCoopCapAuto : (uint32_t)value;
     else if (k == "trace.coop_cap_tiles" && value >= -1 && value <= (1 << 20))
         c.coop_cap_tiles = value < 0 ? rt::kCoopCapAuto : (uint32_t)value;
-    else if (k == "trace.buf_loads" && (value == 0 || value == 1)) c.buf_loads = (uint32_t)value;
     else if (k == "trace.coop_lanes" && (value == 16 || value == 32 || value == 64)) c.coop_lanes = (uint32_t)value;
     else if (k == "trace.coop_max" && value >= 1 && value <= (1 << 24)) c.coop_max = (uint32_t)value;
     else if (k == "debug.poison" && (value == 0 || value == 1)) c.poison = (uint32_t)value;
@@ -701,7 +674,7 @@ bool apply_config(rt::TraceConfig& c, const char* key, int64_t value) {
 extern "C" {
 
 const char* rt_last_error(void) { return g_err.c_str(); }
-const char* rt_version(void) { return "gpu_raytracer_amd 0.3 (gfx950)"; }
+const char* rt_version(void) { return "gpu_raytracer_amd 0.4 (gfx950)"; }
 
 rt_status rt_config_set(const char* key, int64_t value) {
     if (!key) return fail(RT_EINVAL, "null key");
@@ -890,6 +863,20 @@ rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out) {
     const Replica* r = primary_built(s);
     if (!r) return fail(RT_EINVAL, "scene not built");
     *out = r->times;
+    return RT_OK;
+}
+
+// the struct grew in 0.3 and carries no size of its own, so a
+// caller states the size it was compiled with; the prefix that fits is
+// written (never past out_size).  The 0.2 layout (64 B: seven doubles and
+// sort_kind / fused_k01) is the smallest accepted.
+rt_status rt_bvh_build_times_sized(const rt_scene* s, rt_build_times* out, size_t out_size) {
+    if (!s || !out) return fail(RT_EINVAL, "null argument");
+    if (out_size < offsetof(rt_build_times, fused_fallback))
+        return fail(RT_EINVAL, "rt_build_times smaller than the 0.2 layout");
+    const Replica* r = primary_built(s);
+    if (!r) return fail(RT_EINVAL, "scene not built");
+    std::memcpy(out, &r->times, std::min(out_size, sizeof(rt_build_times)));
     return RT_OK;
 }
 
@@ -1225,7 +1212,7 @@ rt_status render_tiled(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_t h
         RTR(sched_for(R.ord, w, h, spp, r, P, &sched));
         hipError_t e = rt::launch_trace(R.bufs.nodes, R.bufs.wnodes, R.bufs.warity,
                                         R.bufs.tri_s, s->n, camf(cam), w, h, spp, r, P,
-                                        true, hits_out ? R.d_slab_hits : nullptr, R.d_slab, nullptr, false, R.d_work,
+                                        true, hits_out ? R.d_slab_hits : nullptr, R.d_slab, nullptr, false,
                                         sched, R.stream);
         if (e != hipSuccess) return hip_fail(e, "launch_trace");
         sched_done(R.ord, cfg);
@@ -1304,7 +1291,7 @@ rt_status rt_render_timed(rt_scene* s, const rt_camera* cam, uint32_t w, uint32_
     HIPR(hipEventRecord(r->r0, r->stream));
     hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                     r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1,
-                                    false, hits_out ? r->d_hits : nullptr, r->d_rgba, nullptr, false, r->d_work, sched,
+                                    false, hits_out ? r->d_hits : nullptr, r->d_rgba, nullptr, false, sched,
                                     r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     sched_done(r->ord, cfg);
@@ -1515,7 +1502,7 @@ static rt_status counters_impl(rt_scene* s, const rt_camera* cam, uint32_t w, ui
     }
     hipError_t e = rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                     r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank,
-                                    nranks, packed, nullptr, nullptr, r->d_ctr, binary, r->d_work, sched, r->stream);
+                                    nranks, packed, nullptr, nullptr, r->d_ctr, binary, sched, r->stream);
     if (e != hipSuccess) return hip_fail(e, "launch_trace");
     HIPR(hipStreamSynchronize(r->stream));
     HIPR(hipMemcpy(counters_out, r->d_ctr, 16, hipMemcpyDeviceToHost));
@@ -1574,7 +1561,7 @@ rt_status rt_render_device(rt_scene* s, const rt_camera* cam, uint32_t w, uint32
     RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
         return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                 r->bufs.tri_s, s->n, camf(cam), w, h, spp, 0, 1, false,
-                                d_hits, d_rgba, nullptr, false, r->d_work, sched, hs);
+                                d_hits, d_rgba, nullptr, false, sched, hs);
     }));
     sched_done(r->ord, cfg);
     return RT_OK;
@@ -1598,7 +1585,7 @@ rt_status rt_render_tiles_device(rt_scene* s, const rt_camera* cam, uint32_t w, 
     RTR(device_launch(*r, stream, ms_out, "launch_trace", [&](hipStream_t hs) {
         return rt::launch_trace(r->bufs.nodes, r->bufs.wnodes, r->bufs.warity,
                                 r->bufs.tri_s, s->n, camf(cam), w, h, spp, rank, nranks,
-                                true, d_packed_hits, d_packed_rgba, nullptr, false, r->d_work, sched, hs);
+                                true, d_packed_hits, d_packed_rgba, nullptr, false, sched, hs);
     }));
     sched_done(r->ord, cfg);
     return RT_OK;
@@ -1763,12 +1750,11 @@ rt_status rt_stage_trace(int device, const rt_node* nodes, uint32_t n, const flo
         HIPR(hipMemcpy(dn.p, nodes, tot * 32, hipMemcpyHostToDevice));
         HIPR(hipMemcpy(dt.p, tris, (size_t)n * 36, hipMemcpyHostToDevice));
     }
-    DevBuf dts, dw;
+    DevBuf dts;
     HIPR(dts.alloc((size_t)(n ? n : 1) * 48));
-    HIPR(dw.alloc(4096));
     HIPR(rt::launch_leaf_tris(dn.p, dt.as<float>(), n, dts.as<float4>(), 0));
     HIPR(rt::launch_trace(dn.p, nullptr, 4u, dts.as<float4>(), n, camf(cam), w, h, spp, 0, 1, false, dh.p, dr.p,
-                          counters ? dc.as<unsigned long long>() : nullptr, true, dw.as<uint32_t>(), nullptr, 0));
+                          counters ? dc.as<unsigned long long>() : nullptr, true, nullptr, 0));
     HIPR(hipDeviceSynchronize());
     if (hits) HIPR(hipMemcpy(hits, dh.p, nh * 16, hipMemcpyDeviceToHost));
     if (rgba) HIPR(hipMemcpy(rgba, dr.p, (size_t)w * h * 4, hipMemcpyDeviceToHost));

@@ -134,7 +134,7 @@ constexpr int kWideStack = RT_WIDE_STACK;
 //   w4 = {ref0..ref3}, w5 = {ref4..ref7}
 // A traversal step over it replaces up to three binary levels (two for the
 // 4-ary form): the heaviest rays' dependent fetch chains are ~25 % shorter
-// (tools/wide_sim.py).  Its per-ray stacks hold 18 entries (a record pushes
+// (tests/tools/wide_sim.py).  Its per-ray stacks hold 18 entries (a record pushes
 // up to 7).
 template <int W> struct WideFmt;
 template <> struct WideFmt<4> {
@@ -164,7 +164,6 @@ template <int W, int NT> struct StackOf {
 constexpr int kWideStackMax = (RT_WIDE_STACK64 > 18 && RT_WIDE_STACK64 > kWideStack) ? RT_WIDE_STACK64
                               : (kWideStack > 18 ? kWideStack : 18);
 constexpr uint32_t kWideRecMaxBytes = 96;  // wnodes is allocated for either arity
-constexpr uint32_t kPoolCounters = 32;  // pool-trace unit counters, 128 B apart (work buffer >= 4 KiB)
 
 // plane = origin + q * 2^e, rounded once: q * 2^e is exact (q < 2^8 and
 // -126 <= e <= 119, so no overflow and an exact denormal at worst), hence

@@ -173,23 +173,10 @@ inline uint32_t coop_cap_for_sl(uint32_t knob) { return knob == kCoopCapAuto ? 0
 // Trace kernel selection / tuning (rt_config_set); every setting gives
 // bit-identical hits and images.
 struct TraceConfig {
-    uint32_t variant = 0;       // 0 wide per-pixel (default), 1 wide pool with refill, 2 binary per-pixel
-    uint32_t blocks = 0;        // pool grid (0 = resident capacity from the occupancy API)
+    uint32_t variant = 0;       // 0 wide per-pixel (default), 2 binary per-pixel (1, the r01 wide pool with
+                                // refill, was removed in r06: measured slower, profiles/rejected_knobs_r06.patch)
     uint32_t wg = 256;          // per-pixel kernels: threads per workgroup (256 = 16x16 tile, 64 = 8x8)
     uint32_t wg_tiles = 64;     // same, for one rank's tiles of a multi-GPU frame (nranks > 1)
-    uint32_t nt_hits = 2;       // nontemporal hit-record stores: 2 = always (default), 1 = frames of >= 2 spp,
-                                // 0 = never (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the frame unchanged;
-                                // the 1M build after a 1080p1 frame 140.3 -> 137.7 us, profiles/ab_nt_hits_1spp_r05.log)
-    uint32_t coop_skip = 1;     // automatic caps: 1 = skip the queue for a shape whose last queue-on frame queued
-                                // < kQueueSkip rays (re-probing every kQueueProbe-th frame); 0 = never
-    uint32_t order_side = 0;    // queue on: 1 = the next order sorted on a side stream (TileSched::side), not in
-                                // k_trace_coop's block 0 (its critical path when the queue is short: bunny substitute
-                                // -3 to -7 %, soup-1M +1 %, profiles/ab_order_side_r05.log; off by default)
-    uint32_t coop_order = 1;    // queue on: 1 = k_trace_coop's block 0 sorts this frame's costs into the next order,
-                                // 0 = k_trace's extra block folds the previous frame's (as with the queue off)
-    uint32_t sl_fold = 1;       // k_trace_sl (full frames, one rank's tiles): 1 = block 0 sorts the next frame's tile
-                                // order (no k_tile_order launch)
-    uint32_t sl_mtf = 1;        // k_trace_sl on one rank's tiles: 1 = Moller-Trumbore before the leaf box test
     uint32_t spp_lanes = 2;     // samples in lanes (k_trace_sl) for 2..16 (power of two) spp: 2 = full frames and
                                 // one rank's tiles (default), 1 = tiles only, 0 = off (a lane loops over its samples)
     uint32_t stack_cap = 0;     // wide stack entries used (tests force the overflow path); 0 = the arity's
@@ -199,11 +186,9 @@ struct TraceConfig {
     uint32_t path_sort = 0;     // wavefront: top key bytes the ray queue is sorted by (0 = unsorted, default)
     uint32_t path_batch = 0;    // wavefront: paths per batch (0 = 4M)
     uint32_t stage_events = 0;  // build: record the per-stage events (rt_bvh_build_times); else total only
-    uint32_t event_fence = 0;   // timing events with the system-scope fence (scenes created afterwards)
     uint32_t tile_order = 1;    // 1: longest-first from the previous same-size frame's wave times; 0: row-major
     uint32_t px_sort = 1;       // with tile_order: each tile's pixels to lanes costliest first (previous
                                 // frame); 1 = full frames only, 2 = also one rank's tiles, 0 = off
-    uint32_t wide_collapse = 1; // K7w entries: 1 = greedy largest-surface cut, 0 = fixed two levels
     uint32_t wide_arity = 4;    // build.wide_arity: 4 = K7w 64-B records, 8 = K7w8 96-B records (greedy cut)
     uint32_t fuse_k01 = 1;      // build.fuse_k01: 1 = K0 + K1 as one launch with a grid barrier when the grid
                                 // is co-resident and no other fused build runs on the device (gather sort);
@@ -213,7 +198,6 @@ struct TraceConfig {
     uint32_t render_emulate = 0;  // rt_render(ngpus > 1): 1 = every rank's replica on the scene's device, gather
                                   // by device copies (tests on a one-GPU box); 0 = one device per rank + RCCL
     uint32_t render_rccl1 = 0;    // rt_render(ngpus = 1) through the tiled + RCCL path (1-rank communicator)
-    uint32_t buf_loads = 1;       // wide step loads through buffer descriptors (one round trip per step)
     uint32_t coop_cap = kCoopCapAuto;  // primary full frames: rays past this many wide steps finish in
                                   // k_trace_coop (lane groups per ray); 0 = off; auto (default):
                                   // coop_cap_for_frame
@@ -228,8 +212,6 @@ struct TraceConfig {
     uint32_t lds_scribble = 0;    // debug.lds_scribble: before every kernel launch, fill the LDS of the
                                   // CUs with a fresh pseudo-random pattern, so a kernel that reads LDS
                                   // it did not write gives a different (wrong) result every launch
-    uint32_t cross_small = 1;   // build.cross_small: 1 = up to 1024 refit blocks, the crossing boxes from one LDS tree over
-                                // every block total (no group-table launch); 0 = the group tables at every size
     uint32_t force_lsb_redo = 0;  // debug.force_lsb_redo: treat every gather-sort build as if a bucket
                                   // had overflowed (tests the host's discard-and-redo branch)
 };
@@ -278,16 +260,13 @@ struct TileSched {
     bool have_prev = false;
     bool order_ready = false;       // `order` for this frame already sorted by the previous frame's k_trace_coop
     bool fresh = true;              // maps (re)allocated: clear both before the first launch
-    // trace.order_side: with the heavy-ray queue on, the next frame's order
-    // is sorted by k_tile_order on this side stream once k_trace is done
-    // (ev_traced), beside k_trace_coop and whatever follows; the next frame's
-    // launch waits for ev_sorted.  Created by the owner (rt_abi.cpp sched_for).
-    hipStream_t side = nullptr;
-    hipEvent_t ev_traced = nullptr, ev_sorted = nullptr;
-    bool side_pending = false;      // ev_sorted not yet waited for
-    // trace.coop_skip: the queue length k_trace_coop reported for the latest
-    // queue-on frame of this shape (mapped pinned host word; ~0u = not yet
-    // known), and the queue-off frames since
+    // Queue skip (automatic caps): the queue length k_trace_coop reported for
+    // the latest queue-on frame of this shape (mapped pinned host word; ~0u =
+    // not yet known), and the queue-off frames since.  Best effort (ADVICE
+    // r05): the host reads the word without waiting for the frame that writes
+    // it, so with frames queued ahead of the host the value may be a few
+    // frames old; it only decides whether a frame runs the queue, never a
+    // pixel's result.
     uint32_t* q_host = nullptr;
     uint32_t* q_dev = nullptr;
     uint32_t q_frames = 0;
@@ -316,7 +295,7 @@ constexpr int kMaxDevices = 64;
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tri_s, uint32_t n,
                         const CamF& cam,
                         uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks, bool packed,
-                        void* hits, void* rgba, unsigned long long* counters, bool binary_counts, uint32_t* work,
+                        void* hits, void* rgba, unsigned long long* counters, bool binary_counts,
                         TileSched* sched, hipStream_t s);
 // Shadow mode: primary hits into `hits`, Lambert + shadow-ray
 // shaded image into `rgba`; tris = the scene's AoS triangles (normals).

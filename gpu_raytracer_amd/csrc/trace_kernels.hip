@@ -550,7 +550,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// A hit record store.  nt (trace.nt_hits): nontemporal -- a frame's hit
+// A hit record store.  nt: nontemporal (primary frames, launch_trace) -- a frame's hit
 // records (530 MB at 4Kx4 or 1080p x 16, 33 MB at 1080p1) stream to HBM while the
 // trace, which uses a few % of HBM bandwidth, runs, instead of staying dirty
 // in L2 / the MALL until the next build's soup read evicts them (DESIGN.md
@@ -1094,8 +1094,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
         if (dsamp == RT_SENT && rgba) {
             const float sc = 1.0f / (float)spp;
             const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
-            if (nt_hits > 1) __builtin_nontemporal_store(px, rgba + pi);
-            else rgba[pi] = px;
+            rgba[pi] = px;
         }
     }
 #ifdef RT_STAMPS
@@ -1270,8 +1269,7 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
     if (valid && smp == 0 && !(dm & pm) && rgba) {
         const float sc = 1.0f / (float)S;
         const uint32_t px = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
-        if (nt_hits > 1) __builtin_nontemporal_store(px, rgba + pi);
-        else rgba[pi] = px;
+        rgba[pi] = px;
     }
     if (cost_out && l == 0) {  // this unit's duration -> its tile's cost map entry (the tile order's key)
         const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - wt0;
@@ -2072,146 +2070,6 @@ __global__ __launch_bounds__(256) void k_pw_finish(const float* __restrict__ pf,
     rgba[(uint64_t)y * W + x] = q8(r * sc) | (q8(g * sc) << 8) | (q8(b * sc) << 16) | (255u << 24);
 }
 
-// ---------------------------------------------------------------- pool
-// Wide traversal with per-lane refill.  The rank's tiles are cut into 8x8
-// units (unit u = quarter u%4 of tile slot u/4), dealt to the waves of a
-// resident grid through sharded atomic counters (a single counter hit by
-// every wave serialises).  A lane
-// whose pixel is finished takes the next pixel of the wave's current unit,
-// then of its next unit, so the wave no longer idles behind its slowest ray
-// until its very last unit.  A lane owns a whole pixel (its spp samples in
-// order), which keeps the §9.7 per-pixel sample average sequential.
-template <bool COUNT, bool PACKED>
-__global__ __launch_bounds__(256) void k_trace_pool(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
-                                                    uint32_t wcap, const float4* __restrict__ tri_s, uint32_t n,
-                                                    Cam cam, uint32_t W, uint32_t H, uint32_t spp, uint32_t rank,
-                                                    uint32_t nranks, uint32_t tilesX, uint32_t nunits,
-                                                    float4* __restrict__ hits, uint32_t* __restrict__ rgba,
-                                                    unsigned long long* __restrict__ counters,
-                                                    uint32_t* __restrict__ work) {
-    __shared__ uint32_t s_ref[(kWideStack + 1) * 256];
-    __shared__ uint16_t s_tn[(kWideStack + 1) * 256];
-    uint32_t* sref = s_ref + threadIdx.x;
-    uint16_t* stn = s_tn + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t g = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const SceneBox sb = scene_box(nodes);
-    const float o[3] = {cam.eye[0], cam.eye[1], cam.eye[2]};
-    const uint32_t limit = 4 * n + 16;
-#ifdef RT_STAMPS
-    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
-    uint32_t iters = 0, fb = 0;
-#endif
-    // wave-uniform cursor: current unit and the next pixel in it.  Units are
-    // dealt dynamically from kPoolCounters counters (one 128-B line each;
-    // counter c owns units c, c+C, c+2C, ...), wave g drawing from c = g % C.
-    const uint32_t cidx = g % kPoolCounters;
-    auto grab = [&]() -> uint32_t {
-        uint32_t j = 0;
-        if (lane == 0) j = atomicAdd(&work[cidx * 32], 1u);
-        j = __shfl(j, 0, 64);
-        return cidx + kPoolCounters * j;
-    };
-    uint32_t unit = grab(), next = 0;
-    // lane state
-    bool have = false;
-    uint32_t x = 0, y = 0, slot = 0, pl = 0, s = 0;
-    float cr = 0.0f, cg = 0.0f, cb = 0.0f;
-    WRay R;
-    uint32_t cn = 0, ct = 0;
-    for (;;) {
-        // ---- refill: idle lanes take the next pixels, in lane order
-        uint64_t idle = __ballot(!have);
-        while (idle && unit < nunits) {
-            const uint32_t take = min((uint32_t)__popcll(idle), 64u - next);
-            const uint32_t pos = lanes_below(idle);
-            if (!have && pos < take) {
-                const uint32_t p = next + pos, q = unit & 3;
-                slot = unit >> 2;
-                const uint32_t lx = (q & 1) * 8 + (p & 7), ly = (q >> 1) * 8 + (p >> 3);
-                pl = ly * 16 + lx;
-                const uint32_t t = rank + slot * nranks;
-                x = (t % tilesX) * 16 + lx;
-                y = (t / tilesX) * 16 + ly;
-                if (x < W && y < H) {
-                    have = true;
-                    s = 0;
-                    cr = cg = cb = 0.0f;
-                    wray_setup(cam, x, y, W, spp, 0, R, sb);
-                }
-            }
-            next += take;
-            if (next >= 64) { unit = grab(); next = 0; }
-            idle = __ballot(!have);
-        }
-        if (__ballot(have) == 0) break;  // no ray in flight and no units left
-#ifdef RT_STAMPS
-        ++iters;
-#endif
-        if (have) {
-            int st = R.fin ? wide_step<COUNT, 256>(R, wnodes, tri_s, o, wcap, limit, sref, stn, cn, ct) : 2;
-            if (st == 2) {
-#ifdef RT_STAMPS
-                fb += 1u << 16;
-#endif
-                if (!R.fin) { R.cur = 0; R.tb = __builtin_inff(); R.hu = R.hv = 0.0f; R.hp = RT_SENT; }
-                trace_ray_from<COUNT>(reinterpret_cast<const char*>(nodes), tri_s, n, o, R.d,
-                                      R.cur == RT_SENT ? RT_SENT : bin_of(R.cur, n - 1), R.tb, R.hu, R.hv, R.hp, cn,
-                                      ct);
-                st = 1;
-            }
-            if (st == 1) {
-                if (hits) {
-                    const uint64_t hi = PACKED ? ((uint64_t)slot * 256 + pl) * spp + s : (uint64_t)(y * W + x) * spp + s;
-                    hits[hi] = make_float4(R.tb, R.hu, R.hv, __uint_as_float(R.hp));
-                }
-                if (R.hp != RT_SENT) {
-                    cr = cr + R.hu;
-                    cg = cg + R.hv;
-                    cb = cb + ((1.0f - R.hu) - R.hv);
-                } else {
-                    cr = cr + 0.0f; cg = cg + 0.0f; cb = cb + 0.0f;
-                }
-                if (++s < spp) {
-                    wray_setup(cam, x, y, W, spp, s, R, sb);
-                } else {
-                    if (rgba) {
-                        const float sc = 1.0f / (float)spp;
-                        const uint32_t px = q8(cr * sc) | (q8(cg * sc) << 8) | (q8(cb * sc) << 16) | (255u << 24);
-                        const uint64_t pi = PACKED ? (uint64_t)slot * 256 + pl : (uint64_t)y * W + x;
-                        rgba[pi] = px;
-                    }
-                    have = false;
-                }
-            }
-        }
-    }
-#ifdef RT_STAMPS
-    uint32_t fbw = fb;
-    for (int off = 32; off >= 1; off >>= 1) fbw += __shfl_xor(fbw, off, 64);
-    if (lane == 0) {
-        const uint64_t wslot = (uint64_t)g * 4;
-        g_rt_stamps[wslot + 0] = st0;
-        g_rt_stamps[wslot + 1] = __builtin_amdgcn_s_memrealtime();
-        g_rt_stamps[wslot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
-                                 ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
-        g_rt_stamps[wslot + 3] = iters | ((uint64_t)fbw << 16);
-    }
-#endif
-    if (COUNT) {
-        unsigned long long a = cn, bsum = ct;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            a += __shfl_xor(a, off, 64);
-            bsum += __shfl_xor(bsum, off, 64);
-        }
-        if (lane == 0) {
-            atomicAdd(&counters[0], a);
-            atomicAdd(&counters[1], bsum);
-        }
-    }
-}
-
 // Gathered slabs [rank][tile][256 px] -> W x H image.
 __global__ __launch_bounds__(256) void k_unpack(const uint32_t* __restrict__ slabs, uint32_t tiles_per_slab, uint32_t W,
                                                 uint32_t H, uint32_t nranks, uint32_t tilesX, uint32_t ntiles,
@@ -2403,7 +2261,7 @@ static void k_trace_go(bool buf, uint32_t warity, bool cq, bool spp1, uint32_t g
 hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity, const float4* tris, uint32_t n,
                         const CamF& c, uint32_t w, uint32_t h, uint32_t spp, uint32_t rank, uint32_t nranks,
                         bool packed, void* hits, void* rgba, unsigned long long* counters, bool binary_counts,
-                        uint32_t* work, TileSched* sched, hipStream_t s) {
+                        TileSched* sched, hipStream_t s) {
     const TraceConfig cfg = config_snapshot();
     const uint32_t nb = tiles_for_rank(w, h, rank, nranks);
     if (!nb) return hipSuccess;
@@ -2416,44 +2274,6 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     uint32_t* R = reinterpret_cast<uint32_t*>(rgba);
     if (warity != 4 && warity != 8) return hipErrorInvalidValue;
     if (warity == 8 && n > kWide8MaxN) return hipErrorInvalidValue;  // the build keeps 8-ary records to n <= kWide8MaxN
-    const uint32_t cap = stack_cap_for(cfg, warity, 256);  // the pool's 256-thread blocks
-    if (cfg.variant == 1 && wnodes && warity == 4 && n >= 2 && !binary_counts && work) {
-        const uint32_t nunits = nb * 4;
-        hipError_t me = hipMemsetAsync(work, 0, kPoolCounters * 128, s);
-        if (me != hipSuccess) return me;
-        uint32_t blocks = cfg.blocks;
-        if (!blocks) {  // auto: exactly the resident capacity (one wave per SIMD slot, no second round)
-            // per device (a process may drive several), computed once each
-            static std::atomic<uint32_t> resident[kMaxDevices];
-            int dev = 0;
-            hipError_t e = hipGetDevice(&dev);
-            if (e != hipSuccess) return e;
-            if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
-            uint32_t r = resident[dev].load(std::memory_order_relaxed);
-            if (!r) {
-                int per_cu = 0, cus = 0;
-                e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                    &per_cu, reinterpret_cast<const void*>(k_trace_pool<false, false>), 256, 0);
-                if (e != hipSuccess) return e;
-                if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
-                    return e;
-                r = (uint32_t)(per_cu > 0 ? per_cu : 1) * (uint32_t)(cus > 0 ? cus : 1);
-                resident[dev].store(r, std::memory_order_relaxed);
-            }
-            blocks = r;
-        }
-        const uint32_t grid = min(blocks, (nunits + 3) / 4);
-#define RT_POOL(C, P)                                                                                               \
-    RT_KLAUNCH((k_trace_pool<C, P>), dim3(grid), dim3(256), 0, s, nodes, wnodes, cap, tris, n, cam, w, h, spp, \
-                       rank, nranks, tilesX, nunits, H, R, counters, work)
-        if (counters) {
-            if (packed) RT_POOL(true, true); else RT_POOL(true, false);
-        } else {
-            if (packed) RT_POOL(false, true); else RT_POOL(false, false);
-        }
-#undef RT_POOL
-        return hipGetLastError();
-    }
     // wide (4-ary) traversal unless asked for the binary one: variant 2, no
     // K7w records (stage entry points), n < 2, or binary work counters
     const bool wide = wnodes && n >= 2 && cfg.variant != 2 && !binary_counts;
@@ -2469,11 +2289,12 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         wide && sched && sched->coop_q && n <= kBufMaxN
             ? (nranks > 1 ? coop_cap_for_tiles(cfg.coop_cap_tiles, nranks) : coop_cap_for_frame(cfg.coop_cap, spp, small))
             : 0u;
-    // trace.coop_skip: with the automatic cap, a frame shape whose last queue-on frame queued fewer than
+    // queue skip: with the automatic cap, a frame shape whose last queue-on frame queued fewer than
     // kQueueSkip rays runs without the queue (its pass would be all launch and order sort), re-probing
-    // every kQueueProbe-th frame (an explicit cap always runs the queue)
+    // every kQueueProbe-th frame (an explicit cap always runs the queue).  Best effort: q_host may be a
+    // few frames old (TileSched::q_host); it picks the schedule, never a result.
     const bool cap_auto = (nranks > 1 ? cfg.coop_cap_tiles : cfg.coop_cap) == kCoopCapAuto;
-    if (coop_cap0 && cap_auto && cfg.coop_skip && sched->q_host) {
+    if (coop_cap0 && cap_auto && sched->q_host) {
         if (__atomic_load_n(sched->q_host, __ATOMIC_RELAXED) < kQueueSkip && sched->q_frames + 1 < kQueueProbe) {
             coop_cap0 = 0u;
             ++sched->q_frames;
@@ -2484,7 +2305,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     // samples in lanes (k_trace_sl): multi-spp tiles and full frames (trace.spp_lanes = 2, the default;
     // 1 = tiles only)
     const bool sl = spp >= 2 && spp <= 16 && (spp & (spp - 1)) == 0 && wide && warity == 4 && !counters &&
-                    n <= kBufMaxN && cfg.buf_loads &&
+                    n <= kBufMaxN &&
                     (cfg.spp_lanes == 2 || (cfg.spp_lanes == 1 && (packed || nranks > 1)));
     // its queue needs the hits of every sample (k_coop_resolve), so no queue without a hits buffer
     const uint32_t sl_cap = !sl || !hits || !sched || !sched->coop_q ? 0u
@@ -2492,24 +2313,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
     const uint32_t coop_cap = sl ? sl_cap : coop_cap0;
     // (k_trace's extra block holds its costs in registers: nb <= 8192, full frames; k_trace_sl's block 0
     // loops, any nb, full frames and one rank's tiles)
-    // (with the heavy-ray queue on, k_trace_coop's block 0 sorts this frame's costs instead, unless
-    // trace.coop_order = 0)
-    const bool can_fold = RT_ORDER_FOLD && sched && wide && !counters && !cfg.order_override &&
-                          (sl ? cfg.sl_fold != 0 && coop_cap == 0
-                              : nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread &&
-                                    (coop_cap == 0 || !cfg.coop_order));
+    // (with the heavy-ray queue on, k_trace_coop's block 0 sorts this frame's costs instead)
+    const bool can_fold = RT_ORDER_FOLD && sched && wide && !counters && !cfg.order_override && coop_cap == 0 &&
+                          (sl || (nranks == 1 && !packed && !small && nb <= 256 * kFoldPerThread));
     OrderFold fold;
-    if (sched && sched->side_pending) {  // the previous frame's order, sorted on the side stream
-        // (a cross-queue wait costs the frame a few us even when the sort is long done: only when it is not)
-        const hipError_t qe = hipEventQuery(sched->ev_sorted);
-        if (qe == hipErrorNotReady) {
-            const hipError_t we = hipStreamWaitEvent(s, sched->ev_sorted, 0);
-            if (we != hipSuccess) return we;
-        } else if (qe != hipSuccess) {
-            return qe;
-        }
-        sched->side_pending = false;
-    }
     if (sched && cfg.tile_order && nb <= 1024 * kOrderPerThread) {
         if (sched->fresh) {  // new maps: clear both once (k_tile_order clears the one it reads)
             hipError_t me = hipMemsetAsync(sched->cost_prev, 0, (size_t)nb * 4, s);
@@ -2578,11 +2385,10 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         cq.cap = sched->coop_qcap / kCoopShards;
     }
     // buffer loads for the wide step whenever the offsets fit 32 bits (WideMem)
-    const bool buf = n <= kBufMaxN && cfg.buf_loads;
-    // nontemporal hit records: trace.nt_hits 2 = always (default), 1 = frames of >= 2 spp, 0 = never; 3 = multi-spp
-    // hits and RGBA (A/B: the kernels' nt_hits > 1 also streams the RGBA stores)
-    const uint32_t nt_hits = (cfg.nt_hits == 2 || ((cfg.nt_hits == 1 || cfg.nt_hits == 3) && spp >= 2))
-                                 ? (cfg.nt_hits == 3 ? 2u : 1u) : 0u;
+    const bool buf = n <= kBufMaxN;
+    // nontemporal hit records, every frame (r05: 10M K0 after a 4Kx4 frame 104.5 -> 82.8 us, the 1M build
+    // after a 1080p1 frame 140.3 -> 137.7 us, frames unchanged; profiles/ab_nt_hits_1spp_r05.log)
+    const uint32_t nt_hits = 1u;
 #define RT_TRACE_NT(C, P, WI, NT)                                                                                    \
     k_trace_go<C, P, WI, NT>(buf, warity, coop_cap != 0, spp == 1, nb * (256 / NT) + (fold.out ? 1u : 0u), s, nodes, \
                              wnodes, stack_cap_for(cfg, warity, NT), tris, n,                                            \
@@ -2600,13 +2406,9 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
         const uint32_t nt = small ? 64u : 256u;
         const uint32_t grid = (uint32_t)((uint64_t)nb * 4 * spp / (nt / 64)) + (fold.out ? 1u : 0u);
         const uint32_t wc = stack_cap_for(cfg, 4, nt);
-#define RT_SL(P, NT, S_)                                                                                           \
-    if (P && !cfg.sl_mtf)                                                                                          \
-        RT_KLAUNCH((k_trace_sl<P, NT, S_, false>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, \
-                   h, rank, nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits, fold);                    \
-    else                                                                                                           \
-        RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
-                   nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits, fold)
+#define RT_SL(P, NT, S_)                                                                                             \
+    RT_KLAUNCH((k_trace_sl<P, NT, S_>), dim3(grid), dim3(NT), 0, s, nodes, wnodes, wc, tris, n, cam, w, h, rank, \
+               nranks, tilesX, H, R, order, cost_out, coop_cap, cq, nt_hits, fold)
 #define RT_SL_S(P, NT)                  \
     switch (spp) {                      \
         case 2: RT_SL(P, NT, 2); break;   \
@@ -2664,19 +2466,7 @@ hipError_t launch_trace(const void* nodes, const uint4* wnodes, uint32_t warity,
             cgrid = r;
         }
         // block 0 sorts this frame's cost map into the next frame's tile order
-        bool ord = !fold.out && cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
-        if (ord && cfg.order_side && sched->side) {
-            // this frame's costs are final when k_trace is: sort them into the next order on the side
-            // stream (k_trace_coop then runs the queue only)
-            hipError_t se = hipEventRecord(sched->ev_traced, s);
-            if (se == hipSuccess) se = hipStreamWaitEvent(sched->side, sched->ev_traced, 0);
-            if (se != hipSuccess) return se;
-            RT_KLAUNCH(k_tile_order, dim3(1), dim3(1024), 0, sched->side, cost_out, nb, sched->order, sched->cost_ema);
-            if ((se = hipEventRecord(sched->ev_sorted, sched->side)) != hipSuccess) return se;
-            sched->side_pending = true;
-            sched->order_ready = true;
-            ord = false;
-        }
+        const bool ord = !fold.out && cost_out && !cfg.order_override && nb <= kOrderInCoop && cgrid > 1;
         uint32_t* ord_cost = ord ? cost_out : nullptr;
         uint32_t* ord_out = ord ? sched->order : nullptr;
         uint32_t* ord_ema = ord ? sched->cost_ema : nullptr;

@@ -161,7 +161,7 @@ class Scene:
 
     def build_times(self) -> BuildTimes:
         t = rt_build_times()
-        call("rt_bvh_build_times", self._h, C.byref(t))
+        call("rt_bvh_build_times_sized", self._h, C.byref(t), C.sizeof(t))
         return BuildTimes(t.bounds, t.morton, t.sort, t.topology, t.refit, t.wide, t.total, t.sort_kind, t.fused_k01,
                           t.fused_fallback, t.lsb_redo)
 

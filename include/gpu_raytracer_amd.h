@@ -119,6 +119,11 @@ rt_status rt_bvh_replicas(const rt_scene* s, uint32_t max, int* devices, uint32_
  * the build ran with rt_config_set("build.stage_events", 1) (0 otherwise --
  * the extra events cost GPU time, so timed builds run without them) */
 rt_status rt_bvh_build_times(const rt_scene* s, rt_build_times* out);
+/* the same, size-checked: out_size = sizeof(rt_build_times) as
+ * the caller was compiled; only that many bytes are written, so a caller
+ * built against the 0.2 header (64 B, no redo fields) is safe.  Smaller than
+ * 64 -> RT_EINVAL.  Prefer this entry point. */
+rt_status rt_bvh_build_times_sized(const rt_scene* s, rt_build_times* out, size_t out_size);
 /* Device-resident BVH exchange ("rank 0 builds and then
  * broadcasts", the alternative to every rank building its replica):
  * rt_bvh_prepare uploads the soup and allocates the BVH buffers without
@@ -320,75 +325,66 @@ rt_status rt_stage_minmax(int device, uint32_t count, const float* a, const floa
 rt_status rt_framebuffer_dump_ppm(const uint8_t* rgba, uint32_t w, uint32_t h, const char* path);
 rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
 
-/* Tuning knobs (process-wide): "trace.variant" 0 = one thread per pixel,
- * wide (4-ary) traversal over the K7w records (default), 1 = wide traversal
- * with per-lane refill from 8x8-pixel units dealt statically to a resident
- * grid, 2 = one thread per pixel, binary traversal; "trace.blocks" variant-1
- * grid (0 = resident capacity); "trace.stack_cap" (1..18; 0 = all, the
- * default: 14 for 4-ary records on 256-thread blocks, 16 on 64-thread
- * blocks -- one rank's tiles --, 18 for 8-ary) wide-traversal stack
- * entries -- rays that need more are re-traced by the binary traversal;
- * "build.wide_arity" 4 (default) / 8: K7w 4-ary or K7w8 8-ary trace records
- * (8-ary: about a quarter fewer dependent record fetches for the costliest
- * rays, more instructions per step; n <= 2^26); "trace.wg" 64/256 threads per block (8x8 quadrant / 16x16
- * tile), default 256; "trace.wg_tiles" the same for one rank's tiles of a
- * multi-GPU frame (rt_render_tiles_device), default 64; "trace.tile_order"
- * 1 = dispatch a frame's tiles longest-first from the previous frame of the
- * same shape's per-tile wave times (a 32 KB cost map per scene; the first
- * frame of a shape runs row-major), 0 = row-major always.  Path mode: "path.wavefront" 0 = megakernel ("path.wg" 64/256
- * threads per block), 1 = wavefront schedule with per-depth ray queues
- * (default); "path.sort" 0..4 = top key bytes each queue is radix-sorted by
- * for coherence (ray kind, direction octant, Morton code of the origin; 0 =
- * unsorted, the default; sorting reads each queue length back to the host);
- * "path.batch" paths per wavefront batch (0 = 4M).  "render.emulate" 0/1:
- * rt_render(ngpus > 1) puts every rank's replica on the scene's device and
- * gathers with device copies instead of RCCL (multi-rank tests on one GPU);
- * "render.rccl1" 0/1: rt_render(ngpus = 1) through the tiled + RCCL path
- * (a 1-rank communicator).  "trace.coop_cap" / "trace.coop_cap_tiles"
- * 0..2^20: a primary ray still traversing after that many wide steps is
- * queued and finished by a whole wave (k_trace_coop, DESIGN.md "Cooperative
- * heavy rays"); 0 = off; -1 = auto, the defaults: for full frames 96 steps
- * at 1 spp on 256-thread tiles (off otherwise) and, for one rank's tiles of a
- * multi-GPU frame, by rank count (88 steps for P = 2, 80 for P = 3..4, 72
- * above); samples-in-lanes frames run without it unless a cap is given;
- * "trace.coop_max" queue entries per frame shape
- * (default 65536; rays beyond it keep tracing alone); "trace.coop_skip" 1
- * (default) / 0: with an automatic cap, a frame shape whose last queue-on
- * frame queued fewer than 64 rays runs without the queue, re-probing every
- * 16th frame; "trace.coop_order" 1 (default) / 0 and "trace.order_side" 0
- * (default) / 1: where a queue-on frame sorts the next tile order
- * (k_trace_coop's block 0 / folded in k_trace from the previous frame's
- * costs; a k_tile_order on a side stream).  "trace.spp_lanes" 2 (default) /
- * 1 / 0: 2..16 spp (a power of two) traced one ray per lane, a pixel's
- * samples in adjacent lanes, for full frames and one rank's tiles / tiles
- * only / never; "trace.sl_fold" 1 (default) / 0: those frames sort the next
- * tile order in their block 0; "trace.sl_mtf" 1 (default) / 0: their
- * rank-tile kernel tests a leaf's triangle before its box; "trace.nt_hits"
- * 2 (default) / 1 / 0 / 3: hit records stored nontemporally for every frame
- * / frames of >= 2 spp / never / + the RGBA words.  "build.stage_events"
- * 0/1: per-stage build events (rt_bvh_build_times); "timing.event_fence"
- * 0/1: timing events of scenes created afterwards record with the
- * system-scope fence (default 0: no L2 writeback at each record).
+/* Tuning knobs (process-wide; 24 keys since r06, which removed the
+ * measured-slower alternatives -- DESIGN.md "Knobs").  Trace:
+ * "trace.variant" 0 = one thread per pixel, wide (4-ary) traversal over the
+ * K7w records (default), 2 = one thread per pixel, binary traversal;
+ * "trace.stack_cap" (1..18; 0 = all, the default: 14 for 4-ary records on
+ * 256-thread blocks, 16 on 64-thread blocks -- one rank's tiles --, 18 for
+ * 8-ary) wide-traversal stack entries -- rays that need more are re-traced by
+ * the binary traversal; "trace.wg" 64/256 threads per block (8x8 quadrant /
+ * 16x16 tile), default 256; "trace.wg_tiles" the same for one rank's tiles
+ * of a multi-GPU frame (rt_render_tiles_device), default 64;
+ * "trace.tile_order" 1 = dispatch a frame's tiles longest-first from the
+ * previous frame of the same shape's per-tile wave times (the first frame of
+ * a shape runs row-major), 0 = row-major always; "trace.px_sort" 1 (default)
+ * / 2 / 0: each tile's pixels dealt to lanes costliest first from the
+ * previous frame, full frames / also one rank's tiles / never;
+ * "trace.spp_lanes" 2 (default) / 1 / 0: 2..16 spp (a power of two) traced
+ * one ray per lane, a pixel's samples in adjacent lanes, for full frames and
+ * one rank's tiles / tiles only / never.  Heavy-ray queue:
+ * "trace.coop_cap" / "trace.coop_cap_tiles" 0..2^20: a primary ray still
+ * traversing after that many wide steps is queued and finished by a lane
+ * group (k_trace_coop, DESIGN.md "Cooperative heavy rays"); 0 = off; -1 =
+ * auto, the defaults: for full frames 96 steps at 1 spp on 256-thread tiles
+ * (off otherwise) and, for one rank's tiles of a multi-GPU frame, by rank
+ * count (88 steps for P = 2, 80 for P = 3..4, 72 above); samples-in-lanes
+ * frames run without it unless a cap is given; with an automatic cap a
+ * frame shape whose last queue-on frame queued fewer than 64 rays runs
+ * without the queue, re-probing every 16th frame; "trace.coop_lanes"
+ * 16/32/64 lanes per queued ray (default 32); "trace.coop_max" queue
+ * entries per frame shape (default 65536; rays beyond it keep tracing
+ * alone).  Build: "build.wide_arity" 4 (default) / 8: K7w 4-ary or K7w8
+ * 8-ary trace records (8-ary: about a quarter fewer dependent record
+ * fetches for the costliest rays, more instructions per step; n <= 2^26);
+ * "build.stage_events" 0/1: per-stage build events (rt_bvh_build_times);
  * "build.sort" (n in 2..12M): 2 = the tile-bucketed gather sort (default:
  * K1 sorts each 4096-key tile by the top 10 key bits, then one block per
  * bucket gathers its runs and sorts them in LDS), 1 = the r01-r03 MSB
  * scatter + bucket sort, 0 = the 4-pass LSB radix sort; a scene whose first
  * build finds a bucket beyond one block's LDS sort keeps the LSB sort, and
  * one whose gather probe finds clustered bins or a skewed bucket moves on
- * to the MSB sort.  "build.cross_small" 1 (default) / 0: scenes of up to
- * 1024 refit blocks take the crossing nodes' boxes from one LDS tree over
- * all block totals instead of the group tables.
- * "build.fuse_k01" 1 (default) / 0: with the gather sort, K0 (bounds) and K1
- * (Morton) as one launch whose blocks meet at a grid barrier, when every sort
- * tile's block fits the device at once (n up to ~1M) and no other such build
- * runs on the device; else two launches.  2 (test only): fused even when the
- * grid cannot be co-resident -- the barrier's bounded waits give up and the
- * build is redone with two launches (rt_build_times.fused_fallback) instead
- * of hanging.  "debug.force_lsb_redo" 0/1 (tests): take the gather-overflow
- * branch, i.e. redo the build with the LSB sort.
+ * to the MSB sort.  "build.fuse_k01" 1 (default) / 0: with the gather sort,
+ * K0 (bounds) and K1 (Morton) as one launch whose blocks meet at a grid
+ * barrier, when every sort tile's block fits the device at once (n up to
+ * ~1M) and no other such build runs on the device; else two launches.  2
+ * (test only): fused even when the grid cannot be co-resident -- the
+ * barrier's bounded waits give up and the build is redone with two launches
+ * (rt_build_times.fused_fallback) instead of hanging.  Path mode:
+ * "path.wavefront" 0 = megakernel ("path.wg" 64/256 threads per block), 1 =
+ * wavefront schedule with per-depth ray queues (default); "path.sort" 0..4
+ * = top key bytes each queue is radix-sorted by for coherence (ray kind,
+ * direction octant, Morton code of the origin; 0 = unsorted, the default;
+ * sorting reads each queue length back to the host); "path.batch" paths per
+ * wavefront batch (0 = 4M).  Multi-GPU: "render.emulate" 0/1: rt_render(ngpus
+ * > 1) puts every rank's replica on the scene's device and gathers with
+ * device copies instead of RCCL (multi-rank tests on one GPU);
+ * "render.rccl1" 0/1: rt_render(ngpus = 1) through the tiled + RCCL path (a
+ * 1-rank communicator).  Debug: "debug.force_lsb_redo" 0/1 (tests): take
+ * the gather-overflow branch, i.e. redo the build with the LSB sort;
  * "debug.poison" 0/1: every device buffer the library allocates from then on
  * is filled with 0xFF bytes before first use, so reading a byte no kernel
- * wrote gives the same (wrong) value every run instead of allocator luck.
+ * wrote gives the same (wrong) value every run instead of allocator luck;
  * "debug.lds_scribble" 0/1: before every kernel launch a scribble kernel
  * fills the CUs' LDS with a pattern that changes every launch, so a kernel
  * reading LDS it did not write differs run to run.  Both debug knobs can

@@ -251,19 +251,17 @@ def test_bvh_cache_rejects_without_device_work(rt, tmp_path):
 # rt_config_set keys: accepted values, a rejected value each, and the default
 # restored afterwards (include/gpu_raytracer_amd.h; INTEGRATION.md "tuning").
 CONFIG_KEYS = {
-    "trace.variant": ([0, 1, 2], [3, -1], 0),
+    "trace.variant": ([0, 2], [1, 3, -1], 0),
     "trace.stack_cap": ([0, 1, 14, 16, 18], [-1, 19], 0),
     "trace.wg": ([64, 256], [128], 256),
     "trace.wg_tiles": ([64, 256], [32], 64),
     "trace.tile_order": ([0, 1], [2], 1),
     "trace.px_sort": ([0, 1, 2], [3], 1),
-    "trace.blocks": ([0, 4096], [-1], 0),
+    "trace.spp_lanes": ([0, 1, 2], [3, -1], 2),
     "build.sort": ([0, 1, 2], [3, -1], 2),
     "build.fuse_k01": ([0, 1, 2], [3, -1], 1),
-    "build.wide_collapse": ([0, 1], [2, -1], 1),
     "build.wide_arity": ([4, 8], [2, 6, 16, -1], 4),
     "build.stage_events": ([0, 1], [2], 0),
-    "timing.event_fence": ([0, 1], [2], 0),
     "path.wavefront": ([0, 1], [2], 1),
     "path.wg": ([64, 256], [100], 64),
     "path.sort": ([0, 4], [5], 0),
@@ -272,12 +270,17 @@ CONFIG_KEYS = {
     "render.rccl1": ([0, 1], [2], 0),
     "trace.coop_cap": ([-1, 0, 1, 96, 1 << 20], [-2, (1 << 20) + 1], -1),
     "trace.coop_cap_tiles": ([-1, 0, 1, 96, 1 << 20], [-2, (1 << 20) + 1], -1),
-    "trace.buf_loads": ([0, 1], [2, -1], 1),
     "trace.coop_lanes": ([16, 32, 64], [0, 8, 48, 128], 32),
     "trace.coop_max": ([1, 64, 65536, 1 << 24], [0, -1, (1 << 24) + 1], 65536),
     "debug.poison": ([0, 1], [2, -1], 0),
     "debug.lds_scribble": ([0, 1], [2, -1], 0),
+    "debug.force_lsb_redo": ([0, 1], [2, -1], 0),
 }
+# r06: knobs whose non-default settings measured slower
+# and served no test-only purpose were removed (profiles/rejected_knobs_r06.patch)
+REMOVED_KEYS = ["trace.nt_hits", "trace.sl_mtf", "trace.sl_fold", "trace.coop_order", "trace.order_side",
+                "trace.coop_skip", "trace.blocks", "trace.buf_loads", "build.wide_collapse", "build.cross_small",
+                "timing.event_fence"]
 
 
 @pytest.mark.parametrize("key", sorted(CONFIG_KEYS))
@@ -300,6 +303,25 @@ def test_config_unknown_key(rt):
     with pytest.raises(rt.RtError) as e:
         rt.config_set("trace.no_such_knob", 1)
     assert e.value.status == -1
+
+
+@pytest.mark.parametrize("key", REMOVED_KEYS)
+def test_config_removed_keys(rt, key):
+    """The pruned knobs are gone: every value is RT_EINVAL."""
+    for v in (0, 1, 2):
+        with pytest.raises(rt.RtError) as e:
+            rt.config_set(key, v)
+        assert e.value.status == -1
+
+
+def test_config_key_count():
+    """The library parses exactly the knobs CONFIG_KEYS lists (at most 25,
+    VERDICT r05 item 5), so this table and rt_abi.cpp cannot drift apart."""
+    import re
+    with open(os.path.join(ROOT, "gpu_raytracer_amd", "csrc", "rt_abi.cpp")) as f:
+        keys = set(re.findall(r'k == "([a-z_]+\.[a-z_0-9]+)"', f.read()))
+    assert keys == set(CONFIG_KEYS)
+    assert len(keys) <= 25
 
 
 def test_wide8_size_cap():

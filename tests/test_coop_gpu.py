@@ -216,21 +216,17 @@ def test_orbit_frame_8_ranks_1m(R, oracle, cfg):
             assert _same_hits(hits, eh), P
 
 
-@pytest.mark.parametrize("side,coop_order", [(1, 1), (0, 0), (1, 0)])
-def test_order_paths_with_queue(R, oracle, cfg, side, coop_order):
-    """Where the next tile order of a queue-on frame is sorted: k_trace_coop's
-    block 0 (the default), a k_tile_order on the side stream after k_trace
-    (trace.order_side), or k_trace's fold block from the previous frame's
-    costs (trace.coop_order 0) -- four successive frames each, full frames
-    and one rank's tiles (P = 3), and full frames on torch's default stream
-    with no host sync between them: every frame == the oracle."""
+def test_order_with_queue(R, oracle, cfg):
+    """A queue-on frame's next tile order is sorted by k_trace_coop's block 0
+    (the side-stream and fold-block alternatives were removed in r06,
+    profiles/rejected_knobs_r06.patch) -- four successive frames each, full
+    frames and one rank's tiles (P = 3), and full frames on torch's default
+    stream with no host sync between them: every frame == the oracle."""
     import torch
     V = _soup_view()
     tris = oracle.soup(40000, 12).reshape(-1, 9)
     w, h, spp = 210, 118, 1
     eh, er = _frame(oracle, tris, V, w, h, spp)
-    cfg("trace.order_side", side, 0)
-    cfg("trace.coop_order", coop_order, 1)
     cfg("trace.coop_cap", 16, -1)
     cfg("trace.coop_cap_tiles", 24, -1)
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
@@ -254,7 +250,7 @@ def test_order_paths_with_queue(R, oracle, cfg, side, coop_order):
 
 
 def test_coop_skip_probe_frames(R, oracle, cfg):
-    """trace.coop_skip (automatic caps): a shape whose queue-on frame queued
+    """The queue skip (automatic caps): a shape whose queue-on frame queued
     fewer than 64 rays runs its next 15 frames without the queue (the order
     folded in k_trace), then probes with it again; a heavy shape keeps it.
     20 frames of a light scene (the bunny substitute's sphere) and of a soup,

@@ -638,29 +638,24 @@ def test_tile_order_moving_camera(R, oracle):
             assert np.array_equal(bits(hits["t"]), bits(eh["t"])), i
 
 
-def test_crossing_ranges_at_group_boundaries(R, oracle):
-    """The crossing stage's group tables (k_group_tables: 64 refit blocks per
-    group) on crafted sorted keys whose subtrees cover exactly one whole group
-    of middle blocks, or sit inside one, for 512- and 256-leaf refit blocks:
+@pytest.mark.parametrize("n", [140_000, 300_000])
+def test_crossing_ranges_at_group_boundaries(R, oracle, n):
+    """The crossing stage on crafted sorted keys whose subtrees cover exactly
+    one whole group (64 refit blocks) of middle blocks, or sit inside one:
+    at 140K (547 refit blocks) the small-scene LDS tree over every block
+    total, at 300K (1172 blocks) the group tables (k_group_tables).
     rt_stage_refit's every node record == boxes unioned in numpy over each
     node's leaf range (a sparse table), with the oracle's topology and escape
     links.  (A middle range of exactly 64 blocks once took a non-existent
     in-group level.)"""
-    n = 140_000
-    segs = [0, 32_356, 65_587, 98_057, 114_692, 131_072 + 77, n]  # segment j: keys j << 24 | offset
+    cuts = [32_356, 65_587, 98_057, 114_692, 131_072 + 77, 196_608 - 5, 262_144 + 3]
+    segs = [0] + [c for c in cuts if c < n] + [n]  # segment j: keys j << 24 | offset
     keys = np.zeros(n, np.uint32)
     for j in range(len(segs) - 1):
         keys[segs[j]:segs[j + 1]] = (j << 24) | np.arange(segs[j + 1] - segs[j], dtype=np.uint32)
     vals = np.arange(n, dtype=np.uint32)
     tris = soup(oracle, n, 5)
-    # 547 refit blocks: the small-scene LDS tree (build.cross_small) and the group tables it replaces
-    R.config_set("build.cross_small", 0)
-    try:
-        nodes_groups = R.stage_refit(keys, vals, tris)
-    finally:
-        R.config_set("build.cross_small", 1)
     nodes = R.stage_refit(keys, vals, tris)
-    assert np.array_equal(nodes.view(np.uint32), nodes_groups.view(np.uint32))
     left, right, rlo, rhi, parent = oracle.karras(keys)
     esc = oracle.escape(n, left, right, parent)
     t = tris.reshape(n, 3, 3)
@@ -691,28 +686,3 @@ def test_crossing_ranges_at_group_boundaries(R, oracle):
     lf = nodes[n - 1:]
     assert np.array_equal(lf["a"], vals) and np.array_equal(lf["esc"], esc[n - 1:])
     assert np.array_equal(bits(lf["lo"]), bits(blo)) and np.array_equal(bits(lf["hi"]), bits(bhi))
-
-
-@pytest.mark.parametrize("spp", [1, 2])
-def test_hit_store_modes(R, oracle, spp):
-    """trace.nt_hits 0 (plain stores), 1 (nontemporal for >= 2 spp), 2 (all
-    frames, the default), 3 (hits and RGBA): the same hits and image."""
-    from gpu_raytracer_amd.scenes import SOUP_VIEW
-    tris = soup(oracle, 30000, 44)
-    exp = oracle.build(tris)
-    w, h = 130, 74
-    ocam = oracle.camera_look_at(SOUP_VIEW.eye, SOUP_VIEW.at, SOUP_VIEW.up, SOUP_VIEW.vfov, w, h)
-    eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)
-    er = oracle.shade(eh, w, h, spp)
-    try:
-        with R.Scene.from_soup(tris) as s:
-            s.build()
-            cam = _cam(R, SOUP_VIEW, w, h)
-            for mode in (0, 1, 2, 3):
-                R.config_set("trace.nt_hits", mode)
-                hits, rgba, _ = s.render(cam, w, h, spp)
-                assert np.array_equal(rgba, er), mode
-                for f in ("t", "u", "v", "prim"):
-                    assert np.array_equal(bits(hits[f]), bits(eh[f])), (mode, f)
-    finally:
-        R.config_set("trace.nt_hits", 2)

@@ -55,7 +55,7 @@ def _same(name, hits, rgba, eh, er):
 @pytest.mark.parametrize("arity", [4, 8])
 def test_poisoned_build_and_render(R, oracle, poison, arity):
     for name, tris, view, (w, h, spp) in _scenes(oracle):
-        _check_wide(R, tris, 1, arity)  # every record restates the cut (poison stays on)
+        _check_wide(R, tris, arity)  # every record restates the cut (poison stays on)
         exp = oracle.build(tris)
         ocam = oracle.camera_look_at(view.eye, view.at, view.up, view.vfov, w, h)
         eh, _ = oracle.trace(exp["nodes"], tris, ocam, w, h, spp)

@@ -67,7 +67,7 @@ def test_random_scene_camera_settings(R, oracle, seed):
     tris = _scene(oracle, rng)
     w, h, spp = int(rng.integers(8, 160)), int(rng.integers(8, 120)), int(rng.integers(1, 4))
     cam, ocam = _camera(R, oracle, tris, rng, w, h)
-    knobs = {"build.wide_arity": int(rng.choice([4, 8])), "trace.variant": int(rng.choice([0, 0, 1, 2])),
+    knobs = {"build.wide_arity": int(rng.choice([4, 8])), "trace.variant": int(rng.choice([0, 0, 2])),
              "trace.stack_cap": int(rng.choice([0, 0, 1, 3])), "trace.coop_cap": int(rng.choice([-1, 0, 2, 24, 96])),
              "trace.coop_cap_tiles": int(rng.choice([-1, 0, 4])), "trace.coop_lanes": int(rng.choice([16, 32, 64]))}
     P = int(rng.choice([1, 1, 2, 3, 8]))

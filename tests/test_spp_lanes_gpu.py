@@ -193,7 +193,7 @@ def test_spp_lanes_equals_loop_kernel(R, cfg):
 
 def test_spp_lanes_folded_order_large_frames(R, cfg):
     """k_trace_sl full frames sort the next frame's tile order in their block
-    0 (trace.sl_fold, a loop over any tile count): 9216 tiles, five frames
+    0 (a loop over any tile count): 9216 tiles, five frames
     (the order is sorted in frame 2 on, used from frame 3), each identical to
     the loop kernel's frame -- a tile the order dropped or repeated would
     leave its pixels unwritten (device-only comparison)."""
@@ -203,9 +203,8 @@ def test_spp_lanes_folded_order_large_frames(R, cfg):
     with R.Scene.generate_soup(300_000, 3) as s:
         s.build()
         ref = None
-        for mode, fold in ((0, 1), (2, 0), (2, 1)):
+        for mode in (0, 2):
             cfg("trace.spp_lanes", mode, 2)
-            cfg("trace.sl_fold", fold, 1)
             for f in range(5):
                 img = torch.zeros(w * h, dtype=torch.int32, device="cuda")
                 hb = torch.zeros(w * h * spp * 4, dtype=torch.float32, device="cuda")
@@ -221,7 +220,7 @@ def test_spp_lanes_folded_order_large_frames(R, cfg):
                 if not np.array_equal(got[0], ref[0]):
                     d = np.nonzero(got[0] != ref[0])[0]
                     tiles = np.unique((d // w // 16) * 128 + (d % w) // 16)
-                    pytest.fail(f"mode {mode} fold {fold} frame {f}: {d.size} pixels differ in {tiles.size} tiles "
+                    pytest.fail(f"mode {mode} frame {f}: {d.size} pixels differ in {tiles.size} tiles "
                                 f"{tiles[:8].tolist()}; first {[(int(p % w), int(p // w)) for p in d[:6]]}: got "
                                 f"{[hex(int(v) & 0xFFFFFFFF) for v in got[0][d[:6]]]} expected "
                                 f"{[hex(int(v) & 0xFFFFFFFF) for v in ref[0][d[:6]]]}; hit records of the first: got "
@@ -231,7 +230,7 @@ def test_spp_lanes_folded_order_large_frames(R, cfg):
                     d = np.nonzero(got[1] != ref[1])[0]
                     rec = np.unique(d // 4)
                     px = rec // spp
-                    pytest.fail(f"mode {mode} fold {fold} frame {f}: {d.size} words in {rec.size} hit records differ "
+                    pytest.fail(f"mode {mode} frame {f}: {d.size} words in {rec.size} hit records differ "
                                 f"(fields {np.bincount(d % 4, minlength=4).tolist()}); first records "
                                 f"{[(int(r), int(p % w), int(p // w)) for r, p in zip(rec[:6], px[:6])]}: got "
                                 f"{got[1].reshape(-1, 4)[rec[:3]].tolist()} expected {ref[1].reshape(-1, 4)[rec[:3]].tolist()}; "

@@ -60,30 +60,29 @@ def _same(hits, rgba, eh, er):
 
 def test_wide8_records(R, oracle):
     rng = np.random.default_rng(5)
-    _check_wide(R, oracle.soup(3000, 2).reshape(-1, 9), 1, 8)
+    _check_wide(R, oracle.soup(3000, 2).reshape(-1, 9), 8)
     flat = oracle.soup(2000, 4).reshape(-1, 9).copy()
     flat[:, 2::3] = 0.25
-    _check_wide(R, flat, 1, 8)
-    _check_wide(R, (rng.random((1500, 9)) * 1e-30).astype(np.float32), 1, 8)
-    _check_wide(R, (rng.random((1500, 9)) * 3e37 - 1.5e37).astype(np.float32), 1, 8)
-    _check_wide(R, np.tile(oracle.soup(1, 3).reshape(-1, 9), (700, 1)), 1, 8)
+    _check_wide(R, flat, 8)
+    _check_wide(R, (rng.random((1500, 9)) * 1e-30).astype(np.float32), 8)
+    _check_wide(R, (rng.random((1500, 9)) * 3e37 - 1.5e37).astype(np.float32), 8)
+    _check_wide(R, np.tile(oracle.soup(1, 3).reshape(-1, 9), (700, 1)), 8)
     for n in (2, 3, 5, 9):  # records with fewer entries than slots
-        rec = _check_wide(R, oracle.soup(n, 9).reshape(-1, 9), 1, 8)
+        rec = _check_wide(R, oracle.soup(n, 9).reshape(-1, 9), 8)
         assert rec.shape == (n - 1, 24)
 
 
 def test_wide8_records_large(R, oracle):
     """A soup spanning many refit blocks: local records (k_topo_refit) and
     crossing ones (k_wide_cross) both restate the cut."""
-    _check_wide(R, oracle.soup(40000, 8).reshape(-1, 9), 1, 8)
+    _check_wide(R, oracle.soup(40000, 8).reshape(-1, 9), 8)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2])
+@pytest.mark.parametrize("variant", [0, 2])
 @pytest.mark.parametrize("cap", [1, 3, 7, 14, 0])
 def test_wide8_render_and_overflow(R, oracle, cfg, variant, cap):
     """cap 1-7 force the overflow hand-off (a record pushes up to 7 entries);
-    0 = the whole 18-entry stack.  Variant 1 (the pool kernel, 4-ary only)
-    falls back to the per-pixel kernel."""
+    0 = the whole 18-entry stack; variant 2 = the binary kernel."""
     V = _soup_view()
     tris = oracle.soup(30000, 11).reshape(-1, 9)
     w, h, spp = 96, 64, 2

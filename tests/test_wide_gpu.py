@@ -10,7 +10,7 @@ from conftest import bits
 pytestmark = pytest.mark.gpu
 SENT = 0xFFFFFFFF
 LEAF = 0x80000000
-VARIANTS = [0, 1, 2]  # wide per pixel (default), wide pool with refill, binary per pixel
+VARIANTS = [0, 2]  # wide per pixel (default), binary per pixel (r06: the wide pool, 1, was removed)
 
 
 @pytest.fixture(scope="module")
@@ -20,7 +20,6 @@ def R(rt):
     yield rt
     rt.config_set("trace.variant", 0)
     rt.config_set("trace.stack_cap", 0)
-    rt.config_set("trace.blocks", 0)
 
 
 def _decode_planes(rec):
@@ -65,16 +64,12 @@ def _half_area(lo, hi):
     return np.float32(np.float32(d[0] * d[1]) + np.float32(d[1] * d[2])) + np.float32(d[2] * d[0])
 
 
-def _entries(X, a, esc, lo_e, hi_e, L0, collapse, arity=4):
-    """Restatement of wide_entries: the record's entries in preorder."""
+def _entries(X, a, esc, lo_e, hi_e, L0, arity=4):
+    """Restatement of wide_entries (the greedy largest-surface cut): the
+    record's entries in preorder."""
     def kids(c):
         L = a[c]
         return [L, esc[L]]  # escape of a left child = its right sibling
-    if collapse == 0 and arity == 4:
-        out = []
-        for c in kids(X):
-            out += kids(c) if c < L0 else [c]
-        return out
     ent = kids(X)
     for _ in range(arity - 2):
         best, ba = -1, None
@@ -99,10 +94,9 @@ def _leaf_range(c, a, esc, L0, memo):
     return memo[c]
 
 
-def _check_wide(R, tris, collapse=1, arity=4):
+def _check_wide(R, tris, arity=4):
     tris = np.ascontiguousarray(tris, np.float32).reshape(-1, 9)
     n = len(tris)
-    R.config_set("build.wide_collapse", collapse)
     R.config_set("build.wide_arity", arity)
     try:
         with R.Scene.from_soup(tris) as s:
@@ -111,7 +105,6 @@ def _check_wide(R, tris, collapse=1, arity=4):
             nodes = s.read_bvh()["nodes"]
             rec = s.read_wide()
     finally:
-        R.config_set("build.wide_collapse", 1)
         R.config_set("build.wide_arity", 4)
     assert rec.shape == (n - 1, 24 if arity == 8 else 16)
     L0 = n - 1
@@ -122,14 +115,13 @@ def _check_wide(R, tris, collapse=1, arity=4):
     assert W == arity
     memo = {}
     for X in range(n - 1):
-        kids = _entries(X, a, esc, lo_e, hi_e, L0, collapse, arity)
+        kids = _entries(X, a, esc, lo_e, hi_e, L0, arity)
         # a preorder cut of X's subtree: consecutive leaf ranges covering X's
         rng = [_leaf_range(c, a, esc, L0, memo) for c in kids]
         xl, xh = _leaf_range(X, a, esc, L0, memo)
         assert rng[0][0] == xl and rng[-1][1] == xh, X
         assert all(rng[i][1] + 1 == rng[i + 1][0] for i in range(len(rng) - 1)), X
-        if collapse == 1 or arity == 8:
-            assert len(kids) == min(arity, xh - xl + 1), X
+        assert len(kids) == min(arity, xh - xl + 1), X
         assert mask[X] == (1 << len(kids)) - 1, X
         for i, c in enumerate(kids):
             want = c if c < L0 else (LEAF | (c - L0))
@@ -141,11 +133,10 @@ def _check_wide(R, tris, collapse=1, arity=4):
     return rec
 
 
-@pytest.mark.parametrize("collapse", [1, 0])
-def test_wide_records_small_and_degenerate(R, oracle, collapse):
-    """K7w records for both entry rules (build.wide_collapse 1 = greedy
-    largest-surface cut, the default; 0 = fixed two levels)."""
-    _check = lambda t: _check_wide(R, t, collapse)  # noqa: E731
+def test_wide_records_small_and_degenerate(R, oracle):
+    """K7w records (the greedy largest-surface cut) on small and degenerate
+    scenes: every record is a preorder cut with outward-rounded boxes."""
+    _check = lambda t: _check_wide(R, t)  # noqa: E731
     _check(oracle.soup(3000, 2).reshape(-1, 9))
     rng = np.random.default_rng(3)
     flat = oracle.soup(2000, 4).reshape(-1, 9).copy()
@@ -166,7 +157,7 @@ def test_wide_records_nonfinite_are_wild(R, oracle, arity):
     tris = oracle.soup(500, 6).reshape(-1, 9).copy()
     tris[17, 0] = np.inf
     tris[301, 4] = -np.inf
-    rec = _check_wide(R, tris, 1, arity)
+    rec = _check_wide(R, tris, arity)
     assert _layout(rec)[1].any()
 
 
@@ -206,22 +197,19 @@ def test_variants_and_stack_overflow(R, oracle, variant, cap):
     _same(hits, rgba, eh, er)
 
 
-@pytest.mark.parametrize("collapse", [0, 1])
 @pytest.mark.parametrize("cap", [2, 14])
-def test_collapse_rules_render_identically(R, oracle, collapse, cap):
-    """Both K7w cut rules (build.wide_collapse) give the oracle's hits and
-    image, with and without forced stack overflows."""
+def test_greedy_cut_renders_identically(R, oracle, cap):
+    """The greedy K7w cut gives the oracle's hits and image, with and without
+    forced stack overflows."""
     from gpu_raytracer_amd.scenes import SOUP_VIEW as V
     tris = oracle.soup(40000, 13).reshape(-1, 9)
     w, h, spp = 120, 72, 1
     cam = R.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     ocam = oracle.camera_look_at(V.eye, V.at, V.up, V.vfov, w, h)
     eh, er = _oracle_render(oracle, tris, ocam, w, h, spp)
-    R.config_set("build.wide_collapse", collapse)
     try:
         hits, rgba = _render_all(R, tris, cam, w, h, spp, 0, cap)
     finally:
-        R.config_set("build.wide_collapse", 1)
         R.config_set("trace.stack_cap", 0)
     _same(hits, rgba, eh, er)
 

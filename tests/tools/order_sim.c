@@ -3,7 +3,7 @@
  * traversal over the same binary BVH, and how often the nearest-first answer
  * (the smallest (t, leaf index) among "self-consistent" candidates, those
  * whose Moller-Trumbore t is not below their own leaf box's slab entry tn)
- * differs from §9.7's.  Built and driven by tools/order_sim.py. */
+ * differs from §9.7's.  Built and driven by tests/tools/order_sim.py. */
 #include <math.h>
 #include <stdint.h>
 #include <string.h>

@@ -31,7 +31,7 @@ for it in range(iters):
         tris = O.soup(n, int(rng.integers(1, 1000))).reshape(-1, 9)
         view = V
     ar = int(rng.choice([4, 8]))
-    var = int(rng.choice([0, 0, 0, 1, 2]))
+    var = int(rng.choice([0, 0, 0, 2]))
     cap = int(rng.choice([0, 0, 1, 3, 14]))
     w, h = int(rng.integers(8, 200)), int(rng.integers(8, 120))
     spp = int(rng.choice([1, 1, 2, 3, 4, 8, 16]))
@@ -40,9 +40,7 @@ for it in range(iters):
              "build.sort": int(rng.choice([2, 2, 1, 0])),
              "trace.coop_cap": int(rng.choice([-1, -1, 0, 2, 24])),
              "trace.coop_cap_tiles": int(rng.choice([-1, -1, 0, 4])),
-             "trace.coop_skip": int(rng.choice([1, 0])), "trace.order_side": int(rng.choice([0, 1])),
-             "trace.coop_order": int(rng.choice([1, 0])), "trace.sl_fold": int(rng.choice([1, 0])),
-             "trace.spp_lanes": int(rng.choice([2, 1, 0])), "trace.nt_hits": int(rng.choice([2, 1, 0, 3])),
+             "trace.spp_lanes": int(rng.choice([2, 1, 0])), "trace.px_sort": int(rng.choice([1, 1, 2, 0])),
              "trace.wg": int(rng.choice([256, 64])), "render.emulate": 1 if P > 1 else 0}
     for k, v in knobs.items():
         R.config_set(k, v)
@@ -65,8 +63,7 @@ for it in range(iters):
     if it % 20 == 0:
         print(f"it {it} ({time.time() - t0:.0f} s)", flush=True)
 for k, v in (("build.wide_arity", 4), ("trace.variant", 0), ("trace.stack_cap", 0), ("build.sort", 2),
-             ("trace.coop_cap", -1), ("trace.coop_cap_tiles", -1), ("trace.coop_skip", 1), ("trace.order_side", 0),
-             ("trace.coop_order", 1), ("trace.sl_fold", 1), ("trace.spp_lanes", 2), ("trace.nt_hits", 2),
+             ("trace.coop_cap", -1), ("trace.coop_cap_tiles", -1), ("trace.spp_lanes", 2), ("trace.px_sort", 1),
              ("trace.wg", 256), ("render.emulate", 0)):
     R.config_set(k, v)
 print(f"done: {iters} scenes x 3 frames, {bad} mismatching renders", flush=True)

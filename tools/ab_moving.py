@@ -47,8 +47,7 @@ for _ in range(rounds):
         res[name].append(float(np.mean(t)))
         for k in kv:  # back to the library defaults
             R.config_set(k, {"trace.coop_cap": -1, "trace.tile_order": 1, "trace.px_sort": 1, "trace.wg": 256,
-                             "trace.buf_loads": 1, "trace.coop_lanes": 32, "trace.coop_cap_tiles": -1,
-                             "trace.spp_lanes": 2, "trace.sl_fold": 1, "trace.sl_mtf": 1, "trace.nt_hits": 2, "trace.coop_order": 1, "trace.order_side": 0, "trace.coop_skip": 1}.get(k, 0))
+                             "trace.coop_lanes": 32, "trace.coop_cap_tiles": -1, "trace.spp_lanes": 2}.get(k, 0))
 for name, _ in configs:
     print(f"{name:<22s} mean trace {np.median(res[name]):.4f} ms  (rounds: {' '.join(f'{x:.4f}' for x in res[name])})",
           flush=True)

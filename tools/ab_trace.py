@@ -21,7 +21,7 @@ sel = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "2"]
 variants = []
 for v in sel:
     order = 1
-    if "o" in v and not v.startswith("pool"):  # e.g. 0o0: row-major tile order (default 1: cost-map order)
+    if "o" in v:  # e.g. 0o0: row-major tile order (default 1: cost-map order)
         v, order = v.split("o")[0], int(v.split("o")[1])
     base = {"trace.tile_order": order}
     tag = "longest-first" if order else "row-major"
@@ -33,9 +33,6 @@ for v in sel:
         variants.append((f"binary, 64-thread blocks ({tag})", {**base, "trace.variant": 2, "trace.wg": 64}))
     elif v == "2":
         variants.append((f"binary ({tag})", {**base, "trace.variant": 2, "trace.wg": 256}))
-    elif v.startswith("pool"):  # pool[-bB]: wide with per-lane refill, B blocks (0 = resident capacity)
-        b = int(v.split("-b")[1]) if "-b" in v else 0
-        variants.append((v, {**base, "trace.variant": 1, "trace.blocks": b}))
 cnts = {}
 for name, cfg in variants:
     for k, v in cfg.items():

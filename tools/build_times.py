@@ -26,7 +26,6 @@ for kv in cfgs:
 import numpy as np  # noqa: E402
 import gpu_raytracer_amd as R  # noqa: E402
 
-R.config_set("timing.event_fence", int(os.environ.get("RT_EVENT_FENCE", "0")))
 for k, v in knobs:
     R.config_set(k, v)
 if os.environ.get("BT_SCENE"):
@@ -68,7 +67,7 @@ for i in range(reps + 3):
     if i >= 3:
         tot.append(ms)
 m = np.median(np.array(rows), 0) * 1e3
-lib = os.path.basename(os.environ.get("RT_LIB", "librtamd.so")) + (" fence" if os.environ.get("RT_EVENT_FENCE") == "1" else "")
+lib = os.path.basename(os.environ.get("RT_LIB", "librtamd.so"))
 lib += " " + ",".join(f"{k}={v}" for k, v in knobs) if knobs else ""
 lib += (" after-trace" + ("" if os.environ["BT_TRACE"] == "1" else " " + os.environ["BT_TRACE"])
         if os.environ.get("BT_TRACE", "0") != "0" else "")
