@@ -186,7 +186,22 @@ struct WRay {
     float tb, hu, hv, ctn;
     uint32_t hp, cur, pend, sp, steps;
     bool fin;  // 1/d finite on every axis: the wide traversal applies
+#ifdef RT_STEPSTAMPS
+    unsigned long long t1, t2;  // diagnostic: s_memtime after the pop and once the step's loads are back
+#endif
 };
+
+#ifdef RT_STEPSTAMPS
+// Diagnostic build only (tools/diag_steps.py): the shader clock at a point
+// of the wide step, with every LDS read before it complete (MI355X guide
+// "In-kernel stamps": one asm statement, the wait inside it).
+#define RT_TSTAMP(v)                                                                        \
+    do {                                                                                    \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : : "memory");        \
+        __builtin_amdgcn_sched_barrier(0);                                                  \
+    } while (0)
+#endif
 
 // The scene box (the binary root's, internal node 0, for n >= 2): every
 // record's origin and grid lie inside it, which bounds the record test's
@@ -414,6 +429,9 @@ template <bool COUNT, int NT, bool ANY = false, bool MTF = false, bool BUF = fal
 __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnodes, const float4* __restrict__ tri_s,
                                          const float* o, uint32_t cap, uint32_t limit, uint32_t* sref, uint16_t* stn,
                                          uint32_t& cn, uint32_t& ct, bool any = ANY, const WideMem* M = nullptr) {
+#ifdef RT_STEPSTAMPS
+    R.t1 = R.t2 = 0ull;
+#endif
     if (++R.steps > limit) return 2;
     if (R.pend == RT_SENT) {
         if (R.cur == RT_SENT) wide_pop<NT>(R, sref, stn);
@@ -434,11 +452,19 @@ __device__ __forceinline__ int wide_step(WRay& R, const uint4* __restrict__ wnod
     const uint32_t to = BUF ? (leaf ? (R.pend & ~kWideLeaf) * 48u : M->tbytes) : 0u;
     uint4 wr[NW];
     float4 T0, T1, T2;
+#ifdef RT_STEPSTAMPS
+    RT_TSTAMP(R.t1);
+#endif
     if (BUF) {
         const uint32_t wo = node ? R.cur * WideFmt<W>::bytes : M->wbytes;
         T0 = bload_f4(M->tr, to); T1 = bload_f4(M->tr, to + 16); T2 = bload_tri2(M->tr, to + 32);
 #pragma unroll
         for (uint32_t k = 0; k < NW; ++k) wr[k] = bload_rec<W>(M->wr, wo + 16 * k, k);
+#ifdef RT_STEPSTAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt vmcnt(0)" : : : "memory");
+        RT_TSTAMP(R.t2);
+#endif
     } else {
         if (leaf) { T0 = tp[0]; T1 = tp[1]; T2 = tp[2]; }
         if (node) {
@@ -1020,6 +1046,11 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
 #ifdef RT_STAMPS
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef RT_STEPSTAMPS
+    unsigned long long ss_pop = 0, ss_wait = 0, ss_exec = 0, mt0;
+    uint32_t ss_n = 0;
+    RT_TSTAMP(mt0);
+#endif
     if (valid) {
         float r = 0.0f, g = 0.0f, b = 0.0f;
         for (uint32_t s = 0; s < spp; ++s) {
@@ -1043,9 +1074,22 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
                 const char* nd = reinterpret_cast<const char*>(nodes);
                 const WideMem M = wide_mem<WA>(wnodes, tri_s, n);
                 while (st == 0) {
+#ifdef RT_STEPSTAMPS
+                    unsigned long long t0, t3;
+                    RT_TSTAMP(t0);
+#endif
                     st = wide_step<COUNT, NT, false, PACKED || SHADOW, BUF, WA>(
                         R, wnodes, tri_s, cam.eye, wcap, 4 * n + 16, s_ref + threadIdx.x, s_tn + threadIdx.x, cn, ct,
                         false, &M);
+#ifdef RT_STEPSTAMPS
+                    RT_TSTAMP(t3);
+                    if (R.t2) {  // a step that fetched: pop + address, the loads, the rest
+                        ss_pop += R.t1 - t0;
+                        ss_wait += R.t2 - R.t1;
+                        ss_exec += t3 - R.t2;
+                        ++ss_n;
+                    }
+#endif
                     if (coop_on && st == 0 && R.steps == coop_cap) st = coop_defer(cq, gw, qslot);
                 }
                 if (PX) steps += R.steps;
@@ -1097,7 +1141,33 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
             rgba[pi] = px;
         }
     }
-#ifdef RT_STAMPS
+#ifdef RT_STEPSTAMPS
+    // per-wave {start, end (100 MHz), HW_ID | XCC_ID << 32, steps of the lane with the most fetching steps,
+    // its pop / wait / rest shader cycles, the wave's shader cycles} (tools/diag_steps.py)
+    {
+        uint32_t best = ss_n;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) best = max(best, (uint32_t)__shfl_xor(best, o, 64));
+        const uint64_t mine = __ballot(ss_n == best);
+        const int src = __builtin_ctzll(mine);
+        const unsigned long long p = __shfl(ss_pop, src, 64), wq = __shfl(ss_wait, src, 64),
+                                 ex = __shfl(ss_exec, src, 64);
+        unsigned long long mt1;
+        RT_TSTAMP(mt1);
+        if (l == 0) {
+            const uint64_t wslot = (uint64_t)gw * 8;
+            g_rt_stamps[wslot + 0] = st0;
+            g_rt_stamps[wslot + 1] = __builtin_amdgcn_s_memrealtime();
+            g_rt_stamps[wslot + 2] = (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                                     ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32);
+            g_rt_stamps[wslot + 3] = best;
+            g_rt_stamps[wslot + 4] = p;
+            g_rt_stamps[wslot + 5] = wq;
+            g_rt_stamps[wslot + 6] = ex;
+            g_rt_stamps[wslot + 7] = mt1 - mt0;
+        }
+    }
+#elif defined(RT_STAMPS)
     // per-wave {start, end, HW_ID | XCC_ID << 32, max lane nodes | wave nodes << 32}
     // (tools/diag_trace.py; node counts only in the COUNT variant)
     {
