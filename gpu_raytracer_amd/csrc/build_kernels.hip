@@ -1180,7 +1180,13 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         const KeyWin keys = stage_keys<T, KW>(keys_g, n, reinterpret_cast<uint32_t*>(s_tab), gb);
         RT_STAMP(1);
         LeafTri lt;
+#ifdef RT_EXP_GATHER_SEQ
+        // traffic attribution only (tools/topo_traffic.sh, wrong output): leaf k's
+        // triangle read coalesced from tris[k] instead of gathered from tris[prim]
+        if (valid) { lt = gather_leaf(k, tris); lt.prim = prim; }
+#else
         if (valid) lt = gather_leaf(prim, tris);
+#endif
         bool deferred = false;
         // topology words stay in registers/LDS: only the crossing nodes' go to
         // global memory (step 2), for k_refit_cross / k_wide_cross

@@ -36,11 +36,16 @@ def report(name, st, phases, nslots):
 
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
-s = R.Scene.generate_soup(n, 1)
+if os.environ.get("BT_SCENE"):  # a substitute scene (bunny / sponza) instead of the soup
+    from gpu_raytracer_amd import scenes as S
+    s = R.Scene.from_soup(S.tris_for(os.environ["BT_SCENE"]))
+    n = s.num_tris
+else:
+    s = R.Scene.generate_soup(n, 1)
 for _ in range(3):
     s.build()
-M = (n + 511) // 512
-if n <= 1_048_576:  # the fused K0 + K1 (its records from block 65536 on)
+M = (n + 255) // 256  # 256-leaf refit blocks (r05)
+if n <= 1_048_576 and s.build_times().fused_k01:  # the fused K0 + K1 (its records from block 65536 on)
     T = (n + 4095) // 4096
     allst = stamps(65536 + T)
     report("k_morton_tb<fused>", allst[65536:65536 + T, :8],
@@ -48,6 +53,8 @@ if n <= 1_048_576:  # the fused K0 + K1 (its records from block 65536 on)
             "scan+table", "cursor scatter (LDS)", "word stores"], 8)
 report("k_topo_refit", stamps(M)[:, :6], ["key window+sync", "topology+leaf (thread 0)", "scans+flags+sync",
                                           "sparse-table sweep+sync", "node+K7w stores"], 6)
+if os.environ.get("BT_SCENE") or os.environ.get("NO_SORT"):
+    sys.exit(0)
 keys = np.random.default_rng(0).integers(0, 2**30, n, dtype=np.uint64).astype(np.uint32)
 for _ in range(2):
     R.stage_sort(keys, np.arange(n, dtype=np.uint32))
