@@ -24,6 +24,23 @@ hipError_t read_stamps_trace(void* out, size_t bytes) { return hipMemcpyFromSymb
 
 struct Cam { float eye[3], w00[3], du[3], dv[3]; };
 
+// The image tile of one rank's slot: round-robin, tile t = rank + slot * P
+// (the costly and cheap image bands spread over every rank).  The
+// RT_EXP_TILE_BANDS diagnostic build (tools/build_exp.sh; wrong gathers,
+// timing only) gives each rank a contiguous band of as many tiles instead,
+// to price the round-robin deal's loss of locality (DESIGN.md, r06:
+// profiles/bands_r06.log -- no per-ray gain, and the bands unbalance the ranks).
+__device__ __forceinline__ uint32_t rank_tile(uint32_t rank, uint32_t slot, uint32_t nranks, uint32_t tilesX, uint32_t H) {
+#ifdef RT_EXP_TILE_BANDS
+    const uint32_t ntl = tilesX * ((H + 15) / 16);
+    return rank * (ntl / nranks) + min(rank, ntl % nranks) + slot;
+#else
+    (void)tilesX;
+    (void)H;
+    return rank + slot * nranks;
+#endif
+}
+
 
 __device__ __forceinline__ float dot3(const float* a, const float* b) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
 __device__ __forceinline__ void cross3(const float* a, const float* b, float* o) {
@@ -1018,7 +1035,7 @@ void k_trace(const void* __restrict__ nodes, const uint4* __restrict__ wnodes,
     constexpr uint32_t WPB = NT / 64;
     const uint32_t gw = blockIdx.x * WPB + (threadIdx.x >> 6);  // global wave id
     const uint32_t slot = order ? order[gw >> 2] : gw >> 2;  // dispatch order -> tile slot
-    const uint32_t t = rank + slot * nranks;
+    const uint32_t t = rank_tile(rank, slot, nranks, tilesX, H);
     const uint32_t tx = t % tilesX, ty = t / tilesX;
     const uint32_t l = threadIdx.x & 63, w = gw & 3;
     // pixel of this lane: the 8x8 quadrant w of the tile, or (trace.px_sort,
@@ -1273,7 +1290,7 @@ __global__ __launch_bounds__(NT, RT_KTILES_WAVES) void k_trace_sl(const void* __
     const uint32_t gw = bid * (NT / 64) + (threadIdx.x >> 6);  // global unit (wave) id
     const uint32_t ti = gw / SH::UPT, q = gw % SH::UPT;
     const uint32_t slot = order ? order[ti] : ti;
-    const uint32_t t = rank + slot * nranks;
+    const uint32_t t = rank_tile(rank, slot, nranks, tilesX, H);
     const uint32_t tx = t % tilesX, ty = t / tilesX;
     const uint32_t l = threadIdx.x & 63, p = l / S, smp = l % S;
     const uint32_t lx = (q % SH::TPR) * SH::TW + p % SH::TW, ly = (q / SH::TPR) * SH::TH + p / SH::TW;
