@@ -839,6 +839,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
     const uint32_t b = blockIdx.x;
     const uint32_t d = (b & 7u) * (kMsbBuckets / 8) + (b >> 3);  // XCD x: buckets [128x, 128x + 128)
+    RT_STAMP(0);  // diagnostic builds only (tools/diag_gather.py)
     for (uint32_t j = tid; j <= NB; j += NT) s_bin[j] = 0u;
     // 1. this bucket's run in every tile: thread tid owns tiles [tid*K, tid*K + K).
     // The bucket's size m is the sum of its runs, and its start the sum of
@@ -874,6 +875,8 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
         bstart[d] = s;
         if (d == kMsbBuckets - 1) bstart[kMsbBuckets] = s + m;
     }
+    RT_STAMP_VAL(7, m);
+    RT_STAMP(1);
     if (m == 0) return;  // block-uniform
     if (m > CAP) {       // block-uniform: beyond one LDS sort
         if (tid == 0) atomicOr(flags + 1, 1u);
@@ -930,6 +933,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
         }
     }
     __syncthreads();
+    RT_STAMP(2);
     // 3. gather: element j = tid + i*NT (consecutive lanes read consecutive
     // words of a run) and decode (key, index)
     uint32_t key[P], val[P], bin[P];
@@ -948,6 +952,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     for (int i = 0; i < P; ++i)
         if (tid + (uint32_t)i * NT < m) atomicAdd(&s_bin[bin[i]], 1u);
     __syncthreads();
+    RT_STAMP(3);
     // 4. bin starts (s_bin[NB] = m) and cursors, then the bin grouping (the
     // marks are dead: s_kv takes their words)
     {
@@ -963,6 +968,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     for (int i = 0; i < P; ++i)
         if (tid + (uint32_t)i * NT < m) s_kv[atomicAdd(&s_cur[bin[i]], 1u)] = make_uint2(key[i], val[i]);
     __syncthreads();
+    RT_STAMP(4);
     // 5. rank in the bin by the (key, index) pair; item-interleaved, so the
     // thread's P bin reads of one step are in flight together
     uint32_t pos[P], len[P], kmax = 0;
@@ -990,6 +996,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
 #pragma unroll
     for (int i = 0; i < P; ++i) pos[i] += r[i];
     __syncthreads();  // every bin read
+    RT_STAMP(5);
 #pragma unroll
     for (int i = 0; i < P; ++i)
         if (tid + (uint32_t)i * NT < m) s_kv[pos[i]] = make_uint2(key[i], val[i]);
@@ -1000,6 +1007,7 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
         kout[s + j] = o.x;
         vout[s + j] = o.y;
     }
+    RT_STAMP(6);
 }
 
 // A probe build's verdict for the gather sort: 1 when some bucket holds more
