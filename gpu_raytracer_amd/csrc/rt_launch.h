@@ -44,13 +44,12 @@ struct BuildBufs {
     // global memory, ~10x the build); a scene's triangles never change
     uint32_t sort_mode = 0;
     uint32_t sort_mode_of = 0;  // the sort (build.sort 1 or 2) whose probe build set sort_mode
-    // the gather sort's probe found clustered bins (a bin of more than
-    // kGatherBinFast keys, ranked in O(bin^2)) or a skewed bucket (over 4x
-    // the mean: one block sorts it while the others idle), but no bucket
-    // beyond its LDS: later builds use the MSB bucket sort instead, with its
-    // own verdict (its LDS radix passes have no per-bin cost, and it spreads
-    // a big bucket; r05: the bunny substitute's 70K-tri build 105 -> 82 us,
-    // profiles/sort_verdict_r05.log)
+    // the gather sort's probe found a run of more than kGatherBinFast
+    // identical keys (duplicated geometry; r06: clustered bins alone take the
+    // gather's radix path and stay) or, with -DRT_GATHER_SKEW=k, a bucket over
+    // k x the mean, but no bucket beyond its LDS: later builds use the MSB
+    // bucket sort instead, with its own verdict (r05: the bunny substitute's
+    // 70K-tri build 105 -> 82 us, profiles/sort_verdict_r05.log)
     uint32_t gather_off = 0;
 };
 // keys one MSB bucket may hold for the LDS bucket sort at this n

@@ -751,9 +751,11 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
 //      order the atomics left -- so neither level needs a stable ranking;
 //   5. the bin-sorted bucket is written back coalesced.
 // A uniform soup's bins hold n / 2^20 keys on average, so step 4 is a short
-// loop; a bin beyond kGatherBinFast keys (clustered geometry) is still
-// exact, at O(bin^2 / 64) LDS broadcasts, and flags the scene (*slow) so its
-// later builds use the LSB sort.  A bucket beyond the block's LDS (a probe
+// loop.  A block with a bin beyond kGatherHot keys (clustered geometry: the
+// bunny and Sponza substitutes' 75- and 32-key bins) sorts its bucket by two
+// stable 10-bit radix passes instead (gather_radix_sort, r06); only a run of
+// more than kGatherBinFast identical keys (degenerate, duplicated geometry)
+// flags the scene (*slow) so its later builds use the MSB sort.  A bucket beyond the block's LDS (a probe
 // build's verdict normally prevents this) flags *overflow and is left
 // unsorted: the host then rebuilds with the LSB sort.
 // Blocks are dealt to buckets XCD by XCD (dispatch order is round-robin over
@@ -762,12 +764,19 @@ __global__ __launch_bounds__(kBigThreads) void k_bucket_sort_big(uint32_t* __res
 // every table row, which its own L2 then serves to its 128 blocks.
 constexpr uint32_t kGatherMaxTilesPerThread = 4;  // runs (tiles) per thread in step 1
 #ifndef RT_GATHER_SKEW
-#define RT_GATHER_SKEW 4  // k_bucket_dense's skew verdict: largest bucket > this x the mean (0: off)
+#define RT_GATHER_SKEW 0  // k_bucket_dense's skew verdict: largest bucket > this x the mean (0: off)
 #endif
 #ifndef RT_GATHER_BIN_FAST
 #define RT_GATHER_BIN_FAST 64
 #endif
-constexpr uint32_t kGatherBinFast = RT_GATHER_BIN_FAST;  // bins above this many keys flag the scene as clustered
+constexpr uint32_t kGatherBinFast = RT_GATHER_BIN_FAST;  // identical-key runs above this flag the scene as clustered
+#ifndef RT_GATHER_HOT
+#define RT_GATHER_HOT 16
+#endif
+constexpr uint32_t kGatherHot = RT_GATHER_HOT;  // a bin above this many keys: the block takes the radix path (r06)
+// the radix path's shapes: P = 8 items per thread in bucket_rank's wave-major
+// order, NT <= 512 (its W x 1024 counters fit next to the bucket)
+constexpr bool gather_radix(int nt, int p) { return p == 8 && nt <= 512; }
 
 // tiles (runs per bucket) the block's LDS holds: NT * 4, less for the
 // 12- and 16-key-per-thread shapes, whose buckets take 96 / 128 KB (n <= 12.05M)
@@ -778,9 +787,16 @@ constexpr int gather_bin_bits(int nt, int p) { return nt * p >= 12288 && p < 16 
 // LDS words of k_bucket_gather<NT, P>: the bucket as (key, index) pairs
 // (2 x NT*P; first the run marks), the bin starts and cursors (2 x (2^BB +
 // 1)), the run offsets and entries (2 x tiles + 1), two [16] reduction rows
+// (radix path: the bucket as keys and values, then W x 1024 counters, 1024
+// digit starts and a [16] row in the same buffer)
+constexpr size_t gather_lds_words(int nt, int p) {
+    return (size_t)2 * nt * p + 2 * ((1u << gather_bin_bits(nt, p)) + 1) + 2 * (size_t)gather_max_tiles(nt, p) + 1 + 32;
+}
+constexpr size_t gather_radix_words(int nt, int p) {
+    return gather_radix(nt, p) ? (size_t)2 * nt * p + (size_t)(nt / 64 + 1) * kMsbBuckets + 16 : 0;
+}
 constexpr size_t gather_lds_bytes(int nt, int p) {
-    return ((size_t)2 * nt * p + 2 * ((1u << gather_bin_bits(nt, p)) + 1) + 2 * (size_t)gather_max_tiles(nt, p) + 1 +
-            32) * 4;
+    return (gather_lds_words(nt, p) > gather_radix_words(nt, p) ? gather_lds_words(nt, p) : gather_radix_words(nt, p)) * 4;
 }
 
 // In-place exclusive scan of a[N] in LDS by NT threads (N a multiple of NT;
@@ -811,6 +827,88 @@ __device__ __forceinline__ void scan_lds(uint32_t* a, uint32_t* s_sw /* [NT / 64
         pre += v[j];
     }
     __syncthreads();
+}
+
+// k_bucket_gather's path for a bucket with a hot bin (r06): the m (key,
+// index) pairs in registers (element j = tid + i*NT) sorted by two stable
+// 10-bit passes (key bits 0..9, then 10..19; bucket_rank's wave-major order),
+// then each identical-key run ordered by index -- the gather left the pairs
+// in atomic order, so equal keys are the only unsorted part.  O(m) plus
+// O(run^2) per run; a run beyond kGatherBinFast keys (degenerate geometry)
+// flags the scene (*slow) so its later builds leave the gather sort.
+template <int NT, int P>
+__device__ __forceinline__ void gather_radix_sort(const uint32_t (&key)[P], const uint32_t (&val)[P],
+                                                            uint32_t m, uint32_t s, uint32_t* __restrict__ kout,
+                                                            uint32_t* __restrict__ vout, uint32_t* __restrict__ flags,
+                                                            uint32_t* s_dyn) {
+    constexpr int NW = NT / 64;
+    constexpr uint32_t CAP = (uint32_t)NT * P;
+    uint32_t* s_rk = s_dyn;       // [CAP] keys
+    uint32_t* s_rv = s_dyn + CAP;  // [CAP] indices
+    uint32_t(*s_wc)[kMsbBuckets] = reinterpret_cast<uint32_t(*)[kMsbBuckets]>(s_dyn + 2 * CAP);
+    uint32_t* s_cnt = s_dyn + 2 * CAP + NW * kMsbBuckets;
+    uint32_t* s_sw = s_cnt + kMsbBuckets;
+    const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+    const uint32_t per = (m + NT - 1) / NT;
+    uint32_t k[P], v[P], dg[P], r[P];
+    bool ok[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {  // pass 1's order is free: the pairs as gathered
+        ok[i] = tid + (uint32_t)i * NT < m;
+        k[i] = key[i];
+        v[i] = val[i];
+    }
+    for (uint32_t shift = 0; shift < kMsbShift; shift += 10) {
+        bucket_rank<NT, P>(k, ok, shift, s_wc, s_cnt, dg, r);  // (its first barrier orders the reads below)
+        scan1024<NT>(s_cnt, s_sw);
+#pragma unroll
+        for (int i = 0; i < P; ++i)
+            if (ok[i]) {
+                const uint32_t p = s_cnt[dg[i]] + r[i];
+                s_rk[p] = k[i];
+                s_rv[p] = v[i];
+            }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < P; ++i) {  // the next pass reads in ranking order
+            const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
+            ok[i] = (uint32_t)i < per && q < m;
+            if (ok[i]) {
+                k[i] = s_rk[q];
+                v[i] = s_rv[q];
+            }
+        }
+        RT_STAMP(4 + shift / 10);  // diagnostic builds only
+    }
+    // sorted by key; each element's place in its identical-key run by index.
+    // Both neighbours first (all 2P reads in flight): a lone key stays put
+    bool tie[P];
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
+        const uint32_t pv = ok[i] && q > 0 ? s_rk[q - 1] : ~k[i];
+        const uint32_t nx = ok[i] && q + 1 < m ? s_rk[q + 1] : ~k[i];
+        tie[i] = ok[i] && (pv == k[i] || nx == k[i]);
+    }
+    bool longrun = false;
+#pragma unroll
+    for (int i = 0; i < P; ++i) {
+        const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
+        if (!ok[i]) continue;
+        uint32_t c = q;
+        if (tie[i]) {
+            uint32_t a = q, e = q + 1;
+            while (a > 0 && s_rk[a - 1] == k[i]) --a;
+            while (e < m && s_rk[e] == k[i]) ++e;
+            c = a;
+            for (uint32_t x = a; x < e; ++x) c += s_rv[x] < v[i] ? 1u : 0u;
+            longrun |= e - a > kGatherBinFast;
+        }
+        kout[s + q] = k[i];
+        vout[s + c] = v[i];
+    }
+    if (__syncthreads_or(longrun) && tid == 0) atomicOr(flags, 1u);
+    RT_STAMP(6);
 }
 
 template <int NT, int P>
@@ -954,11 +1052,20 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
     __syncthreads();
     RT_STAMP(3);
     // 4. bin starts (s_bin[NB] = m) and cursors, then the bin grouping (the
-    // marks are dead: s_kv takes their words)
+    // marks are dead: s_kv takes their words).  A bin beyond kGatherHot keys
+    // (clustered geometry) would make step 5 a long loop: the block sorts by
+    // radix instead (block-uniform)
     {
         uint32_t mx = 0;
         for (uint32_t j = tid; j < NB; j += NT) mx = max(mx, s_bin[j]);
-        if (__syncthreads_or(mx > kGatherBinFast) && tid == 0) atomicOr(flags, 1u);
+        if (__syncthreads_or(mx > kGatherHot)) {
+            if constexpr (gather_radix(NT, P)) {
+                gather_radix_sort<NT, P>(key, val, m, s, kout, vout, flags, s_dyn);
+                return;
+            } else if (tid == 0 && mx > kGatherBinFast) {
+                atomicOr(flags, 1u);
+            }
+        }
     }
     scan_lds<NT, (int)NB>(s_bin, s_sw);  // ends with a barrier
     for (uint32_t j = tid; j < NB; j += NT) s_cur[j] = s_bin[j];

@@ -368,17 +368,30 @@ def test_clustered_scene_switches_sort(R, oracle, n, sort):
     assert max(ms) < 1.0 * n / 1e6, ms
 
 
-@pytest.mark.parametrize("scene", ["bunny", "sponza"])
-def test_clustered_bins_move_to_msb(R, oracle, scene):
-    """The bunny substitute (70K triangles; the poles of its lat-long sphere
-    crowd thousands of them into a few fine cells): its gather-sort probe
-    finds clustered bins (more than 64 keys in a bin, ranked in O(bin^2));
-    the Sponza substitute (262K): a skewed bucket (2048 keys against a mean
-    of 256).  Neither has a bucket beyond the block's LDS, so each scene moves
-    on to the MSB bucket sort (BuildBufs::gather_off), whose own probe keeps
-    it -- every build equals the oracle."""
+def _clustered_tris(oracle, scene):
     from gpu_raytracer_amd import scenes as S
-    t = np.ascontiguousarray(S.tris_for(scene), np.float32).reshape(-1, 9)
+    rng = np.random.default_rng(7)
+    if scene == "hot":  # a soup plus 1500 small triangles in a cube of side 0.01: a 398-key bin
+        c = rng.random((1500, 1, 3)).astype(np.float32) * 0.01 + 0.3
+        h = (c + rng.standard_normal((1500, 3, 3)).astype(np.float32) * 1e-4).reshape(-1, 9)
+        return np.ascontiguousarray(np.concatenate([soup(oracle, 60000, 3), h]), np.float32)
+    if scene == "dup":  # 300 copies of each of 200 triangles: runs of 300 identical keys
+        d = np.repeat(soup(oracle, 200, 5), 300, axis=0)
+        return np.ascontiguousarray(np.concatenate([soup(oracle, 30000, 4), d]), np.float32)
+    return np.ascontiguousarray(S.tris_for(scene), np.float32).reshape(-1, 9)
+
+
+@pytest.mark.parametrize("scene,kind", [("bunny", 2), ("sponza", 2), ("hot", 2), ("dup", 1)])
+def test_clustered_scenes_sort(R, oracle, scene, kind):
+    """Clustered bins stay on the gather sort (r06): the bunny substitute
+    (70K triangles; the poles of its lat-long sphere put up to 75 keys in one
+    fine bin), the Sponza substitute (262K; a 2048-key bucket against a mean
+    of 256, 32-key bins) and a soup with a 398-key bin take the gather's
+    radix path for their hot buckets (gather_radix_sort), bit-exact.  Runs
+    of 300 identical keys (duplicated triangles) flag the scene, which moves
+    on to the MSB bucket sort (BuildBufs::gather_off).  Every build equals
+    the oracle."""
+    t = _clustered_tris(oracle, scene)
     exp = oracle.build(t)
     kinds = []
     with R.Scene.from_soup(t) as s:
@@ -389,7 +402,7 @@ def test_clustered_bins_move_to_msb(R, oracle, scene):
             assert np.array_equal(got["keys"], exp["keys"])
             assert np.array_equal(got["vals"], exp["vals"])
             assert np.array_equal(got["nodes"].view(np.uint32), exp["nodes"].view(np.uint32))
-    assert kinds == [1, 1, 1], kinds
+    assert kinds == [kind] * 3, kinds
 
 
 def test_build_repeat_and_rebuild(R, oracle):

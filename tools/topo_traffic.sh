@@ -11,7 +11,7 @@ mkdir -p gpurun_out
 for n in 1000000 10000000; do
   for lib in librtamd.so exp/gseq.so; do
     tag=$(basename $lib .so)_$n
-    for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
+    for pass in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum" "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum"; do
       p=$(echo $pass | cut -d' ' -f1)
       out=gpurun_out/tt_${tag}_$p
       timeout -k 10 -s KILL 240 rocprofv3 --pmc $pass --output-format csv -d $out -- \
