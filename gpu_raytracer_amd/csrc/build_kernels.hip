@@ -377,6 +377,9 @@ static_assert(kSortTile <= 4096, "tile-local indices are 12 bits");
 #ifndef RT_K1_REVERSE
 #define RT_K1_REVERSE 1
 #endif
+#ifndef RT_K1_AGG
+#define RT_K1_AGG 1  // r06: wave-aggregated bucket atomics for the first lane's bucket (clustered tiles)
+#endif
 #ifndef RT_K1TB_HALVES
 #define RT_K1TB_HALVES 1  // 10M: K1 157 -> 126 us (66 instead of 106 VGPRs); 1M (fused) unchanged
 #endif
@@ -521,7 +524,19 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
 #pragma unroll
             for (int c = 0; c < 3; ++c) qq[c] = quant((bmin[c] + bmax[c]) * 0.5f, p.lo[c], p.inv[c]);
             k8[q] = expand10(qq[0]) * 4u + expand10(qq[1]) * 2u + expand10(qq[2]);
+#if RT_K1_AGG
+            {  // the lanes sharing the first lane's bucket count once (one LDS atomic)
+                const bool ok = (okm >> q) & 1u;
+                const uint32_t bk = k8[q] >> kMsbShift;  // 30-bit keys: bucket < 1024
+                const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk);
+                const uint64_t peers = __ballot(ok && bk == b0);
+                if (ok && bk != b0) atomicAdd(&s_start[bk], 1u);
+                else if (peers && lane == (uint32_t)__ffsll((long long)peers) - 1)
+                    atomicAdd(&s_start[b0], (uint32_t)__popcll(peers));
+            }
+#else
             if ((okm >> q) & 1u) atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);  // 30-bit keys: bucket < 1024
+#endif
         }
     }
     __syncthreads();
@@ -540,11 +555,30 @@ __global__ __launch_bounds__(NT, FUSED ? 1 : RT_K1U_WAVES) void k_morton_tb(cons
     __syncthreads();  // every start read: the starts become the bucket cursors
     if (FUSED) RT_STAMP_HI(5);  // scan + table
 #pragma unroll
-    for (uint32_t q = 0; q < TPT; ++q)
+    for (uint32_t q = 0; q < TPT; ++q) {
+#if RT_K1_AGG
+        // clustered geometry puts a wave's 64 consecutive triangles in few
+        // buckets, and same-address LDS atomics serialise: the lanes sharing
+        // the first lane's bucket take one cursor range (any order within a
+        // bucket is fine: k_bucket_gather sorts by (key, index))
+        const bool ok = (okm >> q) & 1u;
+        const uint32_t bk = k8[q] >> kMsbShift;
+        const uint32_t b0 = __builtin_amdgcn_readfirstlane(bk);
+        const uint64_t peers = __ballot(ok && bk == b0);
+        const uint32_t lead = peers ? (uint32_t)__ffsll((long long)peers) - 1 : 0u;
+        uint32_t pos = 0;
+        if (ok && bk != b0) pos = atomicAdd(&s_start[bk], 1u);
+        else if (peers && lane == lead) pos = atomicAdd(&s_start[b0], (uint32_t)__popcll(peers));
+        const uint32_t base = (uint32_t)__shfl((int)pos, (int)lead, 64);
+        if (ok && bk == b0) pos = base + sort_count_below(peers);
+        if (ok) s_word[pos] = (k8[q] << 12) | (w * 64u * TPT + q * 64u + lane);  // key bits 0..19, index
+#else
         if ((okm >> q) & 1u) {
             const uint32_t pos = atomicAdd(&s_start[k8[q] >> kMsbShift], 1u);
             s_word[pos] = (k8[q] << 12) | (w * 64u * TPT + q * 64u + lane);  // key bits 0..19, index
         }
+#endif
+    }
     __syncthreads();
     if (FUSED) RT_STAMP_HI(6);  // LDS scatter
     const uint32_t trem = n - tbase;

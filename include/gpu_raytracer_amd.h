@@ -363,8 +363,9 @@ rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
  * bucket gathers its runs and sorts them in LDS), 1 = the r01-r03 MSB
  * scatter + bucket sort, 0 = the 4-pass LSB radix sort; a scene whose first
  * build finds a bucket beyond one block's LDS sort keeps the LSB sort, and
- * one whose gather probe finds clustered bins or a skewed bucket moves on
- * to the MSB sort.  "build.fuse_k01" 1 (default) / 0: with the gather sort,
+ * one whose gather probe finds a run of more than 64 identical keys
+ * (duplicated triangles) moves on to the MSB sort; clustered bins stay on
+ * the gather sort, whose blocks sort such buckets by LDS radix passes.  "build.fuse_k01" 1 (default) / 0: with the gather sort,
  * K0 (bounds) and K1 (Morton) as one launch whose blocks meet at a grid
  * barrier, when every sort tile's block fits the device at once (n up to
  * ~1M) and no other such build runs on the device; else two launches.  2

@@ -17,8 +17,9 @@ from oracle import oracle as O  # noqa: E402
 def scene_tris(name):
     if name in ("bunny", "sponza"):
         return np.ascontiguousarray(S.tris_for(name), np.float32).reshape(-1, 9)
-    if name == "soup70k":
-        return O.soup(70000, 2).reshape(-1, 9)
+    if name.startswith("soup"):  # soup70k, soup1m, ...
+        k = name[4:].lower()
+        return O.soup(int(float(k[:-1]) * (1000 if k.endswith("k") else 1000000)), 2).reshape(-1, 9)
     rng = np.random.default_rng(7)
     if name == "hot":  # a uniform soup plus 1500 small triangles crowded into a cube of side 0.01
         t = O.soup(60000, 3).reshape(-1, 9)
