@@ -849,7 +849,7 @@ __device__ __forceinline__ void gather_radix_sort(const uint32_t (&key)[P], cons
     uint32_t* s_cnt = s_dyn + 2 * CAP + NW * kMsbBuckets;
     uint32_t* s_sw = s_cnt + kMsbBuckets;
     const uint32_t tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-    const uint32_t per = (m + NT - 1) / NT;
+    const uint32_t per = __builtin_amdgcn_readfirstlane((m + NT - 1) / NT);
     uint32_t k[P], v[P], dg[P], r[P];
     bool ok[P];
 #pragma unroll
@@ -871,42 +871,54 @@ __device__ __forceinline__ void gather_radix_sort(const uint32_t (&key)[P], cons
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < P; ++i) {  // the next pass reads in ranking order
+            // q < CAP for every item (per <= P): unconditional reads, all in
+            // flight together (a read under `if (ok)` waited item by item)
             const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
             ok[i] = (uint32_t)i < per && q < m;
-            if (ok[i]) {
-                k[i] = s_rk[q];
-                v[i] = s_rv[q];
-            }
+            k[i] = s_rk[q];
+            v[i] = s_rv[q];
         }
+#ifdef RT_GDIAG
+        if (shift) RT_STAMP(4);  // diagnostic: both passes, then the tie loop, then the barrier
+#else
         RT_STAMP(4 + shift / 10);  // diagnostic builds only
+#endif
     }
     // sorted by key; each element's place in its identical-key run by index.
     // Both neighbours first (all 2P reads in flight): a lone key stays put
     bool tie[P];
+    uint32_t c[P];
 #pragma unroll
     for (int i = 0; i < P; ++i) {
         const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
-        const uint32_t pv = ok[i] && q > 0 ? s_rk[q - 1] : ~k[i];
-        const uint32_t nx = ok[i] && q + 1 < m ? s_rk[q + 1] : ~k[i];
-        tie[i] = ok[i] && (pv == k[i] || nx == k[i]);
+        const uint32_t pv = s_rk[q ? q - 1 : 0u];
+        const uint32_t nx = s_rk[q + 1 < CAP ? q + 1 : q];
+        tie[i] = ok[i] && ((q > 0 && pv == k[i]) || (q + 1 < m && nx == k[i]));
+        c[i] = q;
     }
     bool longrun = false;
 #pragma unroll
-    for (int i = 0; i < P; ++i) {
-        const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
-        if (!ok[i]) continue;
-        uint32_t c = q;
+    for (int i = 0; i < P; ++i)
         if (tie[i]) {
+            const uint32_t q = c[i];
             uint32_t a = q, e = q + 1;
             while (a > 0 && s_rk[a - 1] == k[i]) --a;
             while (e < m && s_rk[e] == k[i]) ++e;
-            c = a;
-            for (uint32_t x = a; x < e; ++x) c += s_rv[x] < v[i] ? 1u : 0u;
+            uint32_t r = a;
+            for (uint32_t x = a; x < e; ++x) r += s_rv[x] < v[i] ? 1u : 0u;
+            c[i] = r;
             longrun |= e - a > kGatherBinFast;
         }
-        kout[s + q] = k[i];
-        vout[s + c] = v[i];
-    }
+#pragma unroll
+    for (int i = 0; i < P; ++i)
+        if (ok[i]) {
+            const uint32_t q = w * (64u * per) + (uint32_t)i * 64u + l;
+            kout[s + q] = k[i];
+            vout[s + c[i]] = v[i];
+        }
+#ifdef RT_GDIAG
+    RT_STAMP(5);
+#endif
     if (__syncthreads_or(longrun) && tid == 0) atomicOr(flags, 1u);
     RT_STAMP(6);
 }
