@@ -6,7 +6,7 @@
 set -e
 cd "$(dirname "$0")/../gpu_raytracer_amd"
 mkdir -p lib/exp build/exp
-FLAGS="--offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fPIC -std=c++17 -Wno-unused-function"
+FLAGS="--offload-arch=gfx950 -O3 -ffp-contract=off -fno-fast-math -fno-slp-vectorize -fPIC -std=c++17 -Wno-unused-function"
 while [ $# -gt 1 ]; do
   name=$1; defs=$2; shift 2
   for f in build_kernels sort_kernels trace_kernels; do
