@@ -2,11 +2,11 @@
 for each scene, 3 builds through the library $RT_LIB (default: in-tree) --
 keys, indices and nodes against the oracle, the sort kind of every build --
 then the median build time over 20 builds.
-usage: python tools/gather_check.py [scene ...]   (bunny sponza soup70k hot dup)"""
+usage: python tests/tools/gather_check.py [scene ...]   (bunny sponza soup70k hot dup)"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import gpu_raytracer_amd as R  # noqa: E402
