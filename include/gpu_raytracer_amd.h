@@ -326,7 +326,7 @@ rt_status rt_framebuffer_dump_ppm(const uint8_t* rgba, uint32_t w, uint32_t h, c
 rt_status rt_hits_dump(const rt_hit* hits, size_t count, const char* path);
 
 /* Tuning knobs (process-wide; 24 keys since r06, which removed the
- * measured-slower alternatives -- DESIGN.md "Knobs").  Trace:
+ * measured-slower alternatives -- DESIGN.md, "Round 6", item 5).  Trace:
  * "trace.variant" 0 = one thread per pixel, wide (4-ary) traversal over the
  * K7w records (default), 2 = one thread per pixel, binary traversal;
  * "trace.stack_cap" (1..18; 0 = all, the default: 14 for 4-ary records on
