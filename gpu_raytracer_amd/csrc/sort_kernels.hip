@@ -901,12 +901,44 @@ __device__ __forceinline__ void gather_radix_sort(const uint32_t (&key)[P], cons
     for (int i = 0; i < P; ++i)
         if (tie[i]) {
             const uint32_t q = c[i];
+            // a run within TW positions on either side is read in one round
+            // of (clamped) loads and ranked from registers; a longer run
+            // takes the scans below
+            constexpr int TW = 4;  // (2: Sponza -1.8 us, bunny +1.4; 4: both -1 to -1.4; profiles/gather_radix_r06.log)
+            uint32_t wk[2 * TW], wv[2 * TW];
+#pragma unroll
+            for (int o = 0; o < 2 * TW; ++o) {
+                const int off = o < TW ? o - TW : o - TW + 1;  // -TW..-1, 1..TW
+                const int x = (int)q + off;
+                const uint32_t xc = x < 0 ? 0u : (uint32_t)x >= m ? m - 1u : (uint32_t)x;
+                wk[o] = s_rk[xc];
+                wv[o] = s_rv[xc];
+            }
+            bool inl = true, inr = true;  // still inside the run going left / right
+            uint32_t r = 0, na = 0;  // smaller indices in the run; run members left of q
+#pragma unroll
+            for (int o = TW - 1; o >= 0; --o) {  // left: q-1, q-2, ...
+                const int x = (int)q - (TW - o);
+                inl = inl && x >= 0 && wk[o] == k[i];
+                na += inl ? 1u : 0u;
+                r += (inl && wv[o] < v[i]) ? 1u : 0u;
+            }
+#pragma unroll
+            for (int o = TW; o < 2 * TW; ++o) {  // right: q+1, q+2, ...
+                const uint32_t x = q + (uint32_t)(o - TW + 1);
+                inr = inr && x < m && wk[o] == k[i];
+                r += (inr && wv[o] < v[i]) ? 1u : 0u;
+            }
+            if (!inl && !inr) {
+                c[i] = q - na + r;
+                continue;
+            }
             uint32_t a = q, e = q + 1;
             while (a > 0 && s_rk[a - 1] == k[i]) --a;
             while (e < m && s_rk[e] == k[i]) ++e;
-            uint32_t r = a;
-            for (uint32_t x = a; x < e; ++x) r += s_rv[x] < v[i] ? 1u : 0u;
-            c[i] = r;
+            uint32_t r2 = a;
+            for (uint32_t x = a; x < e; ++x) r2 += s_rv[x] < v[i] ? 1u : 0u;
+            c[i] = r2;
             longrun |= e - a > kGatherBinFast;
         }
 #pragma unroll
