@@ -1137,14 +1137,26 @@ __global__ __launch_bounds__(NT) void k_bucket_gather(const uint32_t* __restrict
 #pragma unroll
     for (int i = 0; i < P; ++i) r[i] = 0;
     for (uint32_t k = 0; k < kmax; ++k) {
-        const uint32_t perU = __builtin_amdgcn_readfirstlane(per);
+        if constexpr (NT <= 512) {
+            // rows i < per (scalar branch), clamped reads in every lane: a
+            // step's reads in flight together (r06; the 10M shapes' 10-16 rows
+            // of ~2-key bins keep the exact reads, whose LDS traffic is lower)
+            const uint32_t perU = __builtin_amdgcn_readfirstlane(per);
 #pragma unroll
-        for (int i = 0; i < P; ++i)
-            if ((uint32_t)i < perU) {  // rows i < per (scalar branch), clamped reads in every lane: a step's reads in flight together (r06)
-                const uint32_t x = pos[i] + k;
-                const uint2 o = s_kv[x < CAP ? x : CAP - 1u];
-                r[i] += (k < len[i] && (o.x < key[i] || (o.x == key[i] && o.y < val[i]))) ? 1u : 0u;
-            }
+            for (int i = 0; i < P; ++i)
+                if ((uint32_t)i < perU) {
+                    const uint32_t x = pos[i] + k;
+                    const uint2 o = s_kv[x < CAP ? x : CAP - 1u];
+                    r[i] += (k < len[i] && (o.x < key[i] || (o.x == key[i] && o.y < val[i]))) ? 1u : 0u;
+                }
+        } else {
+#pragma unroll
+            for (int i = 0; i < P; ++i)
+                if (k < len[i]) {
+                    const uint2 o = s_kv[pos[i] + k];
+                    r[i] += (o.x < key[i] || (o.x == key[i] && o.y < val[i])) ? 1u : 0u;
+                }
+        }
     }
 #pragma unroll
     for (int i = 0; i < P; ++i) pos[i] += r[i];
