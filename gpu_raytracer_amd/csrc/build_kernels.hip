@@ -1525,8 +1525,32 @@ struct WEnt {
     Aabb box;
     uint32_t left, mx;  // topology (internal entries): left child, range end
 };
+// BF (r06, scenes up to kWentBfMaxN): branch-free, three 16-B loads from the
+// entry's record -- an internal node's 32 B (its second word read twice) or a
+// triangle record's 48 B -- so a round's two entries issue all their loads
+// together instead of each waiting inside its own lane-divergent branch
+// (the crossing stage -1 to -1.2 us from 70K to 1M); at 10M the stage is
+// bound by its random lines, and the extra leaf-path loads cost 4 us
+// (profiles/ab_went_bf_r06.log)
+constexpr uint32_t kWentBfMaxN = 1u << 22;
+template <bool BF>
 __device__ __forceinline__ WEnt went_load(const void* nodes, const float4* tri_s, uint32_t i, uint32_t L0) {
     WEnt e;
+    if constexpr (BF) {
+        const bool in = i < L0;
+        const float4* p = in ? reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)i * 32)
+                             : tri_s + (uint64_t)(i - L0) * 3;
+        const float4 A = p[0], B = p[1], C = p[in ? 1 : 2];
+        const float t[9] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w, C.x};
+        float lo[3], hi[3];
+        tri_bounds(t, lo, hi);
+        e.box.lo[0] = in ? A.x : lo[0]; e.box.lo[1] = in ? A.y : lo[1]; e.box.lo[2] = in ? A.z : lo[2];
+        e.box.hi[0] = in ? A.w : hi[0]; e.box.hi[1] = in ? B.x : hi[1]; e.box.hi[2] = in ? B.y : hi[2];
+        const uint32_t esc = __float_as_uint(B.w);
+        e.left = in ? __float_as_uint(B.z) : 0u;
+        e.mx = !in ? 0u : esc == RT_SENT ? L0 : esc >= L0 ? esc - L0 - 1 : esc - 1;
+        return e;
+    }
     if (i < L0) {
         const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const char*>(nodes) + (uint64_t)i * 32);
         const float4 A = p[0], B = p[1];
@@ -1543,7 +1567,7 @@ __device__ __forceinline__ WEnt went_load(const void* nodes, const float4* tri_s
     return e;
 }
 
-template <int W>
+template <int W, bool BF>
 __device__ __forceinline__ void wide_record_g(uint32_t X, const uint4& tx, const Aabb& bx, uint32_t L0,
                                               const void* __restrict__ nodes, const float4* __restrict__ tri_s,
                                               uint4* __restrict__ wnodes) {
@@ -1562,8 +1586,8 @@ __device__ __forceinline__ void wide_record_g(uint32_t X, const uint4& tx, const
     };
     uint32_t l, r;
     kids_of(tx, L0, l, r);
-    put(0, l, went_load(nodes, tri_s, l, L0));
-    put(1, r, went_load(nodes, tri_s, r, L0));
+    put(0, l, went_load<BF>(nodes, tri_s, l, L0));
+    put(1, r, went_load<BF>(nodes, tri_s, r, L0));
 #pragma unroll
     for (int i = 2; i < W; ++i) {
         node[i] = RT_SENT; el[i] = 0u; em[i] = 0u; ar[i] = 0.0f;
@@ -1589,7 +1613,7 @@ __device__ __forceinline__ void wide_record_g(uint32_t X, const uint4& tx, const
         }
         uint32_t c0, c1;
         kids_of(make_uint4(pl, 0u, 0u, pm), L0, c0, c1);
-        const WEnt e0 = went_load(nodes, tri_s, c0, L0), e1 = went_load(nodes, tri_s, c1, L0);
+        const WEnt e0 = went_load<BF>(nodes, tri_s, c0, L0), e1 = went_load<BF>(nodes, tri_s, c1, L0);
         // shift the entries after `best` one slot right, then put the two children at best, best + 1
 #pragma unroll
         for (int i = W - 1; i >= 1; --i) {
@@ -1615,7 +1639,7 @@ __device__ __forceinline__ void wide_record_g(uint32_t X, const uint4& tx, const
 
 // K7w records of the crossing internal nodes, once K6t has written their
 // boxes (every box such a record needs is then final in `nodes`).
-template <int W>
+template <int W, bool BF>
 __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ topo, const uint32_t* __restrict__ cross,
                                                     const uint32_t* __restrict__ cross_ctr, uint32_t cross_cap,
                                                     const void* __restrict__ nodes, const float4* __restrict__ tri_s,
@@ -1633,7 +1657,7 @@ __global__ __launch_bounds__(256) void k_wide_cross(const uint4* __restrict__ to
         const uint32_t X = cross[sh * cross_cap + (q - pre[sh])];
         if (X >= L0) continue;
         // the greedy cut, one record load per entry
-        wide_record_g<W>(X, topo[X], load_aabb_node(nodes, X), L0, nodes, tri_s, wnodes);
+        wide_record_g<W, BF>(X, topo[X], load_aabb_node(nodes, X), L0, nodes, tri_s, wnodes);
     }
 }
 
@@ -1808,12 +1832,15 @@ static hipError_t launch_cross(const BuildBufs& b, uint32_t n, uint32_t arity, h
         RT_KLAUNCH(k_refit_cross<0>, dim3(cross_grid(m, 256)), dim3(256), 0, s, b.topo, b.prebuf, b.sufbuf, b.table, m,
                            b.cross, b.zero + kZCrossCtr, cross_cap(m), b.nodes, n);
     }
-    if (arity == 8)
-        RT_KLAUNCH(k_wide_cross<8>, dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes);
-    else
-        RT_KLAUNCH(k_wide_cross<4>, dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross, b.zero + kZCrossCtr,
-                           cross_cap(m), b.nodes, b.tri_s, n, b.wnodes);
+#define RT_WCROSS(W, BF)                                                                                       \
+    RT_KLAUNCH((k_wide_cross<W, BF>), dim3(cross_grid(m, RT_WCROSS_GRID)), dim3(256), 0, s, b.topo, b.cross,      \
+               b.zero + kZCrossCtr, cross_cap(m), b.nodes, b.tri_s, n, b.wnodes)
+    const bool bf = n <= kWentBfMaxN;
+    if (arity == 8 && bf) RT_WCROSS(8, true);
+    else if (arity == 8) RT_WCROSS(8, false);
+    else if (bf) RT_WCROSS(4, true);
+    else RT_WCROSS(4, false);
+#undef RT_WCROSS
     return hipGetLastError();
 }
 
