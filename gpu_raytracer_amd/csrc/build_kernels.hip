@@ -1225,6 +1225,7 @@ __global__ __launch_bounds__(kRefitT) void k_topo_refit(const uint32_t* __restri
         // topology words stay in registers/LDS: only the crossing nodes' go to
         // global memory (step 2), for k_refit_cross / k_wide_cross
         if (valid) karras_node_leaf(keys, lt, n, k, nullptr, parent, nodes, tri_s, tp, box, true, deferred, false, bstart);
+        RT_STAMP(6);  // diagnostic builds: the own node and leaf done (the wave searches follow)
         karras_wave_search(keys, n, k, deferred, nullptr, parent, tp);
     }
     s_box[tid] = box;

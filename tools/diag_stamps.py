@@ -33,6 +33,11 @@ def report(name, st, phases, nslots):
     for i, ph in enumerate(phases):
         d = (st[:, i + 1] - st[:, i]) / 100.0
         print(f"   {ph:<28s} median {np.median(d):7.2f}  p90 {np.percentile(d, 90):7.2f}  max {d.max():7.2f} us")
+    if os.environ.get("SLOW"):  # the slowest blocks: start, phases (us)
+        tot = st[:, nslots - 1] - st[:, 0]
+        for b in np.argsort(-tot)[:int(os.environ["SLOW"])]:
+            ph = " ".join(f"{(st[b, i + 1] - st[b, i]) / 100:6.2f}" for i in range(len(phases)))
+            print(f"   block {b:6d} start {(st[b, 0] - t0) / 100:6.2f} total {tot[b] / 100:6.2f}: {ph}")
 
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
@@ -51,8 +56,12 @@ if n <= 1_048_576 and s.build_times().fused_k01:  # the fused K0 + K1 (its recor
     report("k_morton_tb<fused>", allst[65536:65536 + T, :8],
            ["loads+partial box", "barrier (+ last block's reduction)", "box read", "keys+LDS histogram",
             "scan+table", "cursor scatter (LDS)", "word stores"], 8)
-report("k_topo_refit", stamps(M)[:, :6], ["key window+sync", "topology+leaf (thread 0)", "scans+flags+sync",
-                                          "sparse-table sweep+sync", "node+K7w stores"], 6)
+st_tr = stamps(M)
+report("k_topo_refit", st_tr[:, :6], ["key window+sync", "topology+leaf (thread 0)", "scans+flags+sync",
+                                      "sparse-table sweep+sync", "node+K7w stores"], 6)
+own, ws = (st_tr[:, 6] - st_tr[:, 1]) / 100.0, (st_tr[:, 2] - st_tr[:, 6]) / 100.0
+print(f"   wave 0's own node + leaf     median {np.median(own):7.2f}  p90 {np.percentile(own, 90):7.2f}  max {own.max():7.2f} us")
+print(f"   wave 0's wave-wide searches  median {np.median(ws):7.2f}  p90 {np.percentile(ws, 90):7.2f}  max {ws.max():7.2f} us")
 if os.environ.get("BT_SCENE") or os.environ.get("NO_SORT"):
     sys.exit(0)
 keys = np.random.default_rng(0).integers(0, 2**30, n, dtype=np.uint64).astype(np.uint32)
